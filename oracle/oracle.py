@@ -1,0 +1,249 @@
+"""CPU oracle for the nrk hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker (or the
+timed CPU baseline).  The product path (``nrk``) never imports it and fails
+loudly when its HIP library is missing.
+
+Each function restates the reference (file:line cited) in numpy / C:
+
+* ``ip_topk``            -- faiss.IndexFlatIP contract, youtubednn_recaller.py:493-494, :520
+* ``youtubednn_recall``  -- YoutubeDNNRecaller.recall, youtubednn_recaller.py:497-535
+* ``tower_user``         -- YoutubeDNN.forward + _extract_embeddings re-norm, :129-178, :467-470
+* ``tower_item``         -- get_item_embedding + re-norm, :184-188, :485-489
+* ``itemcf_sim``         -- ItemCFSimilarity.calculate, item_cf.py:17-89
+* ``itemcf_topn``        -- ItemCFRecaller._precompute_topk_similar_items, itemcf_recaller.py:41-54
+* ``itemcf_recall``      -- ItemCFRecaller.recall, itemcf_recaller.py:56-129
+* ``din_forward``        -- Dice / ActivationUnit / DINModel.forward, DIN.py:29-286
+
+Pinning: tests/test_oracle_golden.py checks every function against the golden
+fixtures produced by executing the reference (tests/golden/make_golden.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "libnrk_oracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        i64, i32, f64 = ctypes.c_int64, ctypes.c_int32, ctypes.c_double
+        L.oracle_ip_topk.argtypes = [P, i64, P, i64, ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_int]
+        L.oracle_ip_topk.restype = None
+        L.oracle_itemcf_sim.argtypes = [i64, P, P, P, P, i32, f64, f64, f64, f64, f64, i64, P, P, P, P, P]
+        L.oracle_itemcf_sim.restype = i64
+        L.oracle_topn_rows.argtypes = [i64, P, P, P, ctypes.c_int, P, P, P]
+        L.oracle_topn_rows.restype = None
+        L.oracle_itemcf_recall.argtypes = [i64, P, P, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int,
+                                           ctypes.c_int, f64, f64, i32, P, P, P]
+        L.oracle_itemcf_recall.restype = None
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# --------------------------------------------------------------------------
+# Recall: exact top-K and the recall() wrapper
+# --------------------------------------------------------------------------
+def ip_topk(users, items, k, nthreads=0, exact=False):
+    """Top-k rows of ``items`` by exact inner product with each user row.
+
+    Returns (scores f32 [nu,k], rows i64 [nu,k]) (+ fp64 exact scores)."""
+    users = np.ascontiguousarray(users, dtype=np.float32)
+    items = np.ascontiguousarray(items, dtype=np.float32)
+    nu, d = users.shape
+    ni = items.shape[0]
+    s = np.empty((nu, k), np.float32)
+    r = np.empty((nu, k), np.int64)
+    e = np.empty((nu, k), np.float64) if exact else None
+    lib().oracle_ip_topk(_p(users), nu, _p(items), ni, d, k, _p(s), _p(r),
+                         _p(e) if exact else None, int(nthreads))
+    return (s, r, e) if exact else (s, r)
+
+
+def youtubednn_recall(scores, rows, user_rawid_2_index, item_index_2_rawid, user_ids, topk):
+    """YoutubeDNNRecaller.recall over a precomputed (k+1) search result.
+
+    Drops rank 0 (:524), maps Faiss row r -> item_index_2_rawid[r] (:528-529,
+    the A3 quirk), skips labels not in the mapping, unknown users -> []."""
+    out = {}
+    for u in user_ids:
+        idx = user_rawid_2_index.get(u)
+        if idx is None or idx >= scores.shape[0]:
+            out[u] = []
+            continue
+        res = []
+        for i in range(1, scores.shape[1]):
+            r = int(rows[idx, i])
+            if r in item_index_2_rawid:
+                res.append((item_index_2_rawid[r], float(scores[idx, i])))
+            if len(res) >= topk:
+                break
+        out[u] = res
+    return out
+
+
+# --------------------------------------------------------------------------
+# Two-tower forward (fp32, numpy)
+# --------------------------------------------------------------------------
+def tower_user(user_emb, item_emb, uid, hist, hist_len, w0, b0, w1, b1):
+    f32 = np.float32
+    ue = user_emb[uid].astype(f32)
+    he = item_emb[hist].astype(f32)
+    T = hist.shape[1]
+    mask = (np.arange(T)[None, :] < hist_len[:, None]).astype(f32)[:, :, None]
+    avg = (he * mask).sum(1, dtype=f32) / (hist_len.astype(f32)[:, None] + f32(1e-8))
+    x = np.concatenate([ue, avg.astype(f32)], 1)
+    x = np.maximum(x @ w0.T.astype(f32) + b0.astype(f32), 0).astype(f32)
+    x = np.maximum(x @ w1.T.astype(f32) + b1.astype(f32), 0).astype(f32)
+    n = np.maximum(np.sqrt((x * x).sum(1, keepdims=True, dtype=f32)), f32(1e-12))
+    x = (x / n).astype(f32)
+    n2 = np.linalg.norm(x, axis=1, keepdims=True)
+    n2[n2 == 0] = 1
+    return (x / n2).astype(f32)
+
+
+def tower_item(item_emb, ids):
+    f32 = np.float32
+    x = item_emb[ids].astype(f32)
+    n = np.maximum(np.sqrt((x * x).sum(1, keepdims=True, dtype=f32)), f32(1e-12))
+    x = (x / n).astype(f32)
+    return (x / np.linalg.norm(x, axis=1, keepdims=True)).astype(f32)
+
+
+# --------------------------------------------------------------------------
+# ItemCF
+# --------------------------------------------------------------------------
+LOC_ALPHA, LOC_ALPHA_REV, LOC_BETA, TIME_ALPHA, CREATED_ALPHA = 1.0, 0.7, 0.9, 0.7, 0.8
+
+
+def itemcf_sim(offsets, items, ts, created, n_items):
+    """Dense-id ItemCF similarity.  Returns (i, j, v, row_rank, cnt) with the
+    (i, j) entries in global first-insertion order."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    items = np.ascontiguousarray(items, np.int32)
+    ts = np.ascontiguousarray(ts, np.int64)
+    created = np.ascontiguousarray(created, np.float64)
+    L = np.diff(offsets)
+    cap = int((L * L).sum()) + 1
+    oi = np.empty(cap, np.int32)
+    oj = np.empty(cap, np.int32)
+    ov = np.empty(cap, np.float64)
+    rank = np.empty(n_items, np.int64)
+    cnt = np.empty(n_items, np.int64)
+    n = lib().oracle_itemcf_sim(len(offsets) - 1, _p(offsets), _p(items), _p(ts), _p(created),
+                                n_items, LOC_ALPHA, LOC_ALPHA_REV, LOC_BETA, TIME_ALPHA,
+                                CREATED_ALPHA, cap, _p(oi), _p(oj), _p(ov), _p(rank), _p(cnt))
+    assert n >= 0
+    return oi[:n], oj[:n], ov[:n], rank, cnt
+
+
+def sim_to_rows(i, j, v, n_items):
+    """Group first-insertion-ordered entries into CSR rows (insertion order kept)."""
+    order = np.argsort(i, kind="stable")
+    off = np.zeros(n_items + 1, np.int64)
+    np.add.at(off, i + 1, 1)
+    return np.cumsum(off), j[order].astype(np.int32), v[order]
+
+
+def itemcf_topn(row_off, cols, vals, topn=20):
+    n_rows = len(row_off) - 1
+    oc = np.full((n_rows, topn), -1, np.int32)
+    ov = np.zeros((n_rows, topn), np.float64)
+    cnt = np.zeros(n_rows, np.int32)
+    lib().oracle_topn_rows(n_rows, _p(np.ascontiguousarray(row_off, np.int64)),
+                           _p(np.ascontiguousarray(cols, np.int32)),
+                           _p(np.ascontiguousarray(vals, np.float64)), topn, _p(oc), _p(ov), _p(cnt))
+    return oc, ov, cnt
+
+
+def itemcf_recall(q_slot, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created, hot, topk, n_items):
+    q_slot = np.ascontiguousarray(q_slot, np.int64)
+    nq = len(q_slot)
+    topn = nbr_cols.shape[1]
+    oi = np.zeros((nq, topk), np.int32)
+    os_ = np.zeros((nq, topk), np.float64)
+    oc = np.zeros(nq, np.int32)
+    hot = np.ascontiguousarray(hot, np.int32)
+    lib().oracle_itemcf_recall(nq, _p(q_slot), _p(np.ascontiguousarray(offsets, np.int64)),
+                               _p(np.ascontiguousarray(items, np.int32)),
+                               _p(np.ascontiguousarray(nbr_cols, np.int32)),
+                               _p(np.ascontiguousarray(nbr_vals, np.float64)),
+                               _p(np.ascontiguousarray(nbr_cnt, np.int32)), topn,
+                               _p(np.ascontiguousarray(created, np.float64)), _p(hot), len(hot),
+                               topk, LOC_BETA, CREATED_ALPHA, n_items, _p(oi), _p(os_), _p(oc))
+    return oi, os_, oc
+
+
+# --------------------------------------------------------------------------
+# DIN (fp32 numpy restatement of DIN.py:29-286)
+# --------------------------------------------------------------------------
+def _dice(x):
+    f32 = np.float32
+    x = x.astype(f32)
+    mean = x.mean(0, keepdims=True, dtype=np.float64).astype(f32)
+    std = x.astype(np.float64).std(0, ddof=1, keepdims=True).astype(f32)
+    xn = (x - mean) / (std + f32(1e-8))
+    p = (1.0 / (1.0 + np.exp(-xn.astype(np.float64)))).astype(f32)
+    return (p * x + (f32(1) - p) * f32(0.01) * x).astype(f32)
+
+
+def din_forward(sd, user, item, hist, ctx, mask, feats, round_bf16=False):
+    """sd: DINModel state_dict as numpy; feats: (user_feats, item_feats, ctx_feats).
+
+    Returns (probs [B], logits [B], att [B,T]).  ``round_bf16`` rounds every
+    embedding table to bf16 first (storage-only bf16, fp32 math)."""
+    f32 = np.float32
+    uf, itf, cf = feats
+
+    def tab(group, f):
+        w = sd[f"{group}.{f}.weight"].astype(f32)
+        return bf16_round(w) if round_bf16 else w
+
+    U = np.concatenate([tab("user_profile_embedding_dict", f)[user[:, n]] for n, f in enumerate(uf)], 1)
+    Q = np.concatenate([tab("item_embedding_dict", f)[item[:, n]] for n, f in enumerate(itf)], 1)
+    K = np.concatenate([tab("item_embedding_dict", f)[hist[:, :, n]] for n, f in enumerate(itf)], 2)
+    C = np.concatenate([tab("context_embedding_dict", f)[ctx[:, n]] for n, f in enumerate(cf)], 1)
+    B, T, d = K.shape
+    q = np.broadcast_to(Q[:, None, :], (B, T, d))
+    X = np.concatenate([K, q, q - K, q * K], 2).astype(f32)
+    a0w, a0b = sd["activation_unit.mlp.0.weight"].astype(f32), sd["activation_unit.mlp.0.bias"].astype(f32)
+    a2w, a2b = sd["activation_unit.mlp.2.weight"].astype(f32), sd["activation_unit.mlp.2.bias"].astype(f32)
+    h = (X @ a0w.T + a0b).astype(f32)
+    h = _dice(h)
+    w = (h @ a2w.T + a2b).astype(f32)[:, :, 0]
+    w = (w * mask.astype(f32)).astype(f32)
+    wh = (w[:, :, None] * K).sum(1, dtype=f32)
+    x = np.concatenate([U, C, Q, wh], 1).astype(f32)
+    for li in (0, 2):
+        x = (x @ sd[f"mlp.{li}.weight"].astype(f32).T + sd[f"mlp.{li}.bias"].astype(f32)).astype(f32)
+        x = _dice(x)
+    logit = (x @ sd["mlp.4.weight"].astype(f32).T + sd["mlp.4.bias"].astype(f32)).astype(f32)[:, 0]
+    prob = (1.0 / (1.0 + np.exp(-logit.astype(np.float64)))).astype(f32)
+    return prob, logit, w
+
+
+def bf16_round(x):
+    """Round-to-nearest-even fp32 -> bf16 -> fp32 (finite inputs)."""
+    b = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    b = (b + 0x7FFF + ((b >> 16) & 1)) >> 16
+    return (b.astype(np.uint32) << 16).view(np.float32).reshape(np.shape(x))

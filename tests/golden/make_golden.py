@@ -1,0 +1,479 @@
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE.
+
+Runs only in the build container (it reads /root/reference, which does not
+exist on the GPU box).  The reference is pure Python; it is imported with two
+shims documented in SURVEY.md §8c:
+
+* ``faiss`` is not installed (pyproject.toml:21 pins faiss-cpu>=1.7.4, not
+  vendored).  A stand-in module provides ``IndexFlatIP`` restating the Faiss
+  contract: exact inner product (fp64, products accumulated sequentially over
+  the dimension), results sorted by score desc, ties -> lower row, labels -1 /
+  scores -FLT_MAX when k > ntotal.  Parity at that boundary is therefore
+  pinned to the restated contract, not to a Faiss binary.
+* ``RecallConfig`` / ``RankConfig`` get ``_project_root=<tmp>`` because their
+  ``__post_init__`` makes directories (config.py:60-71).
+
+Everything else -- ItemCFSimilarity.calculate, ItemCFRecaller.recall,
+YoutubeDNN / YoutubeDNNRecaller.train/_extract_embeddings/recall, DINModel,
+DINDataset, collate_fn -- is the reference's own code, executed unchanged.
+
+Usage:  python tests/golden/make_golden.py   (writes *.npz next to this file)
+"""
+from __future__ import annotations
+
+import os
+import random
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "news-recommendation-tc_amd"))
+REF = "/root/reference"
+
+FLT_MAX = np.float32(3.4028234663852886e38)
+
+
+class IndexFlatIP:
+    """Stand-in for faiss.IndexFlatIP (the contract, restated)."""
+
+    def __init__(self, d):
+        self.d = int(d)
+        self.xb = np.zeros((0, self.d), dtype=np.float32)
+
+    @property
+    def ntotal(self):
+        return self.xb.shape[0]
+
+    def add(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        self.xb = np.concatenate([self.xb, x], 0)
+
+    def search(self, q, k):
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        nq, n = q.shape[0], self.ntotal
+        D = np.full((nq, k), -FLT_MAX, dtype=np.float32)
+        I = np.full((nq, k), -1, dtype=np.int64)
+        xb64 = self.xb.astype(np.float64)
+        rows = np.arange(n)
+        for qi in range(nq):
+            s = np.zeros(n, dtype=np.float64)
+            for t in range(self.d):  # sequential accumulation over the dimension
+                s = s + np.float64(q[qi, t]) * xb64[:, t]
+            order = np.lexsort((rows, -s))[: min(k, n)]
+            D[qi, : len(order)] = s[order].astype(np.float32)
+            I[qi, : len(order)] = order
+        return D, I
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    fa = types.ModuleType("faiss")
+    fa.IndexFlatIP = IndexFlatIP
+    sys.modules["faiss"] = fa
+    import src.utils.config as cfg  # noqa: F401
+
+    return cfg
+
+
+def seed_all(s=23):
+    import torch
+
+    random.seed(s)
+    np.random.seed(s)
+    torch.manual_seed(s)
+
+
+# --------------------------------------------------------------------------
+# ItemCF (item_cf.py:17-89, itemcf_recaller.py:41-129)
+# --------------------------------------------------------------------------
+def gen_itemcf(tmp):
+    import pandas as pd
+    from nrk.data import synth
+    from src.utils.config import RecallConfig
+    from src.similarity.item_cf import ItemCFSimilarity
+    from src.recall.itemcf_recaller import ItemCFRecaller
+    from src.data.extractors import ItemFeatureExtractor, UserFeatureExtractor
+
+    n_users, n_items = 2000, 5000
+    log = synth.make_click_log(n_users=n_users, n_items=n_items, seed=7)
+    art = synth.make_articles(n_items, seed=7)
+    # raw ids that are not 0..n-1 so id handling is exercised
+    click_df = pd.DataFrame(
+        {
+            "user_id": log.user_id * 3 + 100,
+            "click_article_id": log.click_article_id * 7 + 11,
+            "click_timestamp": log.click_timestamp,
+        }
+    )
+    articles_df = pd.DataFrame(
+        {
+            "click_article_id": art.article_id * 7 + 11,
+            "category_id": art.category_id,
+            "words_count": art.words_count,
+            "created_at_ts": art.created_at_ts,
+        }
+    )
+    _, _, created = ItemFeatureExtractor.get_item_info_dict(articles_df)
+    hot = ItemFeatureExtractor.get_item_topk_click(click_df, k=50)
+    uit = UserFeatureExtractor.get_user_item_time_dict(click_df)
+
+    cfg = RecallConfig(_project_root=tmp)
+    sim = ItemCFSimilarity(cfg).calculate(click_df, created)
+
+    rows_i, si, sj, sv = [], [], [], []
+    for i, d in sim.items():
+        rows_i.append(i)
+        for j, v in d.items():
+            si.append(i)
+            sj.append(j)
+            sv.append(v)
+    cfg30 = RecallConfig(_project_root=tmp)
+    rec = ItemCFRecaller(cfg30, sim, created, uit, hot, emb_similarity_matrix={})
+    users = list(uit.keys()) + [-5, -6, 10**9]  # three unknown users (cold start)
+    res = rec.batch_recall(users, topk=30)
+    ru, ri, rs, roff = [], [], [], [0]
+    for u in users:
+        for it, sc in res[u]:
+            ri.append(it)
+            rs.append(sc)
+        ru.append(u)
+        roff.append(len(ri))
+    # user_item_time_dict as CSR (checks the host-side list builder)
+    uu, uoff, uitems, uts = [], [0], [], []
+    for u, lst in uit.items():
+        uu.append(u)
+        for it, ts in lst:
+            uitems.append(it)
+            uts.append(ts)
+        uoff.append(len(uitems))
+    cids = np.array(sorted(created.keys()), dtype=np.int64)
+    np.savez_compressed(
+        os.path.join(HERE, "itemcf_small.npz"),
+        click_user=click_df["user_id"].to_numpy(np.int64),
+        click_item=click_df["click_article_id"].to_numpy(np.int64),
+        click_ts=click_df["click_timestamp"].to_numpy(np.int64),
+        created_ids=cids,
+        created_vals=np.array([created[c] for c in cids], dtype=np.float64),
+        hot=np.array(hot, dtype=np.int64),
+        uit_users=np.array(uu, dtype=np.int64),
+        uit_offsets=np.array(uoff, dtype=np.int64),
+        uit_items=np.array(uitems, dtype=np.int64),
+        uit_ts=np.array(uts, dtype=np.int64),
+        sim_rows=np.array(rows_i, dtype=np.int64),
+        sim_i=np.array(si, dtype=np.int64),
+        sim_j=np.array(sj, dtype=np.int64),
+        sim_v=np.array(sv, dtype=np.float64),
+        recall_users=np.array(ru, dtype=np.int64),
+        recall_offsets=np.array(roff, dtype=np.int64),
+        recall_items=np.array(ri, dtype=np.int64),
+        recall_scores=np.array(rs, dtype=np.float64),
+        topk=np.int64(30),
+        sim_item_topk=np.int64(cfg30.itemcf_sim_item_topk),
+    )
+    print(f"itemcf_small: {len(si)} sim pairs, {len(users)} users recalled")
+
+
+# --------------------------------------------------------------------------
+# YouTubeDNN (youtubednn_recaller.py:86-535)
+# --------------------------------------------------------------------------
+def gen_youtubednn(tmp):
+    import pandas as pd
+    import torch
+    from nrk.data import synth
+    from src.utils.config import RecallConfig
+    from src.recall.youtubednn_recaller import YoutubeDNNRecaller
+
+    log = synth.make_click_log(n_users=1000, n_items=5000, seed=11)
+    rng = np.random.default_rng(11)
+    perm = rng.permutation(len(log))  # click_df row order != time order
+    click_df = pd.DataFrame(
+        {
+            "user_id": log.user_id[perm] * 5 + 3,
+            "click_article_id": log.click_article_id[perm] * 3 + 1,
+            "click_timestamp": log.click_timestamp[perm],
+        }
+    )
+    cfg = RecallConfig(
+        _project_root=tmp,
+        youtubednn_embedding_dim=32,
+        youtubednn_hidden_units=[64, 32],
+        youtubednn_negsample=2,
+    )
+    seed_all(23)
+    rec = YoutubeDNNRecaller(cfg)
+    torch.set_num_threads(8)
+    rec.train(click_df, epochs=1, batch_size=256, learning_rate=0.01)
+    m = rec.model
+    users = sorted(rec.user_rawid_2_index.keys()) + [-1]
+    res = rec.batch_recall(users, topk=30)
+    ri, rs, roff = [], [], [0]
+    for u in users:
+        for it, sc in res[u]:
+            ri.append(it)
+            rs.append(sc)
+        roff.append(len(ri))
+    n_items_enc = len(rec.item_index_2_rawid)
+    np.savez_compressed(
+        os.path.join(HERE, "youtubednn_small.npz"),
+        click_user=click_df["user_id"].to_numpy(np.int64),
+        click_item=click_df["click_article_id"].to_numpy(np.int64),
+        click_ts=click_df["click_timestamp"].to_numpy(np.int64),
+        user_emb=m.user_embedding.weight.detach().numpy(),
+        item_emb=m.item_embedding.weight.detach().numpy(),
+        w0=m.user_tower[0].weight.detach().numpy(),
+        b0=m.user_tower[0].bias.detach().numpy(),
+        w1=m.user_tower[3].weight.detach().numpy(),
+        b1=m.user_tower[3].bias.detach().numpy(),
+        user_embeddings=rec.user_embeddings.astype(np.float32),
+        item_embeddings=rec.item_embeddings.astype(np.float32),
+        user_index_2_rawid=np.array(
+            [rec.user_index_2_rawid[i] for i in range(len(rec.user_index_2_rawid))], np.int64
+        ),
+        item_index_2_rawid=np.array(
+            [rec.item_index_2_rawid[i] for i in range(n_items_enc)], np.int64
+        ),
+        recall_users=np.array(users, dtype=np.int64),
+        recall_offsets=np.array(roff, dtype=np.int64),
+        recall_items=np.array(ri, dtype=np.int64),
+        recall_scores=np.array(rs, dtype=np.float64),
+        topk=np.int64(30),
+        seq_max_len=np.int64(cfg.youtubednn_seq_max_len),
+    )
+    print(f"youtubednn_small: {len(users)} users, {n_items_enc} items")
+
+
+# --------------------------------------------------------------------------
+# Brute-force top-K incl. tie stress, through the real recall() (A4 + A5)
+# --------------------------------------------------------------------------
+def gen_topk(tmp):
+    from src.utils.config import RecallConfig
+    from src.recall.youtubednn_recaller import YoutubeDNNRecaller
+
+    rng = np.random.default_rng(5)
+    d, n_items, k = 32, 5000, 30
+
+    def unit(x):
+        x = x.astype(np.float32)
+        n = np.linalg.norm(x, axis=1, keepdims=True)
+        n[n == 0] = 1
+        return (x / n).astype(np.float32)
+
+    # set A: random unit vectors
+    items_a = unit(rng.standard_normal((n_items, d)))
+    users_a = unit(rng.standard_normal((512, d)))
+    # set B: tie stress -- duplicated rows, quantised vectors, all-zero users
+    base = unit(rng.standard_normal((64, d)))
+    items_b = base[rng.integers(0, 64, size=n_items)]  # heavy exact duplicates
+    q = rng.integers(-1, 2, size=(300, d)).astype(np.float32)
+    items_b[:300] = unit(q)  # quantised rows -> many equal scores
+    users_b = unit(rng.standard_normal((256, d)))
+    users_b[:32] = 0.0  # ReLU'd-to-zero users: every score ties at 0
+    users_b[32:96] = unit(rng.integers(-1, 2, size=(64, d)))
+    users_b[96:128] = base[rng.integers(0, 64, size=32)]
+
+    out = {}
+    for tag, users, items in (("a", users_a, items_a), ("b", users_b, items_b)):
+        idx = IndexFlatIP(d)
+        idx.add(items)
+        D, I = idx.search(users, k + 1)
+        rec = YoutubeDNNRecaller(RecallConfig(_project_root=tmp, youtubednn_embedding_dim=d))
+        rec.model = object()
+        rec.user_embeddings = users
+        rec.item_embeddings = items
+        rec.faiss_index = idx
+        rec.user_rawid_2_index = {1000 + u: u for u in range(len(users))}
+        # non-identity row->raw mapping exercises the A3 quirk
+        raw = rng.permutation(n_items).astype(np.int64) * 2 + 1
+        rec.item_index_2_rawid = {r: int(raw[r]) for r in range(n_items)}
+        uu = list(rec.user_rawid_2_index.keys()) + [7]
+        res = rec.batch_recall(uu, topk=k)
+        ri, rs, roff = [], [], [0]
+        for u in uu:
+            for it, sc in res[u]:
+                ri.append(it)
+                rs.append(sc)
+            roff.append(len(ri))
+        out.update(
+            {
+                f"{tag}_users": users,
+                f"{tag}_items": items,
+                f"{tag}_D": D,
+                f"{tag}_I": I.astype(np.int64),
+                f"{tag}_raw": raw,
+                f"{tag}_recall_users": np.array(uu, np.int64),
+                f"{tag}_recall_offsets": np.array(roff, np.int64),
+                f"{tag}_recall_items": np.array(ri, np.int64),
+                f"{tag}_recall_scores": np.array(rs, np.float64),
+            }
+        )
+    # k > ntotal: -1 labels / -FLT_MAX scores
+    idx = IndexFlatIP(d)
+    idx.add(items_a[:10])
+    D, I = idx.search(users_a[:4], 16)
+    out["small_D"], out["small_I"] = D, I
+    out["k"] = np.int64(k)
+    np.savez_compressed(os.path.join(HERE, "topk_small.npz"), **out)
+    print("topk_small: sets a (random) and b (tie stress)")
+
+
+# --------------------------------------------------------------------------
+# DIN (DIN.py:29-286, 289-520)
+# --------------------------------------------------------------------------
+USER_FEATS = ["user_click_count", "user_avg_time_gap", "device_group", "avg_click_time", "avg_word_count"]
+ITEM_FEATS = ["category_id", "article_popularity", "created_at_ts", "words_count"]
+CTX_FEATS = [
+    "score", "sim_1", "time_diff_1", "word_diff_1", "sim_2", "time_diff_2", "word_diff_2",
+    "sim_3", "time_diff_3", "word_diff_3", "sim_max", "sim_mean", "sim_min", "sim_std",
+    "item_user_sim", "recall_in_user_cat",
+]
+
+
+def gen_din(tmp):
+    import torch
+    from src.rank.DIN import DINModel
+
+    torch.set_num_threads(8)
+    uv = dict(zip(USER_FEATS, [38, 121, 7, 501, 91]))
+    iv = dict(zip(ITEM_FEATS, [51, 201, 509, 81]))
+    cv = {f: 12 for f in CTX_FEATS}
+    seed_all(23)
+    model = DINModel(uv, iv, cv, embedding_dim=32, attention_hidden_units=[36],
+                     mlp_hidden_units=[200, 80], activation="dice").eval()
+    sd = {k: v.detach().numpy() for k, v in model.state_dict().items()}
+
+    cap = {}
+    model.mlp.register_forward_hook(lambda m, i, o: cap.__setitem__("logit", o.detach()))
+    model.activation_unit.register_forward_hook(lambda m, i, o: cap.__setitem__("att", o.detach()))
+
+    rng = np.random.default_rng(29)
+    out = {f"sd::{k}": v for k, v in sd.items()}
+    T = 50
+    for tag, B in (("b512", 512), ("b4096", 4096), ("b37", 37)):
+        user = np.stack([rng.integers(0, uv[f], B) for f in USER_FEATS], 1)
+        item = np.stack([rng.integers(0, iv[f], B) for f in ITEM_FEATS], 1)
+        ctx = np.stack([rng.integers(0, cv[f], B) for f in CTX_FEATS], 1)
+        hl = rng.integers(1, T + 1, B)
+        hl[rng.random(B) < 0.2] = 0
+        mask = (np.arange(T)[None] < hl[:, None]).astype(np.float32)
+        hist = np.stack([rng.integers(0, iv[f], (B, T)) for f in ITEM_FEATS], 2)
+        hist = hist * (mask[:, :, None] > 0)
+        batch = {
+            "user_profile": {f: torch.from_numpy(user[:, n].astype(np.int64)) for n, f in enumerate(USER_FEATS)},
+            "recall_item": {f: torch.from_numpy(item[:, n].astype(np.int64)) for n, f in enumerate(ITEM_FEATS)},
+            "history_items": {f: torch.from_numpy(hist[:, :, n].astype(np.int64)) for n, f in enumerate(ITEM_FEATS)},
+            "context": {f: torch.from_numpy(ctx[:, n].astype(np.int64)) for n, f in enumerate(CTX_FEATS)},
+            "history_mask": torch.from_numpy(mask),
+        }
+        with torch.no_grad():
+            probs = model(batch).numpy()
+        out.update(
+            {
+                f"{tag}_user": user.astype(np.int16),
+                f"{tag}_item": item.astype(np.int16),
+                f"{tag}_ctx": ctx.astype(np.int16),
+                f"{tag}_hist": hist.astype(np.int16),
+                f"{tag}_mask": mask.astype(np.uint8),
+                f"{tag}_probs": probs.astype(np.float32),
+                f"{tag}_logits": cap["logit"].squeeze(-1).numpy().astype(np.float32),
+                f"{tag}_att": cap["att"].squeeze(-1).numpy().astype(np.float32),
+            }
+        )
+    out["user_feats"] = np.array(USER_FEATS)
+    out["item_feats"] = np.array(ITEM_FEATS)
+    out["ctx_feats"] = np.array(CTX_FEATS)
+    np.savez_compressed(os.path.join(HERE, "din_small.npz"), **out)
+    print("din_small: B in {512, 4096, 37}, T=50")
+
+
+def gen_din_encode(tmp):
+    """Host encoding A14: DINDataset + collate_fn (DIN.py:289-520)."""
+    import pandas as pd
+    import torch
+    from sklearn.preprocessing import LabelEncoder
+    from src.rank.DIN import DINDataset, collate_fn
+
+    rng = np.random.default_rng(31)
+    n_users, n_items, n_rows, T = 60, 150, 400, 30
+    users = [str(u) for u in range(1000, 1000 + n_users)]
+    items = [str(i) for i in range(5000, 5000 + n_items)]
+    upd = {
+        u: {f: float(np.round(rng.random() * 7, 1)) for f in USER_FEATS}
+        for u in users[: n_users - 5]  # 5 users without a profile -> all-zero row
+    }
+    ifd = {
+        it: {f: int(rng.integers(0, 12)) for f in ITEM_FEATS} for it in items[: n_items - 10]
+    }
+    uhd = {}
+    for u in users[5:]:  # 5 users without history
+        L = int(rng.integers(0, 45))
+        uhd[u] = [items[int(x)] for x in rng.integers(0, n_items, L)]
+    main = pd.DataFrame(
+        {
+            "user_id": [int(users[x]) for x in rng.integers(0, n_users, n_rows)],
+            "item_id": [int(items[x]) for x in rng.integers(0, n_items, n_rows)],
+            "label": rng.integers(0, 2, n_rows),
+        }
+    )
+    for f in CTX_FEATS:
+        main[f] = rng.integers(0, 10, n_rows).astype(float)
+        main.loc[rng.random(n_rows) < 0.05, f] = 99.0  # unseen bin -> 0
+    enc = {}
+    for f in USER_FEATS:
+        le = LabelEncoder()
+        le.fit(list({p[f] for p in upd.values()}))
+        enc[f] = le
+    for f in ITEM_FEATS:
+        le = LabelEncoder()
+        le.fit(list({p[f] for p in ifd.values()}))
+        enc[f] = le
+    fit_rows = main[main[CTX_FEATS[0]] != 99.0]
+    for f in CTX_FEATS:
+        le = LabelEncoder()
+        le.fit(fit_rows[f].fillna(0).astype(str))
+        enc[f] = le
+    ds = DINDataset(main, upd, ifd, uhd, USER_FEATS, ITEM_FEATS, CTX_FEATS, "label", enc)
+    b = collate_fn([ds[i] for i in range(len(ds))], seq_max_len=T)
+    out = {
+        "main_user": main["user_id"].to_numpy(np.int64),
+        "main_item": main["item_id"].to_numpy(np.int64),
+        "main_label": main["label"].to_numpy(np.int64),
+        "main_ctx": main[CTX_FEATS].to_numpy(np.float64),
+        "prof_users": np.array([int(u) for u in upd], np.int64),
+        "prof_vals": np.array([[upd[u][f] for f in USER_FEATS] for u in upd], np.float64),
+        "ifeat_items": np.array([int(i) for i in ifd], np.int64),
+        "ifeat_vals": np.array([[ifd[i][f] for f in ITEM_FEATS] for i in ifd], np.int64),
+        "hist_users": np.array([int(u) for u in uhd], np.int64),
+        "hist_offsets": np.cumsum([0] + [len(v) for v in uhd.values()]).astype(np.int64),
+        "hist_items": np.array([int(i) for v in uhd.values() for i in v], np.int64),
+        "T": np.int64(T),
+        "out_user": np.stack([b["user_profile"][f].numpy() for f in USER_FEATS], 1),
+        "out_item": np.stack([b["recall_item"][f].numpy() for f in ITEM_FEATS], 1),
+        "out_hist": np.stack([b["history_items"][f].numpy() for f in ITEM_FEATS], 2),
+        "out_ctx": np.stack([b["context"][f].numpy() for f in CTX_FEATS], 1),
+        "out_mask": b["history_mask"].numpy(),
+        "out_labels": b["labels"].numpy(),
+    }
+    for f in USER_FEATS + ITEM_FEATS + CTX_FEATS:
+        out[f"classes::{f}"] = np.array([str(c) for c in enc[f].classes_])
+    np.savez_compressed(os.path.join(HERE, "din_encode_small.npz"), **out)
+    print("din_encode_small: host encoding fixture")
+
+
+def main():
+    import_reference()
+    tmp = tempfile.mkdtemp(prefix="nrk_golden_")
+    gen_topk(tmp)
+    gen_itemcf(tmp)
+    gen_youtubednn(tmp)
+    gen_din(tmp)
+    gen_din_encode(tmp)
+
+
+if __name__ == "__main__":
+    main()
