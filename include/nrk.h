@@ -1,0 +1,185 @@
+/*
+ * nrk.h -- C ABI of libnrk.so, the MI355X-native recall + rank hot path.
+ *
+ * Every entry point:
+ *   - takes caller-owned DEVICE buffers (plain pointers + sizes, row-major,
+ *     contiguous) and an explicit HIP stream (hipStream_t passed as void*);
+ *   - is asynchronous on that stream, performs no hidden allocation, no host
+ *     synchronisation and no hipMalloc/hipMemcpy (graph-capturable); scratch
+ *     comes from a caller workspace sized by the matching *_bytes() query;
+ *   - returns NRK_OK (0) or an error code; nrk_last_error() gives a
+ *     thread-local message.  No C++ exception crosses the ABI.
+ *
+ * The reference (qiqiqicheng/news-recommendation-tc) is pure Python with no
+ * FFI of its own; each function below names the reference call site it
+ * replaces (paths relative to the reference root).  The Python plugins in
+ * news-recommendation-tc_amd/nrk bind these through ctypes; INTEGRATION.md
+ * shows the binding a reference maintainer would add.
+ */
+#ifndef NRK_H
+#define NRK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* nrk_stream_t; /* hipStream_t */
+
+#define NRK_OK 0
+#define NRK_EINVAL 1       /* bad argument (shape, null pointer, size)      */
+#define NRK_EHIP 2         /* HIP runtime error (launch / device)           */
+#define NRK_EUNSUPPORTED 3 /* configuration outside the compiled variants   */
+
+const char* nrk_last_error(void);
+int nrk_abi_version(void);
+
+/* ---------------------------------------------------------------------- */
+/* YouTubeDNN two-tower forward                                           */
+/* ---------------------------------------------------------------------- */
+
+/* User tower, eval mode.  Replaces YoutubeDNN.forward / get_user_embedding
+ * (src/recall/youtubednn_recaller.py:129-182) as driven by
+ * _extract_embeddings (:425-470), INCLUDING the host-side numpy
+ * re-normalisation with zero-norm -> 1 (:467-470):
+ *   x   = [E_u[uid] ; sum_{t<len} E_i[hist_t] / (len + 1e-8)]
+ *   x   = ReLU(W1 ReLU(W0 x + b0) + b1)          (dropout = identity)
+ *   out = renorm(x / max(||x||, 1e-12))
+ * dim in {16, 32, 64}; h0 <= 128; h1 == dim.  hist is [n, seq_len]. */
+int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* item_table,
+                    int64_t n_item_rows, int dim, const int32_t* uid, const int32_t* hist,
+                    const int32_t* hist_len, int64_t n, int seq_len, const float* w0,
+                    const float* b0, int h0, const float* w1, const float* b1, int h1,
+                    float* out, nrk_stream_t stream);
+
+/* Item tower.  Replaces get_item_embedding (:184-188) + numpy re-norm
+ * (:485-489): out[r] = renorm(normalize(E_i[ids[r]])). */
+int nrk_tt_item_fwd(const float* item_table, int64_t n_item_rows, int dim, const int32_t* ids,
+                    int64_t n, float* out, nrk_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Brute-force inner-product top-K (replaces faiss.IndexFlatIP)           */
+/* ---------------------------------------------------------------------- */
+
+/* Catalog = the "index": a bf16 copy of the item rows in MFMA-fragment
+ * order plus the max row norm.  Replaces faiss.IndexFlatIP(d).add(items)
+ * (youtubednn_recaller.py:493-494).  items stays the fp32 source of truth
+ * for exact rescoring and must outlive the catalog. */
+size_t nrk_ip_catalog_bytes(int64_t n_items, int dim);
+int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* catalog,
+                         nrk_stream_t stream);
+
+/* Exact top-k by inner product for every user row.  Replaces
+ * faiss_index.search(user_emb, topk + 1) (youtubednn_recaller.py:520) for a
+ * whole user batch at once.  Contract (same as IndexFlatIP): exact score
+ * (fp64 accumulation of the fp32 products), sorted by score desc, ties ->
+ * lower row; fewer than k items -> rows -1 / scores -FLT_MAX.
+ * out_rows are catalog rows + row_offset (global rows of a shard).
+ * out_exact (nullable) receives the fp64 scores used for ordering (the
+ * merge key for catalog-sharded runs).  k <= 40; dim <= 256. */
+size_t nrk_ip_topk_workspace_bytes(int64_t n_users, int64_t n_items, int dim, int k);
+int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const void* catalog,
+                int64_t n_items, int dim, int k, int64_t row_offset, float* out_scores,
+                int32_t* out_rows, double* out_exact, void* workspace, size_t workspace_bytes,
+                nrk_stream_t stream);
+
+/* The two phases of nrk_ip_topk, for callers that pipeline or time them:
+ * screen (bf16 MFMA scan -> per-user candidate band in the workspace) and
+ * finish (exact fp64 rescoring + ordering, exact fallback for overflowed
+ * users).  finish must follow screen on the same workspace. */
+int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
+                       int dim, int k, void* workspace, size_t workspace_bytes,
+                       nrk_stream_t stream);
+int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items, int64_t n_items,
+                       int dim, int k, int64_t row_offset, float* out_scores, int32_t* out_rows,
+                       double* out_exact, void* workspace, size_t workspace_bytes,
+                       nrk_stream_t stream);
+
+/* Merge n_lists per-shard top-k_in lists (fp64 exact scores + global rows,
+ * list l of user u at [l * list_stride + u * k_in]) into the top-k_out by
+ * (score desc, row asc).  New: the catalog-sharded multi-GPU merge
+ * (SURVEY.md §8e); n_lists * k_in <= 512. */
+int nrk_topk_merge(const double* in_exact, const int32_t* in_rows, int n_lists,
+                   int64_t list_stride, int64_t n_users, int k_in, int k_out, float* out_scores,
+                   int32_t* out_rows, double* out_exact, nrk_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* ItemCF co-occurrence similarity                                        */
+/* ---------------------------------------------------------------------- */
+
+/* Replaces ItemCFSimilarity.calculate (src/similarity/item_cf.py:17-89).
+ * Input: user click lists in CSR (users in ascending id order, each list in
+ * click-time order = UserFeatureExtractor.get_user_item_time_dict,
+ * src/data/extractors.py:10-36), dense item ids, raw ms timestamps, and the
+ * MinMax-scaled created time per dense item (float64).
+ * Pass 1 (nrk_itemcf_pair_offsets): per-user pair-slot offsets
+ * (pair_off[u] = sum_{v<u} L_v^2, pair_off[n_users] = total) -- the caller
+ * reads the total to size the workspace and outputs.
+ * Pass 2 (nrk_itemcf_sim): one entry per distinct (i, j), sorted by (i, j):
+ * normalised similarity (fp64, per-pair weights summed in the reference's
+ * order), first-encounter slot (the dict insertion order that the
+ * reference's stable sorts use as tie-break) and item_cnt per dense item.
+ * *out_n (device int64) receives the number of entries. */
+int nrk_itemcf_pair_offsets(const int64_t* offsets, int64_t n_users, int64_t* pair_off,
+                            nrk_stream_t stream);
+size_t nrk_itemcf_workspace_bytes(int64_t n_pairs, int32_t n_items);
+int nrk_itemcf_sim(const int64_t* offsets, int64_t n_users, const int32_t* items,
+                   const int64_t* ts, const double* created, int32_t n_items,
+                   const int64_t* pair_off, int64_t n_pairs, double loc_alpha,
+                   double loc_alpha_rev, double loc_beta, double time_alpha,
+                   double created_alpha, int32_t* out_i, int32_t* out_j, double* out_v,
+                   int64_t* out_first, int64_t* out_n, int64_t* out_cnt, void* workspace,
+                   size_t workspace_bytes, nrk_stream_t stream);
+
+/* Per-row top-n of the similarity CSR by (score desc, first-encounter asc):
+ * replaces ItemCFRecaller._precompute_topk_similar_items
+ * (src/recall/itemcf_recaller.py:41-54).  row_off has n_rows + 1 entries.
+ * Outputs [n_rows, topn] (-1 / 0 padded) and counts. topn <= 64. */
+int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
+                    const double* vals, const int64_t* first, int topn, int32_t* out_cols,
+                    double* out_vals, int32_t* out_cnt, nrk_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* DIN attention-over-history scorer                                      */
+/* ---------------------------------------------------------------------- */
+
+/* DINModel.forward (src/rank/DIN.py:214-286) in eval mode for one batch,
+ * as DINRanker.predict drives it (DIN.py:1219-1283).  Dice uses the batch
+ * statistics (mean, unbiased std over the batch, DIN.py:39-44), so a batch
+ * is the unit of work and the caller batches exactly like the reference.
+ *
+ * Embedding tables: all per-feature nn.Embedding(vocab, 32) tables
+ * concatenated row-wise into one table (fp32: table_dtype 0, bf16: 1);
+ * feature f's row r lives at row_base[f] + r.  Feature order: user features
+ * [0, n_user), item features [n_user, n_user + n_item) (shared by the
+ * candidate and the history), context features after them.
+ * Index tensors are int32: user [B, n_user], item [B, n_item],
+ * hist [B, T, n_item], ctx [B, n_ctx]; mask [B, T] float (1 valid, 0 pad).
+ * Weights (fp32, the state_dict tensors): att_w0 [36, 4*n_item*32],
+ * att_b0 [36], att_w1 [36], att_b1 [1]; mlp_w0 [h1, in], mlp_b0 [h1],
+ * mlp_w1 [h2, h1], mlp_b1 [h2], mlp_w2 [h2], mlp_b2 [1]
+ * with in = 32 * (n_user + n_ctx + 2 * n_item).
+ * nrk_din_prepare derives the batch-invariant attention matrices once per
+ * weight load into prep (nrk_din_prep_bytes).  B >= 2 (B = 1 is NaN in the
+ * reference too). */
+size_t nrk_din_prep_bytes(int n_item);
+int nrk_din_prepare(const float* att_w0, int n_item, void* prep, nrk_stream_t stream);
+size_t nrk_din_workspace_bytes(int64_t batch, int seq_len, int n_user, int n_item, int n_ctx,
+                               int h1, int h2);
+int nrk_din_forward(const void* table, int table_dtype, const int64_t* row_base, int n_user,
+                    int n_item, int n_ctx, const int32_t* user_idx, const int32_t* item_idx,
+                    const int32_t* hist_idx, const int32_t* ctx_idx, const float* mask,
+                    int64_t batch, int seq_len, const void* prep, const float* att_b0,
+                    const float* att_w1, const float* att_b1, const float* mlp_w0,
+                    const float* mlp_b0, int h1, const float* mlp_w1, const float* mlp_b1,
+                    int h2, const float* mlp_w2, const float* mlp_b2, float* out_probs,
+                    float* out_logits, void* workspace, size_t workspace_bytes,
+                    nrk_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NRK_H */

@@ -1,0 +1,782 @@
+// ip_topk.hip -- brute-force user x item inner-product top-K on gfx950.
+//
+// Replaces faiss.IndexFlatIP.add/.search (src/recall/youtubednn_recaller.py
+// :493-494, :520).  Contract (= IndexFlatIP): exact inner product, score desc,
+// ties -> lower row.  "Exact" is the fp64 sum of the fp32 products,
+// accumulated in dimension order (the oracle's definition, oracle/nrk_oracle.c).
+//
+// Design (MI355X-first, see DESIGN.md "ip_topk"):
+//   1. ip_screen   -- the one dense contraction on MFMA: fp16 32x32x16 tiles
+//      (power-of-two scaled, so the only error is fp16 rounding), items
+//      (A operand) streamed through LDS from a catalog pre-packed in
+//      fragment order, 32 users per wave (B operand) held in registers.
+//      Each lane owns one user x one 16-item half of every 32-item block.
+//      Per block the lane takes the max of its 16 scores; only when that
+//      beats the lane threshold tau does it append ONE entry (block max,
+//      block id) to its LDS list.  tau = theta - 2*eps, theta = K-th largest
+//      listed block max (a lower bound of the K-th largest score: K distinct
+//      blocks each hold an item >= theta), eps bounds |fp16 score - exact|
+//      (eps = c(D) * ||u|| * max_j ||v_j||).  A full list is compacted by a
+//      register bitonic sort (all lanes at once, no serial LDS chains).
+//   2. ip_refine   -- one wave per user: fp64 exact rescoring of every item
+//      of the flagged blocks, keep items with exact score >= cut + eps
+//      (typically K + a few), wave bitonic sort on (score desc, row asc).
+//   3. ip_fallback -- users whose candidate band overflowed (dense exact or
+//      near ties, e.g. duplicated catalog rows): exact fp64 radix-select over
+//      the whole catalog.  Never taken on non-degenerate data.
+#include "nrk_common.h"
+
+#include <float.h>
+
+namespace nrk {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int IP_CL = 64;          // per-lane candidate list capacity (LDS)
+constexpr int IP_CW = IP_CL - 16;  // entries kept per lane after the final flush
+constexpr int IP_KMAX = 40;
+constexpr int IP_USERS_PER_WG = 128;  // 4 waves x 32 users
+constexpr size_t CATALOG_HDR = 256;
+
+static inline int pad_dim(int d) {
+    return d <= 16 ? 16 : d <= 32 ? 32 : d <= 64 ? 64 : d <= 128 ? 128 : 256;
+}
+__host__ __device__ static inline int64_t n_blocks_of(int64_t n_items) { return (n_items + 31) / 32; }
+
+// Catalog header (after the packed blocks).
+struct CatalogHdr {
+    float max_norm;  // max_j ||v_j||_2 (fp32)
+    float max_abs;   // max_j,d |v_jd|
+    float scale;     // power of two applied before the fp16 conversion
+    int32_t dim;
+    int32_t dp;
+};
+
+// 2^(14 - e) where m = f * 2^e, f in [0.5, 1): maps max |x| into [2^13, 2^14)
+__device__ __forceinline__ float pow2_scale(float maxabs) {
+    if (!(maxabs > 0.0f)) return 1.0f;
+    int e;
+    (void)frexpf(maxabs, &e);
+    return ldexpf(1.0f, 14 - e);
+}
+
+static inline size_t catalog_body_bytes(int64_t n_items, int dp) {
+    return (size_t)n_blocks_of(n_items) * 64u * (size_t)dp;
+}
+
+// --------------------------------------------------------- catalog build --
+// Thread -> one 16-byte fragment: block b, k-step s, lane l:
+//   8 bf16 of item 32b + (l & 31), dims 16s + 8(l >> 5) + [0, 8).
+__global__ void catalog_pack_kernel(const float* __restrict__ items, int64_t n_items, int dim,
+                                    int dp, const CatalogHdr* __restrict__ hdr,
+                                    uint4* __restrict__ out) {
+    const int ds = dp / 16;
+    const float scale = hdr->scale;
+    const int64_t total = n_blocks_of(n_items) * ds * 64;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(t & 63);
+        const int s = (int)((t >> 6) % ds);
+        const int64_t b = (t >> 6) / ds;
+        const int64_t item = b * 32 + (lane & 31);
+        const int d0 = 16 * s + 8 * (lane >> 5);
+        uint16_t v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int d = d0 + e;
+            const float f = (item < n_items && d < dim) ? items[item * dim + d] : 0.0f;
+            v[e] = __builtin_bit_cast(uint16_t, (_Float16)(f * scale));
+        }
+        uint4 o;
+        o.x = v[0] | ((uint32_t)v[1] << 16);
+        o.y = v[2] | ((uint32_t)v[3] << 16);
+        o.z = v[4] | ((uint32_t)v[5] << 16);
+        o.w = v[6] | ((uint32_t)v[7] << 16);
+        out[t] = o;
+    }
+}
+
+__global__ void catalog_norm_kernel(const float* __restrict__ items, int64_t n_items, int dim,
+                                    CatalogHdr* hdr) {
+    float m = 0.0f, a = 0.0f;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_items;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        float s = 0.0f;
+        for (int d = 0; d < dim; ++d) {
+            const float x = items[r * dim + d];
+            s += x * x;
+            a = fmaxf(a, fabsf(x));
+        }
+        m = fmaxf(m, sqrtf(s));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m = fmaxf(m, __shfl_xor(m, o, WAVE));
+        a = fmaxf(a, __shfl_xor(a, o, WAVE));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax((unsigned int*)&hdr->max_norm, __float_as_uint(m));
+        atomicMax((unsigned int*)&hdr->max_abs, __float_as_uint(a));
+    }
+}
+
+__global__ void catalog_hdr_kernel(CatalogHdr* hdr, int dim, int dp) {
+    hdr->dim = dim;
+    hdr->dp = dp;
+    hdr->scale = pow2_scale(hdr->max_abs);
+}
+
+// ------------------------------------------------------------- screening --
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float round_down_sub(float theta, float two_eps) {
+    float c = theta - two_eps;
+    return __uint_as_float(c > 0.0f ? __float_as_uint(c) - 1u
+                                    : (c == 0.0f ? 0x80000001u : __float_as_uint(c) + 1u));
+}
+
+// Register bitonic sort of 64 floats, descending (per lane, no cross-lane).
+__device__ __forceinline__ void sort64_desc(float (&x)[64]) {
+#pragma unroll
+    for (int kl = 1; kl <= 6; ++kl) {
+#pragma unroll
+        for (int jl = kl - 1; jl >= 0; --jl) {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) {
+                const int p = i ^ (1 << jl);
+                if (p > i) {
+                    const bool desc = ((i >> kl) & 1) == 0;
+                    const float a = x[i], b = x[p];
+                    const float hi = fmaxf(a, b), lo = fminf(a, b);
+                    x[i] = desc ? hi : lo;
+                    x[p] = desc ? lo : hi;
+                }
+            }
+        }
+    }
+}
+
+struct LaneList {
+    uint2* base;  // this wave's list area: entry j of lane at base[j * 64 + lane]
+    int lane;
+    __device__ __forceinline__ uint2 get(int j) const { return base[j * WAVE + lane]; }
+    __device__ __forceinline__ void put(int j, uint2 v) const { base[j * WAVE + lane] = v; }
+};
+
+// Compact every lane's list: theta = k-th largest listed block max,
+// keep entries >= theta - 2 eps (eps == 0: exactly the first k in list
+// order among ties -- the zero user, whose scores are exact).
+__device__ __forceinline__ void lanes_flush(const LaneList& L, int& n, float& tau, float& theta,
+                                            bool& ovf, int k, float eps, bool active) {
+    float sv[IP_CL];
+    uint32_t pv[IP_CL];
+    float x[IP_CL];
+#pragma unroll
+    for (int j = 0; j < IP_CL; ++j) {
+        const uint2 e = L.get(j);
+        const bool ok = active && j < n;
+        sv[j] = ok ? __uint_as_float(e.x) : -INFINITY;
+        pv[j] = e.y;
+        x[j] = sv[j];
+    }
+    if (!(active && n >= k)) return;
+    sort64_desc(x);
+    float th = x[0];
+    int gt = 0;
+#pragma unroll
+    for (int j = 1; j < IP_CL; ++j) th = (j == k - 1) ? x[j] : th;
+#pragma unroll
+    for (int j = 0; j < IP_CL; ++j) gt += (x[j] > th) ? 1 : 0;
+    const float cut = (eps == 0.0f) ? th : round_down_sub(th, 2.0f * eps);
+    const int eq_allow = k - gt;
+    int m = 0, eq_seen = 0;
+#pragma unroll
+    for (int j = 0; j < IP_CL; ++j) {
+        const float s = sv[j];
+        bool keep;
+        if (eps == 0.0f) {
+            keep = s > th || (s == th && eq_seen < eq_allow);
+            eq_seen += (s == th) ? 1 : 0;
+        } else {
+            keep = s >= cut;
+        }
+        if (keep && m < IP_CL - 1) {
+            L.put(m, make_uint2(__float_as_uint(s), pv[j]));
+            ++m;
+        } else if (keep) {
+            ovf = true;
+        }
+    }
+    n = m;
+    theta = th;
+    tau = ovf ? INFINITY : fmaxf(tau, cut);  // an overflowed user is redone exactly
+}
+
+template <int DP>
+__global__ __launch_bounds__(256, 1) void ip_screen_kernel(
+    const float* __restrict__ users, int64_t n_users, const uint8_t* __restrict__ catalog,
+    int64_t n_items, int dim, int k, uint2* __restrict__ cand, int32_t* __restrict__ cand_cnt,
+    float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
+    int32_t* __restrict__ ovf_count) {
+    constexpr int DS = DP / 16;
+    constexpr int BLOCK_BYTES = 64 * DP;
+    constexpr int TILE_BYTES = BLOCK_BYTES >= 8192 ? BLOCK_BYTES : 8192;
+    constexpr int TB = TILE_BYTES / BLOCK_BYTES;
+    constexpr int LPT = TILE_BYTES / (256 * 16);  // 16-B loads per thread per tile
+    constexpr int LIST_BYTES = 4 * IP_CL * WAVE * 8;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * TILE_BYTES + LIST_BYTES];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63, h = lane >> 5;
+    const int64_t user = (int64_t)blockIdx.x * IP_USERS_PER_WG + wave * 32 + (lane & 31);
+    const bool active = user < n_users;
+
+    const int64_t nblk = n_blocks_of(n_items);
+    const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk * BLOCK_BYTES);
+    const float vmax = hdr->max_norm;
+    const float sv_scale = hdr->scale;
+
+    // B operand: 32 users x DP dims, fp16 (scaled by a power of two); lane
+    // holds user (lane&31), dims 16s + 8h + [0, 8) for k-step s.
+    float uval[DS][8];
+    float nrm2 = 0.0f, uabs = 0.0f;
+#pragma unroll
+    for (int s = 0; s < DS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int d = 16 * s + 8 * h + e;
+            const float f = (active && d < dim) ? users[user * dim + d] : 0.0f;
+            uval[s][e] = f;
+            nrm2 += f * f;
+            uabs = fmaxf(uabs, fabsf(f));
+        }
+    nrm2 += __shfl_xor(nrm2, 32, WAVE);
+    uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
+    const float su = pow2_scale(uabs);
+    f16x8 ufrag[DS];
+#pragma unroll
+    for (int s = 0; s < DS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ufrag[s][e] = (_Float16)(uval[s][e] * su);
+    // |fp16 score - exact| <= (2^-10 + 2^-22 + (D-1) 2^-24 (1+2^-11)^2) ||u|| ||v||
+    // (+ subnormal terms, < 2^-30 relative after the power-of-two scaling).
+    const float ceps = 9.765625e-4f + 3.0517578e-5f + (float)DP * 1.1920929e-7f;
+    const float eps = (nrm2 == 0.0f) ? 0.0f : ceps * sqrtf(nrm2) * vmax * 1.0001f + 1e-30f;
+    const float scl = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
+    const float eps_s = eps * scl;
+
+    LaneList L{reinterpret_cast<uint2*>(smem + 2 * TILE_BYTES) + wave * IP_CL * WAVE, lane};
+    int n = 0;
+    float tau = -INFINITY, theta = -INFINITY;
+    bool ovf = false;
+
+    const int64_t ntile = (nblk + TB - 1) / TB;
+    const uint4* cat4 = reinterpret_cast<const uint4*>(catalog);
+    const int64_t body16 = nblk * (BLOCK_BYTES / 16);
+    uint4 stage[LPT];
+    auto load_tile = [&](int64_t t) {
+#pragma unroll
+        for (int q = 0; q < LPT; ++q) {
+            const int64_t idx = t * (TILE_BYTES / 16) + q * 256 + tid;
+            stage[q] = idx < body16 ? cat4[idx] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_tile = [&](int buf) {
+        uint4* dst = reinterpret_cast<uint4*>(smem + buf * TILE_BYTES);
+#pragma unroll
+        for (int q = 0; q < LPT; ++q) dst[q * 256 + tid] = stage[q];
+    };
+
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int64_t t = 0; t < ntile; ++t) {
+        if (t + 1 < ntile) load_tile(t + 1);
+        const uint8_t* buf = smem + (t & 1) * TILE_BYTES;
+#pragma unroll
+        for (int b = 0; b < TB; ++b) {
+            const int64_t blk = t * TB + b;
+            if (blk >= nblk) break;
+            f32x16 acc = {};
+#pragma unroll
+            for (int s = 0; s < DS; ++s) {
+                const uint4 av = *reinterpret_cast<const uint4*>(buf + (b * DS + s) * 1024 + lane * 16);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, av), ufrag[s], acc, 0, 0, 0);
+            }
+            const int64_t row0 = blk * 32;
+            if (row0 + 32 > n_items) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row >= n_items) acc[r] = -INFINITY;
+                }
+            }
+            float mx = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
+#pragma unroll
+            for (int r = 4; r < 16; r += 4)
+                mx = fmaxf(mx, fmaxf(fmaxf(acc[r], acc[r + 1]), fmaxf(acc[r + 2], acc[r + 3])));
+            if (__ballot(active && mx > tau)) {
+                if (__ballot(active && n >= IP_CL)) lanes_flush(L, n, tau, theta, ovf, k, eps_s, active);
+                if (active && mx > tau && n < IP_CL) {
+                    L.put(n, make_uint2(__float_as_uint(mx), (uint32_t)(blk * 2 + h)));
+                    ++n;
+                }
+            }
+        }
+        if (t + 1 < ntile) store_tile((t + 1) & 1);
+        __syncthreads();
+    }
+
+    lanes_flush(L, n, tau, theta, ovf, k, eps_s, active);
+    const float th_u = fmaxf(theta, __shfl_xor(theta, 32, WAVE));
+    const bool ovf_u = ovf || __shfl_xor((int)ovf, 32, WAVE);
+    if (!active) return;
+    float cut = th_u;
+    if (eps_s != 0.0f && th_u != -INFINITY) cut = round_down_sub(th_u, 2.0f * eps_s);
+    int m = 0;
+    uint2* dst = cand + (user * 2 + h) * IP_CW;
+    for (int j = 0; j < n; ++j) {
+        const uint2 e = L.get(j);
+        if (!(__uint_as_float(e.x) >= cut)) continue;
+        if (m < IP_CW) dst[m] = e;
+        ++m;
+    }
+    const bool ovf2 = ovf_u || (m > IP_CW) || __shfl_xor((int)(m > IP_CW), 32, WAVE);
+    cand_cnt[user * 2 + h] = m < IP_CW ? m : IP_CW;
+    if (h == 0) {
+        // unscaled cut and eps for the refinement (exact power-of-two rescale)
+        ucut[user] = make_float2(cut == -INFINITY ? -INFINITY : cut / scl, eps);
+        ovf_flag[user] = ovf2 ? 1 : 0;
+        if (ovf2) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)user;
+    }
+}
+
+// ------------------------------------------------------------ refinement --
+__device__ __forceinline__ double exact_dot(const float* __restrict__ a, const float* __restrict__ b,
+                                            int dim) {
+    double s = 0.0;
+    if ((dim & 3) == 0) {
+        const float4* a4 = reinterpret_cast<const float4*>(a);
+        const float4* b4 = reinterpret_cast<const float4*>(b);
+        for (int t = 0; t < dim / 4; ++t) {
+            const float4 x = a4[t], y = b4[t];
+            s += (double)x.x * (double)y.x;
+            s += (double)x.y * (double)y.y;
+            s += (double)x.z * (double)y.z;
+            s += (double)x.w * (double)y.w;
+        }
+    } else {
+        for (int t = 0; t < dim; ++t) s += (double)a[t] * (double)b[t];
+    }
+    return s + 0.0;
+}
+
+constexpr int IP_SURV = 128;  // exact survivors per user held by the refine
+
+__global__ __launch_bounds__(256) void ip_refine_kernel(
+    const float* __restrict__ users, int64_t n_users, const float* __restrict__ items,
+    int64_t n_items, int dim, int k, int64_t row_offset, const uint2* __restrict__ cand,
+    const int32_t* __restrict__ cand_cnt, const float2* __restrict__ ucut,
+    const int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
+    int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
+    double* __restrict__ out_e) {
+    __shared__ Cand surv[4][IP_SURV];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t u = (int64_t)blockIdx.x * 4 + wave;
+    if (u >= n_users || ovf_flag[u]) return;
+    const float* uv = users + u * dim;
+    // zero user: every score is exactly 0 -> the lowest rows win the ties
+    float nz = 0.0f;
+    for (int d = lane; d < dim; d += WAVE) nz += fabsf(uv[d]);
+    nz = wave_sum_f32(nz);
+    if (nz == 0.0f) {
+        if (lane < k) {
+            const bool ok = lane < n_items;
+            out_s[u * k + lane] = ok ? 0.0f : -FLT_MAX;
+            out_r[u * k + lane] = ok ? (int32_t)(lane + row_offset) : -1;
+            if (out_e) out_e[u * k + lane] = ok ? 0.0 : -INFINITY;
+        }
+        return;
+    }
+    const int n0 = cand_cnt[2 * u], n1 = cand_cnt[2 * u + 1];
+    const float2 ce = ucut[u];
+    double thr = -INFINITY;
+    if (ce.x != -INFINITY) {
+        thr = (double)ce.x + (double)ce.y;
+        thr = thr - fabs(thr) * 1e-15 - 1e-300;  // round down
+    }
+    const int nitem = (n0 + n1) * 16;
+    int cnt = 0;
+    for (int base = 0; base < nitem; base += WAVE) {
+        const int idx = base + lane;
+        bool keep = false;
+        double s = 0.0;
+        int32_t row = 0;
+        if (idx < nitem) {
+            const int b = idx >> 4, r = idx & 15;
+            const uint32_t lb = (b < n0) ? cand[(2 * u) * IP_CW + b].y : cand[(2 * u + 1) * IP_CW + (b - n0)].y;
+            const int64_t blk = lb >> 1, hh = lb & 1;
+            const int64_t rr = blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (rr < n_items) {
+                row = (int32_t)rr;
+                s = exact_dot(uv, items + rr * dim, dim);
+                keep = s >= thr;
+            }
+        }
+        const unsigned long long bal = __ballot(keep);
+        const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+        if (keep && pos < IP_SURV) surv[wave][pos] = Cand{s, row};
+        cnt += __popcll(bal);
+    }
+    if (cnt > IP_SURV) {  // dense exact ties: hand the user to the exact fallback
+        if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
+        return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    Cand x[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int idx = e * 64 + lane;
+        if (idx < cnt) x[e] = surv[wave][idx];
+        else { x[e].s = -INFINITY; x[e].row = INT32_MAX; }
+    }
+    wave_bitonic_sort<2>(x);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int idx = e * 64 + lane;
+        if (idx < k) {
+            const bool ok = x[e].row != INT32_MAX;
+            out_s[u * k + idx] = ok ? (float)x[e].s : -FLT_MAX;
+            out_r[u * k + idx] = ok ? (int32_t)(x[e].row + row_offset) : -1;
+            if (out_e) out_e[u * k + idx] = ok ? x[e].s : -INFINITY;
+        }
+    }
+}
+
+// -------------------------------------------------------------- fallback --
+__device__ __forceinline__ uint64_t okey(double s) {
+    const uint64_t b = (uint64_t)__double_as_longlong(s);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__global__ __launch_bounds__(256) void ip_fallback_kernel(
+    const float* __restrict__ users, const float* __restrict__ items, int64_t n_items, int dim,
+    int k, int64_t row_offset, const int32_t* __restrict__ ovf_list,
+    const int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
+    double* __restrict__ out_e) {
+    __shared__ unsigned int hist[256];
+    __shared__ Cand sel[64];
+    __shared__ int sel_n;
+    __shared__ unsigned long long s_prefix;
+    __shared__ int s_krem;
+    __shared__ int wcnt[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int cnt = *ovf_count;
+    const int kk = (int)(n_items < k ? n_items : k);
+    for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+        const int64_t u = ovf_list[q];
+        const float* uv = users + u * dim;
+        unsigned long long prefix = 0, mask = 0;
+        int krem = kk;
+        for (int pass = 7; pass >= 0 && kk > 0; --pass) {
+            hist[tid] = 0;
+            __syncthreads();
+            for (int64_t r = tid; r < n_items; r += 256) {
+                const uint64_t key = okey(exact_dot(uv, items + r * dim, dim));
+                if ((key & mask) == prefix) atomicAdd(&hist[(key >> (8 * pass)) & 255], 1u);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int cum = 0, b = 255;
+                for (; b > 0; --b) {
+                    if (cum + (int)hist[b] >= krem) break;
+                    cum += hist[b];
+                }
+                s_prefix = prefix | ((unsigned long long)b << (8 * pass));
+                s_krem = krem - cum;
+            }
+            __syncthreads();
+            prefix = s_prefix;
+            krem = s_krem;
+            mask |= 0xFFull << (8 * pass);
+        }
+        if (tid == 0) sel_n = 0;
+        __syncthreads();
+        int taken = 0;
+        for (int64_t c0 = 0; c0 < n_items && kk > 0; c0 += 256) {
+            const int64_t r = c0 + tid;
+            double s = 0.0;
+            uint64_t key = 0;
+            const bool valid = r < n_items;
+            if (valid) {
+                s = exact_dot(uv, items + r * dim, dim);
+                key = okey(s);
+            }
+            const bool gt = valid && key > prefix;
+            const bool eq = valid && key == prefix;
+            if (gt) {
+                const int pos = atomicAdd(&sel_n, 1);
+                sel[pos] = Cand{s, (int32_t)r};
+            }
+            const unsigned long long bal = __ballot(eq);
+            if (lane == 0) wcnt[wave] = __popcll(bal);
+            __syncthreads();
+            int before = taken;
+            for (int w = 0; w < wave; ++w) before += wcnt[w];
+            before += __popcll(bal & ((1ull << lane) - 1ull));
+            if (eq && before < krem) {
+                const int pos = atomicAdd(&sel_n, 1);
+                sel[pos] = Cand{s, (int32_t)r};
+            }
+            taken += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+            __syncthreads();
+        }
+        __syncthreads();
+        if (wave == 0) {
+            Cand x[1];
+            if (lane < sel_n) x[0] = sel[lane];
+            else { x[0].s = -INFINITY; x[0].row = INT32_MAX; }
+            wave_bitonic_sort<1>(x);
+            if (lane < k) {
+                const bool ok = lane < kk;
+                out_s[u * k + lane] = ok ? (float)x[0].s : -FLT_MAX;
+                out_r[u * k + lane] = ok ? (int32_t)(x[0].row + row_offset) : -1;
+                if (out_e) out_e[u * k + lane] = ok ? x[0].s : -INFINITY;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------- merge --
+template <int E>
+__global__ __launch_bounds__(256) void topk_merge_kernel(
+    const double* __restrict__ in_e, const int32_t* __restrict__ in_r, int n_lists,
+    int64_t stride, int64_t n_users, int k_in, int k_out, float* __restrict__ out_s,
+    int32_t* __restrict__ out_r, double* __restrict__ out_e) {
+    const int lane = threadIdx.x & 63;
+    const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (u >= n_users) return;
+    Cand x[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int idx = e * 64 + lane;
+        const int l = idx / k_in, j = idx - l * k_in;
+        x[e].s = -INFINITY;
+        x[e].row = INT32_MAX;
+        if (l < n_lists) {
+            const int64_t o = l * stride + u * k_in + j;
+            const int32_t r = in_r[o];
+            if (r >= 0) {
+                x[e].s = in_e[o];
+                x[e].row = r;
+            }
+        }
+    }
+    wave_bitonic_sort<E>(x);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int idx = e * 64 + lane;
+        if (idx < k_out) {
+            const bool ok = x[e].row != INT32_MAX;
+            out_s[u * k_out + idx] = ok ? (float)x[e].s : -FLT_MAX;
+            out_r[u * k_out + idx] = ok ? x[e].row : -1;
+            if (out_e) out_e[u * k_out + idx] = ok ? x[e].s : -INFINITY;
+        }
+    }
+}
+
+// ------------------------------------------------------------- workspace --
+struct IpWs {
+    uint2* cand;
+    float2* ucut;
+    int32_t* cnt;
+    int32_t* ovf_flag;
+    int32_t* ovf_list;
+    int32_t* ovf_count;
+    size_t bytes;
+};
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static IpWs ip_ws_layout(void* base, int64_t n_users) {
+    IpWs w;
+    uint8_t* p = reinterpret_cast<uint8_t*>(base);
+    size_t off = 0;
+    w.ovf_count = reinterpret_cast<int32_t*>(p + off);
+    off += 256;
+    w.cand = reinterpret_cast<uint2*>(p + off);
+    off += align256((size_t)n_users * 2 * IP_CW * sizeof(uint2));
+    w.ucut = reinterpret_cast<float2*>(p + off);
+    off += align256((size_t)n_users * sizeof(float2));
+    w.cnt = reinterpret_cast<int32_t*>(p + off);
+    off += align256((size_t)n_users * 2 * sizeof(int32_t));
+    w.ovf_flag = reinterpret_cast<int32_t*>(p + off);
+    off += align256((size_t)n_users * sizeof(int32_t));
+    w.ovf_list = reinterpret_cast<int32_t*>(p + off);
+    off += align256((size_t)n_users * sizeof(int32_t));
+    w.bytes = off;
+    return w;
+}
+
+}  // namespace nrk
+
+using namespace nrk;
+
+extern "C" {
+
+size_t nrk_ip_catalog_bytes(int64_t n_items, int dim) {
+    if (n_items < 0 || dim <= 0 || dim > 256) return 0;
+    return catalog_body_bytes(n_items, pad_dim(dim)) + CATALOG_HDR;
+}
+
+int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* catalog,
+                         nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(items != nullptr || n_items == 0, "items is null");
+    NRK_REQUIRE(catalog != nullptr, "catalog is null");
+    NRK_REQUIRE(n_items >= 0 && n_items < INT32_MAX, "n_items out of range");
+    NRK_REQUIRE(dim > 0 && dim <= 256, "dim must be in [1, 256]");
+    const int dp = pad_dim(dim);
+    hipStream_t s = as_stream(stream);
+    const size_t body = catalog_body_bytes(n_items, dp);
+    CatalogHdr* hdr = reinterpret_cast<CatalogHdr*>(reinterpret_cast<uint8_t*>(catalog) + body);
+    if (hipMemsetAsync(hdr, 0, CATALOG_HDR, s) != hipSuccess) {
+        set_error("nrk_ip_catalog_build: hipMemsetAsync failed");
+        return NRK_EHIP;
+    }
+    const int64_t total = n_blocks_of(n_items) * (dp / 16) * 64;
+    if (total > 0) {
+        const int g2 = (int)std::min<int64_t>((n_items + 255) / 256, 2048);
+        catalog_norm_kernel<<<g2, 256, 0, s>>>(items, n_items, dim, hdr);
+    }
+    catalog_hdr_kernel<<<1, 1, 0, s>>>(hdr, dim, dp);
+    if (total > 0) {
+        const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+        catalog_pack_kernel<<<grid, 256, 0, s>>>(items, n_items, dim, dp, hdr,
+                                                 reinterpret_cast<uint4*>(catalog));
+    }
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+size_t nrk_ip_topk_workspace_bytes(int64_t n_users, int64_t n_items, int dim, int k) {
+    (void)n_items;
+    (void)dim;
+    (void)k;
+    if (n_users < 0) return 0;
+    return ip_ws_layout(nullptr, n_users).bytes;
+}
+
+static int ip_check(const float* users, int64_t n_users, const float* items, const void* catalog,
+                    int64_t n_items, int dim, int k, void* workspace, size_t workspace_bytes) {
+    NRK_REQUIRE(n_users >= 0 && n_items >= 0, "negative sizes");
+    NRK_REQUIRE(n_items < INT32_MAX, "n_items must fit int32 rows");
+    NRK_REQUIRE(dim > 0 && dim <= 256, "dim must be in [1, 256]");
+    NRK_REQUIRE(k >= 1, "k must be >= 1");
+    if (k > IP_KMAX) NRK_UNSUPPORTED("k > 40 is not compiled");
+    if (n_users == 0) return NRK_OK;
+    NRK_REQUIRE(users && workspace, "null pointer");
+    NRK_REQUIRE(n_items == 0 || (items && catalog), "items/catalog null");
+    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users).bytes, "workspace too small");
+    return NRK_OK;
+}
+
+int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
+                       int dim, int k, void* workspace, size_t workspace_bytes,
+                       nrk_stream_t stream) {
+    clear_error();
+    int rc = ip_check(users, n_users, (const float*)catalog, catalog, n_items, dim, k, workspace,
+                      workspace_bytes);
+    if (rc != NRK_OK || n_users == 0) return rc;
+    const IpWs w = ip_ws_layout(workspace, n_users);
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
+        set_error("nrk_ip_topk_screen: hipMemsetAsync failed");
+        return NRK_EHIP;
+    }
+    const int dp = pad_dim(dim);
+    const int grid = (int)((n_users + IP_USERS_PER_WG - 1) / IP_USERS_PER_WG);
+    const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
+    if (n_items == 0) {
+        // nothing to search: every output row is padding
+        (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * 2 * sizeof(int32_t), s);
+        (void)hipMemsetAsync(w.ovf_flag, 0, (size_t)n_users * sizeof(int32_t), s);
+    } else {
+#define NRK_SCREEN(DPV)                                                                     \
+    ip_screen_kernel<DPV><<<grid, 256, 0, s>>>(users, n_users, cat, n_items, dim, k, w.cand, \
+                                              w.cnt, w.ucut, w.ovf_flag, w.ovf_list, w.ovf_count)
+        switch (dp) {
+            case 16: NRK_SCREEN(16); break;
+            case 32: NRK_SCREEN(32); break;
+            case 64: NRK_SCREEN(64); break;
+            case 128: NRK_SCREEN(128); break;
+            default: NRK_SCREEN(256); break;
+        }
+#undef NRK_SCREEN
+    }
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items, int64_t n_items,
+                       int dim, int k, int64_t row_offset, float* out_scores, int32_t* out_rows,
+                       double* out_exact, void* workspace, size_t workspace_bytes,
+                       nrk_stream_t stream) {
+    clear_error();
+    int rc = ip_check(users, n_users, items, items, n_items, dim, k, workspace, workspace_bytes);
+    if (rc != NRK_OK || n_users == 0) return rc;
+    NRK_REQUIRE(out_scores && out_rows, "null output");
+    const IpWs w = ip_ws_layout(workspace, n_users);
+    hipStream_t s = as_stream(stream);
+    const int g2 = (int)((n_users + 3) / 4);
+    ip_refine_kernel<<<g2, 256, 0, s>>>(users, n_users, items, n_items, dim, k, row_offset, w.cand,
+                                        w.cnt, w.ucut, w.ovf_flag, w.ovf_list, w.ovf_count,
+                                        out_scores, out_rows, out_exact);
+    if (n_items > 0)
+        ip_fallback_kernel<<<256, 256, 0, s>>>(users, items, n_items, dim, k, row_offset, w.ovf_list,
+                                               w.ovf_count, out_scores, out_rows, out_exact);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const void* catalog,
+                int64_t n_items, int dim, int k, int64_t row_offset, float* out_scores,
+                int32_t* out_rows, double* out_exact, void* workspace, size_t workspace_bytes,
+                nrk_stream_t stream) {
+    int rc = nrk_ip_topk_screen(users, n_users, catalog, n_items, dim, k, workspace,
+                                workspace_bytes, stream);
+    if (rc != NRK_OK) return rc;
+    return nrk_ip_topk_finish(users, n_users, items, n_items, dim, k, row_offset, out_scores,
+                              out_rows, out_exact, workspace, workspace_bytes, stream);
+}
+
+int nrk_topk_merge(const double* in_exact, const int32_t* in_rows, int n_lists, int64_t list_stride,
+                   int64_t n_users, int k_in, int k_out, float* out_scores, int32_t* out_rows,
+                   double* out_exact, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_lists >= 1 && k_in >= 1 && k_out >= 1 && n_users >= 0, "bad sizes");
+    NRK_REQUIRE(list_stride >= n_users * (int64_t)k_in, "list_stride too small");
+    const int tot = n_lists * k_in;
+    if (tot > 512) NRK_UNSUPPORTED("n_lists * k_in > 512");
+    NRK_REQUIRE(k_out <= tot, "k_out > n_lists * k_in");
+    if (n_users == 0) return NRK_OK;
+    NRK_REQUIRE(in_exact && in_rows && out_scores && out_rows, "null pointer");
+    hipStream_t s = as_stream(stream);
+    const int grid = (int)((n_users + 3) / 4);
+    if (tot <= 64)
+        topk_merge_kernel<1><<<grid, 256, 0, s>>>(in_exact, in_rows, n_lists, list_stride, n_users, k_in, k_out, out_scores, out_rows, out_exact);
+    else if (tot <= 128)
+        topk_merge_kernel<2><<<grid, 256, 0, s>>>(in_exact, in_rows, n_lists, list_stride, n_users, k_in, k_out, out_scores, out_rows, out_exact);
+    else if (tot <= 256)
+        topk_merge_kernel<4><<<grid, 256, 0, s>>>(in_exact, in_rows, n_lists, list_stride, n_users, k_in, k_out, out_scores, out_rows, out_exact);
+    else
+        topk_merge_kernel<8><<<grid, 256, 0, s>>>(in_exact, in_rows, n_lists, list_stride, n_users, k_in, k_out, out_scores, out_rows, out_exact);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,168 @@
+// tower.hip -- YouTubeDNN two-tower forward (eval) on gfx950.
+//
+// User tower: YoutubeDNN.forward (src/recall/youtubednn_recaller.py:129-178)
+// as _extract_embeddings drives it (:425-470), fused with the numpy
+// re-normalisation of :467-470.  Item tower: get_item_embedding (:184-188)
+// fused with :485-489.  Memory-bound gathers (1 + T rows of D fp32 per user)
+// feeding a 2-layer MLP that fits in LDS; one wave per user.
+#include "nrk_common.h"
+
+namespace nrk {
+
+template <int D>
+__global__ __launch_bounds__(256) void tt_user_kernel(
+    const float* __restrict__ user_table, const float* __restrict__ item_table,
+    const int32_t* __restrict__ uid, const int32_t* __restrict__ hist,
+    const int32_t* __restrict__ hist_len, int64_t n, int T, const float* __restrict__ w0,
+    const float* __restrict__ b0, int h0, const float* __restrict__ w1,
+    const float* __restrict__ b1, int h1, float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* sw0 = lds;               // [h0][2D]
+    float* sb0 = sw0 + h0 * 2 * D;  // [h0]
+    float* sw1 = sb0 + h0;          // [h1][h0]
+    float* sb1 = sw1 + h1 * h0;     // [h1]
+    for (int i = threadIdx.x; i < h0 * 2 * D; i += blockDim.x) sw0[i] = w0[i];
+    for (int i = threadIdx.x; i < h0; i += blockDim.x) sb0[i] = b0[i];
+    for (int i = threadIdx.x; i < h1 * h0; i += blockDim.x) sw1[i] = w1[i];
+    for (int i = threadIdx.x; i < h1; i += blockDim.x) sb1[i] = b1[i];
+    __syncthreads();  // the only block barrier: the user loop below is per wave
+
+    constexpr int P = WAVE / D;  // history phases per lane group
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int d = lane % D, ph = lane / D;
+    const int64_t wstride = (int64_t)gridDim.x * 4;
+    for (int64_t u = (int64_t)blockIdx.x * 4 + wave; u < n; u += wstride) {
+        const int len = hist_len[u];
+        const int32_t* hr = hist + u * T;
+        float sum = 0.0f;
+        for (int t = ph; t < len; t += P) sum += item_table[(int64_t)hr[t] * D + d];
+#pragma unroll
+        for (int off = D; off < WAVE; off <<= 1) sum += __shfl_xor(sum, off, WAVE);
+        // lane q < D holds x[q] = E_u[uid][q] and x[D + q] = mean[q]
+        const float xu = user_table[(int64_t)uid[u] * D + d];
+        const float xm = sum / ((float)len + 1e-8f);
+        // layer 0: lane o (and o + 64) owns output o
+        float y0 = 0.0f, y1 = 0.0f;
+        {
+            float z0 = lane < h0 ? sb0[lane] : 0.0f;
+            float z1 = lane + WAVE < h0 ? sb0[lane + WAVE] : 0.0f;
+            const float* wr0 = sw0 + (lane < h0 ? lane : 0) * 2 * D;
+            const float* wr1 = sw0 + (lane + WAVE < h0 ? lane + WAVE : 0) * 2 * D;
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                const float xq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xu), q));
+                z0 += wr0[q] * xq;
+                z1 += wr1[q] * xq;
+            }
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                const float mq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xm), q));
+                z0 += wr0[D + q] * mq;
+                z1 += wr1[D + q] * mq;
+            }
+            y0 = fmaxf(z0, 0.0f);
+            y1 = fmaxf(z1, 0.0f);
+        }
+        // layer 1: lane o < h1 owns output o
+        float v = 0.0f;
+        {
+            float z = lane < h1 ? sb1[lane] : 0.0f;
+            const float* wr = sw1 + (lane < h1 ? lane : 0) * h0;
+            const int q0 = h0 < WAVE ? h0 : WAVE;
+            for (int q = 0; q < q0; ++q)
+                z += wr[q] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y0), q));
+            for (int q = WAVE; q < h0; ++q)
+                z += wr[q] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y1), q - WAVE));
+            v = lane < h1 ? fmaxf(z, 0.0f) : 0.0f;
+        }
+        const float nn = sqrtf(wave_sum_f32(v * v));
+        v = v / fmaxf(nn, 1e-12f);
+        float n2 = sqrtf(wave_sum_f32(v * v));
+        if (n2 == 0.0f) n2 = 1.0f;
+        if (lane < h1) out[u * h1 + lane] = v / n2;
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void tt_item_kernel(const float* __restrict__ table,
+                                                      const int32_t* __restrict__ ids, int64_t n,
+                                                      float* __restrict__ out) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const float* src = table + (int64_t)ids[r] * D;
+        float v[D];
+        float s = 0.0f;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            v[q] = src[q];
+            s += v[q] * v[q];
+        }
+        const float inv = fmaxf(sqrtf(s), 1e-12f);
+        float s2 = 0.0f;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            v[q] = v[q] / inv;
+            s2 += v[q] * v[q];
+        }
+        const float n2 = sqrtf(s2);
+#pragma unroll
+        for (int q = 0; q < D; ++q) out[r * D + q] = v[q] / n2;
+    }
+}
+
+}  // namespace nrk
+
+using namespace nrk;
+
+extern "C" {
+
+int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* item_table,
+                    int64_t n_item_rows, int dim, const int32_t* uid, const int32_t* hist,
+                    const int32_t* hist_len, int64_t n, int seq_len, const float* w0,
+                    const float* b0, int h0, const float* w1, const float* b1, int h1,
+                    float* out, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n >= 0 && seq_len >= 1, "bad sizes");
+    NRK_REQUIRE(n_user_rows > 0 && n_item_rows > 0, "empty embedding tables");
+    if (!(dim == 16 || dim == 32 || dim == 64)) NRK_UNSUPPORTED("dim must be 16, 32 or 64");
+    NRK_REQUIRE(h0 >= 1 && h0 <= 128, "h0 must be in [1, 128]");
+    NRK_REQUIRE(h1 == dim, "last hidden width must equal the embedding dim "
+                           "(youtubednn_recaller.py:461-465)");
+    if (n == 0) return NRK_OK;
+    NRK_REQUIRE(user_table && item_table && uid && hist && hist_len && w0 && b0 && w1 && b1 && out,
+                "null pointer");
+    const size_t lds = sizeof(float) * ((size_t)h0 * 2 * dim + h0 + (size_t)h1 * h0 + h1);
+    hipStream_t s = as_stream(stream);
+    const int grid = (int)std::min<int64_t>((n + 3) / 4, 2048);
+#define NRK_TT_LAUNCH(DD)                                                                      \
+    do {                                                                                       \
+        (void)hipFuncSetAttribute((const void*)tt_user_kernel<DD>,                                 \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);             \
+        tt_user_kernel<DD><<<grid, 256, lds, s>>>(user_table, item_table, uid, hist, hist_len, \
+                                                  n, seq_len, w0, b0, h0, w1, b1, h1, out);    \
+    } while (0)
+    if (dim == 16) NRK_TT_LAUNCH(16);
+    else if (dim == 32) NRK_TT_LAUNCH(32);
+    else NRK_TT_LAUNCH(64);
+#undef NRK_TT_LAUNCH
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_tt_item_fwd(const float* item_table, int64_t n_item_rows, int dim, const int32_t* ids,
+                    int64_t n, float* out, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n >= 0 && n_item_rows > 0, "bad sizes");
+    if (!(dim == 16 || dim == 32 || dim == 64)) NRK_UNSUPPORTED("dim must be 16, 32 or 64");
+    if (n == 0) return NRK_OK;
+    NRK_REQUIRE(item_table && ids && out, "null pointer");
+    hipStream_t s = as_stream(stream);
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    if (dim == 16) tt_item_kernel<16><<<grid, 256, 0, s>>>(item_table, ids, n, out);
+    else if (dim == 32) tt_item_kernel<32><<<grid, 256, 0, s>>>(item_table, ids, n, out);
+    else tt_item_kernel<64><<<grid, 256, 0, s>>>(item_table, ids, n, out);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,164 @@
+"""Torch-tensor front end of the C ABI (include/nrk.h).
+
+Every op validates shapes / dtypes / devices on the host before it launches
+(the kernels trust their arguments), runs on the current HIP stream, and
+allocates its outputs and workspace with the torch caching allocator.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_P = _lib.P
+
+
+def _stream():
+    return _P(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return _P(t.data_ptr()) if t is not None else None
+
+
+def _dev(*ts):
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise ValueError("nrk ops need device (cuda/HIP) tensors")
+        if not t.is_contiguous():
+            raise ValueError("nrk ops need contiguous tensors")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError("tensors on different devices")
+    return dev
+
+
+def _need(t, dtype, shape=None, name="tensor"):
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+
+
+# ------------------------------------------------------------------ tower --
+def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1):
+    """YoutubeDNN user tower + re-normalisation (youtubednn_recaller.py:129-178, :467-470)."""
+    _dev(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1)
+    n, T = hist.shape
+    D = user_table.shape[1]
+    h0, h1 = w0.shape[0], w1.shape[0]
+    _need(user_table, torch.float32, name="user_table")
+    _need(item_table, torch.float32, (item_table.shape[0], D), "item_table")
+    _need(uid, torch.int32, (n,), "uid")
+    _need(hist, torch.int32, name="hist")
+    _need(hist_len, torch.int32, (n,), "hist_len")
+    _need(w0, torch.float32, (h0, 2 * D), "w0")
+    _need(b0, torch.float32, (h0,), "b0")
+    _need(w1, torch.float32, (h1, h0), "w1")
+    _need(b1, torch.float32, (h1,), "b1")
+    if n and (int(hist_len.min()) < 0 or int(hist_len.max()) > T):
+        raise ValueError("hist_len out of [0, T]")
+    out = torch.empty((n, h1), dtype=torch.float32, device=uid.device)
+    _lib.call("nrk_tt_user_fwd", _ptr(user_table), user_table.shape[0], _ptr(item_table),
+              item_table.shape[0], D, _ptr(uid), _ptr(hist), _ptr(hist_len), n, T,
+              _ptr(w0), _ptr(b0), h0, _ptr(w1), _ptr(b1), h1, _ptr(out), _stream())
+    return out
+
+
+def tt_item_fwd(item_table, ids):
+    """get_item_embedding + re-normalisation (youtubednn_recaller.py:184-188, :485-489)."""
+    _dev(item_table, ids)
+    _need(item_table, torch.float32, name="item_table")
+    _need(ids, torch.int32, name="ids")
+    n, D = ids.shape[0], item_table.shape[1]
+    out = torch.empty((n, D), dtype=torch.float32, device=ids.device)
+    _lib.call("nrk_tt_item_fwd", _ptr(item_table), item_table.shape[0], D, _ptr(ids), n,
+              _ptr(out), _stream())
+    return out
+
+
+# ------------------------------------------------------------------ top-k --
+class Catalog:
+    """The search index: fp32 rows (kept for exact rescoring) + packed bf16
+    copy in MFMA fragment order.  = faiss.IndexFlatIP(d).add(items)."""
+
+    def __init__(self, items: torch.Tensor):
+        _dev(items)
+        _need(items, torch.float32, name="items")
+        if items.dim() != 2 or not (1 <= items.shape[1] <= 256):
+            raise ValueError("items must be [n, d] with 1 <= d <= 256")
+        self.items = items
+        self.n, self.d = items.shape
+        nbytes = _lib.lib().nrk_ip_catalog_bytes(self.n, self.d)
+        self.packed = torch.empty(nbytes, dtype=torch.uint8, device=items.device)
+        _lib.call("nrk_ip_catalog_build", _ptr(items), self.n, self.d, _ptr(self.packed), _stream())
+
+    @property
+    def ntotal(self):
+        return self.n
+
+
+def ip_topk(users, catalog: Catalog, k: int, row_offset: int = 0, exact: bool = False, workspace=None):
+    """Exact top-k rows per user (scores f32 [n,k], rows i32 [n,k] (+ fp64))."""
+    _dev(users, catalog.items)
+    _need(users, torch.float32, name="users")
+    if users.dim() != 2 or users.shape[1] != catalog.d:
+        raise ValueError(f"users must be [n, {catalog.d}]")
+    if not (1 <= k <= 40):
+        raise ValueError("k must be in [1, 40]")
+    n = users.shape[0]
+    dev = users.device
+    s = torch.empty((n, k), dtype=torch.float32, device=dev)
+    r = torch.empty((n, k), dtype=torch.int32, device=dev)
+    e = torch.empty((n, k), dtype=torch.float64, device=dev) if exact else None
+    ws_bytes = _lib.lib().nrk_ip_topk_workspace_bytes(n, catalog.n, catalog.d, k)
+    if workspace is None or workspace.numel() < ws_bytes:
+        workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    _lib.call("nrk_ip_topk", _ptr(users), n, _ptr(catalog.items), _ptr(catalog.packed), catalog.n,
+              catalog.d, k, int(row_offset), _ptr(s), _ptr(r), _ptr(e), _ptr(workspace),
+              workspace.numel(), _stream())
+    return (s, r, e) if exact else (s, r)
+
+
+def ip_topk_workspace(n_users, catalog: Catalog, k, device):
+    nb = _lib.lib().nrk_ip_topk_workspace_bytes(n_users, catalog.n, catalog.d, k)
+    return torch.empty(nb, dtype=torch.uint8, device=device)
+
+
+def topk_merge(exact_lists, row_lists, k_out):
+    """Merge [G, n, k_in] per-shard lists (fp64 scores + global rows)."""
+    _dev(exact_lists, row_lists)
+    _need(exact_lists, torch.float64, name="exact_lists")
+    _need(row_lists, torch.int32, tuple(exact_lists.shape), "row_lists")
+    G, n, k_in = exact_lists.shape
+    if G * k_in > 512 or k_out > G * k_in:
+        raise ValueError("need G*k_in <= 512 and k_out <= G*k_in")
+    dev = exact_lists.device
+    s = torch.empty((n, k_out), dtype=torch.float32, device=dev)
+    r = torch.empty((n, k_out), dtype=torch.int32, device=dev)
+    e = torch.empty((n, k_out), dtype=torch.float64, device=dev)
+    _lib.call("nrk_topk_merge", _ptr(exact_lists), _ptr(row_lists), G, n * k_in, n, k_in, k_out,
+              _ptr(s), _ptr(r), _ptr(e), _stream())
+    return s, r, e
+
+
+def ip_topk_screen(users, catalog: Catalog, k: int, workspace):
+    """Phase 1 of ip_topk (bf16 MFMA scan -> candidate band in ``workspace``)."""
+    _dev(users, workspace)
+    n = users.shape[0]
+    _lib.call("nrk_ip_topk_screen", _ptr(users), n, _ptr(catalog.packed), catalog.n, catalog.d, k,
+              _ptr(workspace), workspace.numel(), _stream())
+
+
+def ip_topk_finish(users, catalog: Catalog, k: int, workspace, out_scores, out_rows,
+                   out_exact=None, row_offset: int = 0):
+    """Phase 2 of ip_topk (exact rescoring + ordering) into preallocated outputs."""
+    _dev(users, workspace, out_scores, out_rows, out_exact)
+    n = users.shape[0]
+    _lib.call("nrk_ip_topk_finish", _ptr(users), n, _ptr(catalog.items), catalog.n, catalog.d, k,
+              int(row_offset), _ptr(out_scores), _ptr(out_rows), _ptr(out_exact), _ptr(workspace),
+              workspace.numel(), _stream())

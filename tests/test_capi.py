@@ -1,0 +1,49 @@
+"""C ABI checks that need no GPU: the library loads, and it exports every
+entry point include/nrk.h declares with the signature nrk/_lib.py binds."""
+import os
+import re
+
+from nrk import _lib
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "nrk.h")
+
+
+def declared():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(nrk_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_abi():
+    names = declared()
+    assert "nrk_ip_topk" in names and "nrk_din_forward" in names and "nrk_itemcf_sim" in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    missing = [n for n in declared() if getattr(L, n, None) is None]
+    assert not missing, f"libnrk.so lacks {missing}"
+
+
+def test_binding_covers_header():
+    assert sorted(_lib.SIGNATURES) == declared()
+
+
+def test_host_queries_without_gpu():
+    L = _lib.lib()
+    assert L.nrk_abi_version() == 1
+    assert L.nrk_ip_catalog_bytes(364047, 32) > 364047 * 32 * 2
+    assert L.nrk_ip_topk_workspace_bytes(250000, 364047, 32, 31) > 0
+
+
+def test_argument_errors_raise_valueerror():
+    import pytest
+
+    L = _lib.lib()
+    rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, 0, 0, None, None, None, None, 0, None)
+    assert rc == _lib.NRK_EINVAL
+    assert b"k must be" in L.nrk_last_error()
+    with pytest.raises(ValueError):
+        _lib.check(rc, "nrk_ip_topk")
+    rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, 64, 0, None, None, None, None, 0, None)
+    assert rc == _lib.NRK_EUNSUPPORTED

@@ -1,0 +1,179 @@
+"""GPU parity: ip_topk (faiss.IndexFlatIP replacement) and the two-tower forward.
+
+Checker = the CPU oracle (oracle/) and the golden fixtures from the reference.
+Bar: bit-exact row indices (ties -> lower row), scores equal to the fp32
+rounding of the exact fp64 score (so exact equality is expected; the
+reference's own tolerance 1e-5 is the documented bar).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from nrk import ops as _ops
+
+    return _ops
+
+
+def _dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def _run_topk(ops, users, items, k, row_offset=0):
+    cat = ops.Catalog(_dev(items, torch.float32))
+    s, r, e = ops.ip_topk(_dev(users, torch.float32), cat, k, row_offset=row_offset, exact=True)
+    torch.cuda.synchronize()
+    return s.cpu().numpy(), r.cpu().numpy().astype(np.int64), e.cpu().numpy()
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_ip_topk_golden(ops, golden, tag):
+    g = golden("topk_small")
+    k = int(g["k"]) + 1
+    s, r, e = _run_topk(ops, g[f"{tag}_users"], g[f"{tag}_items"], k)
+    assert np.array_equal(r, g[f"{tag}_I"])
+    assert np.array_equal(s, g[f"{tag}_D"])
+
+
+def test_ip_topk_padding_golden(ops, golden):
+    g = golden("topk_small")
+    k = g["small_I"].shape[1]
+    s, r, _ = _run_topk(ops, g["a_users"][:4], g["a_items"][:10], k)
+    assert np.array_equal(r, g["small_I"])
+    assert np.array_equal(s, g["small_D"])
+
+
+def _unit(x):
+    n = np.linalg.norm(x, axis=1, keepdims=True)
+    n[n == 0] = 1
+    return (x / n).astype(np.float32)
+
+
+@pytest.mark.parametrize(
+    "n_users,n_items,d,k",
+    [
+        (1, 1, 32, 1),
+        (3, 31, 32, 31),
+        (129, 33, 32, 31),
+        (300, 1000, 32, 31),
+        (257, 5003, 32, 40),
+        (130, 4097, 16, 10),
+        (70, 3000, 50, 21),
+        (200, 2500, 64, 31),
+        (64, 2000, 128, 31),
+        (40, 1500, 250, 21),
+    ],
+)
+def test_ip_topk_vs_oracle(ops, n_users, n_items, d, k):
+    rng = np.random.default_rng(n_users * 7 + n_items + d)
+    users = _unit(rng.standard_normal((n_users, d)))
+    items = _unit(rng.standard_normal((n_items, d)))
+    s, r, e = _run_topk(ops, users, items, k)
+    so, ro, eo = oracle.ip_topk(users, items, k, exact=True)
+    assert np.array_equal(r, ro)
+    assert np.array_equal(s, so)
+    assert np.array_equal(e[ro >= 0], eo[ro >= 0])
+
+
+def test_ip_topk_unnormalised_and_offset(ops):
+    rng = np.random.default_rng(3)
+    users = (rng.standard_normal((150, 32)) * 5).astype(np.float32)
+    items = (rng.standard_normal((2000, 32)) * rng.random((2000, 1)) * 3).astype(np.float32)
+    s, r, _ = _run_topk(ops, users, items, 31, row_offset=1000)
+    so, ro = oracle.ip_topk(users, items, 31)
+    assert np.array_equal(r, ro + 1000)
+    assert np.array_equal(s, so)
+
+
+def test_ip_topk_ties_overflow_fallback(ops):
+    # heavy exact duplicates -> candidate band overflows -> exact fallback path
+    rng = np.random.default_rng(9)
+    base = _unit(rng.standard_normal((4, 32)))
+    items = base[rng.integers(0, 4, size=6000)]
+    users = _unit(rng.standard_normal((64, 32)))
+    users[:8] = 0.0
+    users[8:16] = base[rng.integers(0, 4, size=8)]
+    s, r, _ = _run_topk(ops, users, items, 31)
+    so, ro = oracle.ip_topk(users, items, 31)
+    assert np.array_equal(r, ro)
+    assert np.array_equal(s, so)
+
+
+def test_recall_lists_match_reference(golden):
+    """YoutubeDNNRecaller.recall semantics end to end (drop rank 0, row->raw quirk)."""
+    from nrk.recall.youtubednn_recaller import YoutubeDNNRecaller
+
+    g = golden("youtubednn_small")
+    rec = YoutubeDNNRecaller.from_embeddings(
+        g["user_embeddings"], g["item_embeddings"],
+        user_index_2_rawid=g["user_index_2_rawid"], item_index_2_rawid=g["item_index_2_rawid"],
+    )
+    k = int(g["topk"])
+    res = rec.batch_recall([int(u) for u in g["recall_users"]], topk=k)
+    ro = g["recall_offsets"]
+    for n, u in enumerate(g["recall_users"]):
+        got = res[int(u)]
+        assert [a for a, _ in got] == g["recall_items"][ro[n]:ro[n + 1]].tolist()
+        np.testing.assert_allclose([b for _, b in got], g["recall_scores"][ro[n]:ro[n + 1]], atol=1e-6)
+    assert rec.recall(10**9, topk=5) == []
+
+
+def test_tower_matches_golden(ops, golden):
+    from nrk.data import synth
+
+    g = golden("youtubednn_small")
+    log = synth.ClickLog(g["click_user"], g["click_item"], g["click_ts"])
+    uid, hist, hlen, _, profile = synth.youtubednn_histories(log, int(g["seq_max_len"]))
+    out = ops.tt_user_fwd(_dev(g["user_emb"]), _dev(g["item_emb"]), _dev(uid, torch.int32),
+                          _dev(hist, torch.int32), _dev(hlen, torch.int32), _dev(g["w0"]),
+                          _dev(g["b0"]), _dev(g["w1"]), _dev(g["b1"]))
+    it = ops.tt_item_fwd(_dev(g["item_emb"]), _dev(profile, torch.int32))
+    np.testing.assert_allclose(out.cpu().numpy(), g["user_embeddings"], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(it.cpu().numpy(), g["item_embeddings"], atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("D,h0", [(16, 64), (32, 64), (64, 128), (32, 100)])
+def test_tower_vs_oracle(ops, D, h0):
+    rng = np.random.default_rng(D + h0)
+    U, I, T, n = 500, 3000, 30, 777
+    ue = (rng.standard_normal((U, D)) * 0.01).astype(np.float32)
+    ie = (rng.standard_normal((I, D)) * 0.01).astype(np.float32)
+    w0 = (rng.standard_normal((h0, 2 * D)) * 0.2).astype(np.float32)
+    b0 = (rng.standard_normal(h0) * 0.01).astype(np.float32)
+    w1 = (rng.standard_normal((D, h0)) * 0.2).astype(np.float32)
+    b1 = (rng.standard_normal(D) * 0.01).astype(np.float32)
+    uid = rng.integers(0, U, n)
+    hlen = rng.integers(0, T + 1, n)
+    hist = rng.integers(0, I, (n, T)) * (np.arange(T)[None] < hlen[:, None])
+    out = ops.tt_user_fwd(_dev(ue), _dev(ie), _dev(uid, torch.int32), _dev(hist, torch.int32),
+                          _dev(hlen, torch.int32), _dev(w0), _dev(b0), _dev(w1), _dev(b1))
+    ref = oracle.tower_user(ue, ie, uid, hist, hlen, w0, b0, w1, b1)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-5, rtol=0)
+
+
+def test_full_size_topk_properties(ops):
+    """Config 2 shapes (250k x 364,047 x 32, k=31): sortedness, exact scores,
+    and oracle agreement on a user sample."""
+    rng = np.random.default_rng(23)
+    U, I, D, K = 250_000, 364_047, 32, 31
+    g = torch.Generator(device="cuda").manual_seed(23)
+    users = torch.nn.functional.normalize(torch.randn(U, D, device="cuda", generator=g), dim=1)
+    items = torch.nn.functional.normalize(torch.randn(I, D, device="cuda", generator=g), dim=1)
+    cat = ops.Catalog(items.contiguous())
+    s, r, e = ops.ip_topk(users.contiguous(), cat, K, exact=True)
+    torch.cuda.synchronize()
+    assert bool((r >= 0).all()) and bool((r < I).all())
+    assert bool((e[:, :-1] >= e[:, 1:]).all())
+    sample = np.sort(rng.choice(U, 256, replace=False))
+    so, ro = oracle.ip_topk(users[sample].cpu().numpy(), items.cpu().numpy(), K, nthreads=8)
+    assert np.array_equal(r[sample].cpu().numpy().astype(np.int64), ro)
+    assert np.array_equal(s[sample].cpu().numpy(), so)
