@@ -171,7 +171,7 @@ def main():
     achieved = flops / (screen_ms * 1e-3) / 1e12
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                "kernel": "ip_screen_kernel<32>", "kernel_ms": round(screen_ms, 4),
+                "kernel": "ip_screen_kernel<32> (fp16 MFMA 32x32x16)", "kernel_ms": round(screen_ms, 4),
                 "algorithmic_flop_per_launch": flops}
 
     cpu = None
@@ -196,7 +196,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "recalled pairs/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16",
+            "vs_baseline": None, "dtype": "fp16",
             "data": "synthetic Tianchi-shaped click log (seeded), random-init YouTubeDNN weights",
             "config": {"workload": "BASELINE config 2: YouTubeDNN recall (user tower + exact top-31 "
                                    "IP search), 250k users x 364,047 items, D=32",

@@ -78,7 +78,7 @@ int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* cat
  * lower row; fewer than k items -> rows -1 / scores -FLT_MAX.
  * out_rows are catalog rows + row_offset (global rows of a shard).
  * out_exact (nullable) receives the fp64 scores used for ordering (the
- * merge key for catalog-sharded runs).  k <= 40; dim <= 256. */
+ * merge key for catalog-sharded runs).  k <= 32; dim <= 256. */
 size_t nrk_ip_topk_workspace_bytes(int64_t n_users, int64_t n_items, int dim, int k);
 int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const void* catalog,
                 int64_t n_items, int dim, int k, int64_t row_offset, float* out_scores,

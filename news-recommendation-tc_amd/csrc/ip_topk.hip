@@ -11,15 +11,16 @@
 //      (A operand) streamed through LDS from a catalog pre-packed in
 //      fragment order, 32 users per wave (B operand) held in registers.
 //      Each lane owns one user x one 16-item half of every 32-item block.
-//      Per block the lane takes the max of its 16 scores; only when that
-//      beats the lane threshold tau does it append ONE entry (block max,
-//      block id) to its LDS list.  tau = theta - 2*eps, theta = K-th largest
-//      listed block max (a lower bound of the K-th largest score: K distinct
-//      blocks each hold an item >= theta), eps bounds |fp16 score - exact|
+//      Per block the lane takes the max of its 16 scores and appends
+//      (half-block max, half-block id) to its LDS list, branch-free: the
+//      entry is always written and kept only if it beats the lane threshold
+//      tau = theta - 2*eps, theta = K-th largest listed half-block max (a
+//      lower bound of the K-th largest score: K distinct half-blocks each
+//      hold an item >= theta), eps bounds |fp16 score - exact|
 //      (eps = c(D) * ||u|| * max_j ||v_j||).  A full list is compacted by a
 //      register bitonic sort (all lanes at once, no serial LDS chains).
 //   2. ip_refine   -- one wave per user: fp64 exact rescoring of every item
-//      of the flagged blocks, keep items with exact score >= cut + eps
+//      of the flagged half-blocks, keep items with exact score >= cut + eps
 //      (typically K + a few), wave bitonic sort on (score desc, row asc).
 //   3. ip_fallback -- users whose candidate band overflowed (dense exact or
 //      near ties, e.g. duplicated catalog rows): exact fp64 radix-select over
@@ -28,6 +29,8 @@
 
 #include <float.h>
 
+#include <type_traits>
+
 namespace nrk {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -35,7 +38,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int IP_CL = 64;          // per-lane candidate list capacity (LDS)
 constexpr int IP_CW = IP_CL - 16;  // entries kept per lane after the final flush
-constexpr int IP_KMAX = 40;
+constexpr int IP_KMAX = 32;
 constexpr int IP_USERS_PER_WG = 128;  // 4 waves x 32 users
 constexpr size_t CATALOG_HDR = 256;
 
@@ -164,21 +167,19 @@ struct LaneList {
     __device__ __forceinline__ void put(int j, uint2 v) const { base[j * WAVE + lane] = v; }
 };
 
-// Compact every lane's list: theta = k-th largest listed block max,
+// Compact every lane's list: theta = k-th largest listed sub-block max,
 // keep entries >= theta - 2 eps (eps == 0: exactly the first k in list
-// order among ties -- the zero user, whose scores are exact).
+// order among ties -- the zero user, whose scores are exact).  Only the 64
+// scores live in registers; compaction re-reads the list in 16-entry chunks
+// (writes go to positions <= the chunk being read, so chunks stay intact).
+template <int CAP>  // entries a lane may keep: room for one tile of appends
 __device__ __forceinline__ void lanes_flush(const LaneList& L, int& n, float& tau, float& theta,
                                             bool& ovf, int k, float eps, bool active) {
-    float sv[IP_CL];
-    uint32_t pv[IP_CL];
     float x[IP_CL];
 #pragma unroll
     for (int j = 0; j < IP_CL; ++j) {
-        const uint2 e = L.get(j);
-        const bool ok = active && j < n;
-        sv[j] = ok ? __uint_as_float(e.x) : -INFINITY;
-        pv[j] = e.y;
-        x[j] = sv[j];
+        const float v = __uint_as_float(L.base[j * WAVE + L.lane].x);
+        x[j] = (active && j < n) ? v : -INFINITY;
     }
     if (!(active && n >= k)) return;
     sort64_desc(x);
@@ -192,20 +193,26 @@ __device__ __forceinline__ void lanes_flush(const LaneList& L, int& n, float& ta
     const int eq_allow = k - gt;
     int m = 0, eq_seen = 0;
 #pragma unroll
-    for (int j = 0; j < IP_CL; ++j) {
-        const float s = sv[j];
-        bool keep;
-        if (eps == 0.0f) {
-            keep = s > th || (s == th && eq_seen < eq_allow);
-            eq_seen += (s == th) ? 1 : 0;
-        } else {
-            keep = s >= cut;
-        }
-        if (keep && m < IP_CL - 1) {
-            L.put(m, make_uint2(__float_as_uint(s), pv[j]));
-            ++m;
-        } else if (keep) {
-            ovf = true;
+    for (int c = 0; c < IP_CL; c += 16) {
+        uint2 e[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) e[j] = L.get(c + j);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float s = __uint_as_float(e[j].x);
+            bool keep = c + j < n;
+            if (eps == 0.0f) {
+                keep = keep && (s > th || (s == th && eq_seen < eq_allow));
+                eq_seen += (c + j < n && s == th) ? 1 : 0;
+            } else {
+                keep = keep && s >= cut;
+            }
+            if (keep && m < CAP) {
+                L.put(m, e[j]);
+                ++m;
+            } else if (keep) {
+                ovf = true;  // band denser than the list: the user is redone exactly
+            }
         }
     }
     n = m;
@@ -215,24 +222,28 @@ __device__ __forceinline__ void lanes_flush(const LaneList& L, int& n, float& ta
 
 template <int DP>
 __global__ __launch_bounds__(256, 1) void ip_screen_kernel(
-    const float* __restrict__ users, int64_t n_users, const uint8_t* __restrict__ catalog,
-    int64_t n_items, int dim, int k, uint2* __restrict__ cand, int32_t* __restrict__ cand_cnt,
+    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog,
+    int n_items, int dim, int k, uint2* __restrict__ cand, int32_t* __restrict__ cand_cnt,
     float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
     int32_t* __restrict__ ovf_count) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
-    constexpr int TILE_BYTES = BLOCK_BYTES >= 8192 ? BLOCK_BYTES : 8192;
-    constexpr int TB = TILE_BYTES / BLOCK_BYTES;
-    constexpr int LPT = TILE_BYTES / (256 * 16);  // 16-B loads per thread per tile
+    constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : (8192 / BLOCK_BYTES > 4 ? 4 : 8192 / BLOCK_BYTES);
+    constexpr int TILE_BYTES = TB * BLOCK_BYTES;
+    constexpr int LPT = TILE_BYTES / (256 * 16);  // 1-KB LDS-DMA pieces per wave per tile
     constexpr int LIST_BYTES = 4 * IP_CL * WAVE * 8;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * TILE_BYTES + LIST_BYTES];
+    constexpr int NSLOT = (3 * TILE_BYTES + LIST_BYTES <= 163840) ? 3 : 2;  // LDS tile ring
+    // all LDS in ONE array (a second __shared__ object makes hipcc wait on
+    // the LDS-DMA before unrelated ds_reads)
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NSLOT * TILE_BYTES + LIST_BYTES];
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-    const int64_t user = (int64_t)blockIdx.x * IP_USERS_PER_WG + wave * 32 + (lane & 31);
+    const int user = blockIdx.x * IP_USERS_PER_WG + wave * 32 + (lane & 31);
     const bool active = user < n_users;
 
-    const int64_t nblk = n_blocks_of(n_items);
+    const int nblk = (n_items + 31) >> 5;
+    const int ntile = (nblk + TB - 1) / TB;
     const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk * BLOCK_BYTES);
     const float vmax = hdr->max_norm;
     const float sv_scale = hdr->scale;
@@ -241,12 +252,13 @@ __global__ __launch_bounds__(256, 1) void ip_screen_kernel(
     // holds user (lane&31), dims 16s + 8h + [0, 8) for k-step s.
     float uval[DS][8];
     float nrm2 = 0.0f, uabs = 0.0f;
+    const float* urow = users + (size_t)(active ? user : 0) * dim;
 #pragma unroll
     for (int s = 0; s < DS; ++s)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const int d = 16 * s + 8 * h + e;
-            const float f = (active && d < dim) ? users[user * dim + d] : 0.0f;
+            const float f = (active && d < dim) ? urow[d] : 0.0f;
             uval[s][e] = f;
             nrm2 += f * f;
             uabs = fmaxf(uabs, fabsf(f));
@@ -266,89 +278,171 @@ __global__ __launch_bounds__(256, 1) void ip_screen_kernel(
     const float scl = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
     const float eps_s = eps * scl;
 
-    LaneList L{reinterpret_cast<uint2*>(smem + 2 * TILE_BYTES) + wave * IP_CL * WAVE, lane};
+    LaneList L{reinterpret_cast<uint2*>(smem + NSLOT * TILE_BYTES) + wave * IP_CL * WAVE, lane};
     int n = 0;
-    float tau = -INFINITY, theta = -INFINITY;
+    float tau = active ? -INFINITY : INFINITY, theta = -INFINITY;
     bool ovf = false;
 
-    const int64_t ntile = (nblk + TB - 1) / TB;
-    const uint4* cat4 = reinterpret_cast<const uint4*>(catalog);
-    const int64_t body16 = nblk * (BLOCK_BYTES / 16);
-    uint4 stage[LPT];
-    auto load_tile = [&](int64_t t) {
+    const int body_bytes = nblk * BLOCK_BYTES;
+    const int tail_blk = n_items >> 5;  // first block holding a row >= n_items
+    // Tile t -> ring slot t % NSLOT by LDS-DMA (global_load_lds_dwordx4: one
+    // 1-KB piece per wave-instruction, no VGPR staging, nothing for the
+    // compiler to sink); tiles past the end re-load the last piece (keeps
+    // the per-wave vmcnt accounting uniform, the data is never used).
+#ifdef NRK_SCREEN_STATS
+    // dev-only instrumentation (separate build): per wave flushes and cycles,
+    // written to ovf_list[n_users + 8 * gwave ...]
+    unsigned long long st_slow = 0, st_flush = 0, st_cyc_slow = 0, st_cyc_flush = 0;
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+#endif
+    auto issue_tile = [&](int t) {
+        uint8_t* slot = smem + (t % NSLOT) * TILE_BYTES;
 #pragma unroll
         for (int q = 0; q < LPT; ++q) {
-            const int64_t idx = t * (TILE_BYTES / 16) + q * 256 + tid;
-            stage[q] = idx < body16 ? cat4[idx] : make_uint4(0, 0, 0, 0);
+            const int piece = q * 4 + wave;
+            int off = t * TILE_BYTES + piece * 1024;
+            off = off < body_bytes ? off : body_bytes - 1024;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(catalog + off + lane * 16),
+                (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16, 0, 0);
         }
     };
-    auto store_tile = [&](int buf) {
-        uint4* dst = reinterpret_cast<uint4*>(smem + buf * TILE_BYTES);
+    // one tile: TB blocks x DS k-steps of MFMA, then per block the lane's
+    // half-block max is appended branch-free (kept when it beats tau)
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
+    // this lane's list slot 0 (entry j at + j * 512)
+    const uint32_t list_lds = lds_base + NSLOT * TILE_BYTES + (wave * IP_CL * WAVE + lane) * 8;
+    // Fragment reads as inline asm: hipcc's waitcnt pass would otherwise put
+    // a vmcnt(0) (drain every LDS-DMA in flight, i.e. the prefetch) in front
+    // of any ds_read of the ring.  Ordering is explicit: the caller's counted
+    // vmcnt + barrier retire the slot's DMA; lgkmcnt(0) retires these reads.
+    auto compute_tile = [&](int t, auto slot_c) {
+        constexpr int SLOT = decltype(slot_c)::value;
+        static_assert(SLOT * TILE_BYTES + TILE_BYTES <= 65536, "ds offset range");
+        const uint32_t lds0 = lds_base + lane * 16;
+        u32x4 afr[TB][DS];
 #pragma unroll
-        for (int q = 0; q < LPT; ++q) dst[q * 256 + tid] = stage[q];
-    };
-
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-    for (int64_t t = 0; t < ntile; ++t) {
-        if (t + 1 < ntile) load_tile(t + 1);
-        const uint8_t* buf = smem + (t & 1) * TILE_BYTES;
+        for (int b = 0; b < TB; ++b)
+#pragma unroll
+            for (int s = 0; s < DS; ++s)
+                asm volatile("ds_read_b128 %0, %1 offset:%2"
+                             : "=v"(afr[b][s])
+                             : "v"(lds0), "i"(SLOT * TILE_BYTES + (b * DS + s) * 1024));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);  // no MFMA hoisted above the wait
+#ifdef NRK_SCREEN_STATS
+        const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
+        f32x16 acc[TB];
 #pragma unroll
         for (int b = 0; b < TB; ++b) {
-            const int64_t blk = t * TB + b;
-            if (blk >= nblk) break;
-            f32x16 acc = {};
+            acc[b] = f32x16{};
 #pragma unroll
-            for (int s = 0; s < DS; ++s) {
-                const uint4 av = *reinterpret_cast<const uint4*>(buf + (b * DS + s) * 1024 + lane * 16);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, av), ufrag[s], acc, 0, 0, 0);
-            }
-            const int64_t row0 = blk * 32;
-            if (row0 + 32 > n_items) {
+            for (int s = 0; s < DS; ++s)
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afr[b][s]), ufrag[s], acc[b], 0, 0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < TB; ++b) {
+            const int blk = t * TB + b;
+            if (blk >= tail_blk) {  // uniform: partial / padding block(s) of the last tile
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int64_t row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (row >= n_items) acc[r] = -INFINITY;
+                    const int row = blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row >= n_items) acc[b][r] = -INFINITY;
                 }
             }
-            float mx = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
+            float mx = fmaxf(fmaxf(acc[b][0], acc[b][1]), acc[b][2]);
 #pragma unroll
-            for (int r = 4; r < 16; r += 4)
-                mx = fmaxf(mx, fmaxf(fmaxf(acc[r], acc[r + 1]), fmaxf(acc[r + 2], acc[r + 3])));
-            if (__ballot(active && mx > tau)) {
-                if (__ballot(active && n >= IP_CL)) lanes_flush(L, n, tau, theta, ovf, k, eps_s, active);
-                if (active && mx > tau && n < IP_CL) {
-                    L.put(n, make_uint2(__float_as_uint(mx), (uint32_t)(blk * 2 + h)));
-                    ++n;
-                }
-            }
+            for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, acc[b][r]), acc[b][r + 1]);
+            mx = fmaxf(mx, acc[b][15]);
+            // inline-asm store: invisible to hipcc's waitcnt pass, which would
+            // otherwise drain the in-flight LDS-DMA before every list append
+            const uint2 ent = make_uint2(__float_as_uint(mx), (uint32_t)(blk * 2 + h));
+            asm volatile("ds_write_b64 %0, %1" ::"v"(list_lds + (uint32_t)n * (WAVE * 8)), "v"(ent)
+                         : "memory");
+            n += (mx > tau) ? 1 : 0;
         }
-        if (t + 1 < ntile) store_tile((t + 1) & 1);
-        __syncthreads();
-    }
+#ifdef NRK_SCREEN_STATS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        st_cyc_slow += __builtin_amdgcn_s_memtime() - c0;  // MFMA + max + append
+#endif
+    };
 
-    lanes_flush(L, n, tau, theta, ovf, k, eps_s, active);
+    // one ring phase: tile t lives in ring slot slot_c (compile-time, so the
+    // fragment reads use immediate offsets)
+    auto phase = [&](int t, auto slot_c) {
+        // tile t landed (this wave's pieces; the younger tiles stay in flight),
+        // then the barrier makes every wave's pieces visible and retires every
+        // read of the slot about to be refilled ((t - 1) % NSLOT)
+#ifdef NRK_SCREEN_STATS
+        const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+#endif
+        if constexpr (NSLOT == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#ifdef NRK_SCREEN_STATS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        st_slow += __builtin_amdgcn_s_memtime() - w0;  // cycles in vmcnt wait + barrier
+#endif
+        issue_tile(t + NSLOT - 1);
+        compute_tile(t, slot_c);
+    };
+#pragma unroll
+    for (int p = 0; p < NSLOT - 1; ++p) issue_tile(p);
+    for (int t = 0;; t += NSLOT) {
+        if (t < ntile) phase(t, std::integral_constant<int, 0>{});
+        if (t + 1 < ntile) phase(t + 1, std::integral_constant<int, 1>{});
+        if constexpr (NSLOT == 3)
+            if (t + 2 < ntile) phase(t + 2, std::integral_constant<int, 2>{});
+        // compaction (one code site; the final pass always compacts): keep
+        // room for the next NSLOT tiles' appends
+        const bool fin = t + NSLOT >= ntile;
+        if (fin || __ballot(active && n > IP_CL - NSLOT * TB)) {
+#ifdef NRK_SCREEN_STATS
+            const unsigned long long st_f0 = __builtin_amdgcn_s_memtime();
+#endif
+            lanes_flush<IP_CL - NSLOT * TB>(L, n, tau, theta, ovf, k, eps_s, active);
+#ifdef NRK_SCREEN_STATS
+            ++st_flush;
+            st_cyc_flush += __builtin_amdgcn_s_memtime() - st_f0;
+#endif
+        }
+        if (fin) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
+
+#ifdef NRK_SCREEN_STATS
+    if (lane == 0) {
+        unsigned long long* st = reinterpret_cast<unsigned long long*>(ovf_list + n_users) +
+                                 8 * ((size_t)blockIdx.x * 4 + wave);
+        st[0] = st_slow;
+        st[1] = st_flush;
+        st[2] = st_cyc_slow;
+        st[3] = st_cyc_flush;
+        st[4] = __builtin_amdgcn_s_memtime() - st_t0;
+    }
+#endif
     const float th_u = fmaxf(theta, __shfl_xor(theta, 32, WAVE));
     const bool ovf_u = ovf || __shfl_xor((int)ovf, 32, WAVE);
     if (!active) return;
     float cut = th_u;
     if (eps_s != 0.0f && th_u != -INFINITY) cut = round_down_sub(th_u, 2.0f * eps_s);
-    int m = 0;
-    uint2* dst = cand + (user * 2 + h) * IP_CW;
+    int mcount = 0;
+    uint2* dst = cand + ((size_t)user * 2 + h) * IP_CW;
     for (int j = 0; j < n; ++j) {
         const uint2 e = L.get(j);
         if (!(__uint_as_float(e.x) >= cut)) continue;
-        if (m < IP_CW) dst[m] = e;
-        ++m;
+        if (mcount < IP_CW) dst[mcount] = e;
+        ++mcount;
     }
-    const bool ovf2 = ovf_u || (m > IP_CW) || __shfl_xor((int)(m > IP_CW), 32, WAVE);
-    cand_cnt[user * 2 + h] = m < IP_CW ? m : IP_CW;
+    const bool ovf2 = ovf_u || (mcount > IP_CW) || __shfl_xor((int)(mcount > IP_CW), 32, WAVE);
+    cand_cnt[user * 2 + h] = mcount < IP_CW ? mcount : IP_CW;
     if (h == 0) {
         // unscaled cut and eps for the refinement (exact power-of-two rescale)
         ucut[user] = make_float2(cut == -INFINITY ? -INFINITY : cut / scl, eps);
         ovf_flag[user] = ovf2 ? 1 : 0;
-        if (ovf2) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)user;
+        if (ovf2) ovf_list[atomicAdd(ovf_count, 1)] = user;
     }
 }
 
@@ -415,9 +509,8 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         int32_t row = 0;
         if (idx < nitem) {
             const int b = idx >> 4, r = idx & 15;
-            const uint32_t lb = (b < n0) ? cand[(2 * u) * IP_CW + b].y : cand[(2 * u + 1) * IP_CW + (b - n0)].y;
-            const int64_t blk = lb >> 1, hh = lb & 1;
-            const int64_t rr = blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const uint32_t q = (b < n0) ? cand[(2 * u) * IP_CW + b].y : cand[(2 * u + 1) * IP_CW + (b - n0)].y;
+            const int64_t rr = (int64_t)(q >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (q & 1);
             if (rr < n_items) {
                 row = (int32_t)rr;
                 s = exact_dot(uv, items + rr * dim, dim);
@@ -674,10 +767,10 @@ size_t nrk_ip_topk_workspace_bytes(int64_t n_users, int64_t n_items, int dim, in
 static int ip_check(const float* users, int64_t n_users, const float* items, const void* catalog,
                     int64_t n_items, int dim, int k, void* workspace, size_t workspace_bytes) {
     NRK_REQUIRE(n_users >= 0 && n_items >= 0, "negative sizes");
-    NRK_REQUIRE(n_items < INT32_MAX, "n_items must fit int32 rows");
+    NRK_REQUIRE(n_items < (1ll << 30) && n_users < (1ll << 30), "n_items / n_users must be < 2^30");
     NRK_REQUIRE(dim > 0 && dim <= 256, "dim must be in [1, 256]");
     NRK_REQUIRE(k >= 1, "k must be >= 1");
-    if (k > IP_KMAX) NRK_UNSUPPORTED("k > 40 is not compiled");
+    if (k > IP_KMAX) NRK_UNSUPPORTED("k > 32 is not compiled");
     if (n_users == 0) return NRK_OK;
     NRK_REQUIRE(users && workspace, "null pointer");
     NRK_REQUIRE(n_items == 0 || (items && catalog), "items/catalog null");
@@ -707,7 +800,7 @@ int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog,
         (void)hipMemsetAsync(w.ovf_flag, 0, (size_t)n_users * sizeof(int32_t), s);
     } else {
 #define NRK_SCREEN(DPV)                                                                     \
-    ip_screen_kernel<DPV><<<grid, 256, 0, s>>>(users, n_users, cat, n_items, dim, k, w.cand, \
+    ip_screen_kernel<DPV><<<grid, 256, 0, s>>>(users, (int)n_users, cat, (int)n_items, dim, k, w.cand, \
                                               w.cnt, w.ucut, w.ovf_flag, w.ovf_list, w.ovf_count)
         switch (dp) {
             case 16: NRK_SCREEN(16); break;

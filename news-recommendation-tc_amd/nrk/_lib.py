@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnrk.so")
+# NRK_LIB_PATH: developer override (e.g. the instrumented build under build_stats/)
+LIB_PATH = os.environ.get("NRK_LIB_PATH") or os.path.join(_HERE, "libnrk.so")
 
 NRK_OK, NRK_EINVAL, NRK_EHIP, NRK_EUNSUPPORTED = 0, 1, 2, 3
 

@@ -108,8 +108,8 @@ def ip_topk(users, catalog: Catalog, k: int, row_offset: int = 0, exact: bool = 
     _need(users, torch.float32, name="users")
     if users.dim() != 2 or users.shape[1] != catalog.d:
         raise ValueError(f"users must be [n, {catalog.d}]")
-    if not (1 <= k <= 40):
-        raise ValueError("k must be in [1, 40]")
+    if not (1 <= k <= 32):
+        raise ValueError("k must be in [1, 32]")
     n = users.shape[0]
     dev = users.device
     s = torch.empty((n, k), dtype=torch.float32, device=dev)

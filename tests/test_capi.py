@@ -45,5 +45,5 @@ def test_argument_errors_raise_valueerror():
     assert b"k must be" in L.nrk_last_error()
     with pytest.raises(ValueError):
         _lib.check(rc, "nrk_ip_topk")
-    rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, 64, 0, None, None, None, None, 0, None)
+    rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, 33, 0, None, None, None, None, 0, None)
     assert rc == _lib.NRK_EUNSUPPORTED

@@ -65,7 +65,7 @@ def _unit(x):
         (3, 31, 32, 31),
         (129, 33, 32, 31),
         (300, 1000, 32, 31),
-        (257, 5003, 32, 40),
+        (257, 5003, 32, 32),
         (130, 4097, 16, 10),
         (70, 3000, 50, 21),
         (200, 2500, 64, 31),
