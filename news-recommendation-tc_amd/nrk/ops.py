@@ -162,3 +162,94 @@ def ip_topk_finish(users, catalog: Catalog, k: int, workspace, out_scores, out_r
     _lib.call("nrk_ip_topk_finish", _ptr(users), n, _ptr(catalog.items), catalog.n, catalog.d, k,
               int(row_offset), _ptr(out_scores), _ptr(out_rows), _ptr(out_exact), _ptr(workspace),
               workspace.numel(), _stream())
+
+
+# -------------------------------------------------------------------- DIN --
+class DinParams:
+    """Device-resident DIN weights in kernel layout (DINModel state_dict,
+    DIN.py:133-212): concatenated embedding table (fp32 or bf16 storage),
+    per-feature row offsets, prepared attention matrices and the MLP."""
+
+    def __init__(self, state_dict, user_feats, item_feats, ctx_feats, table_dtype="fp32",
+                 device="cuda"):
+        import numpy as np
+
+        def arr(k):
+            v = state_dict[k]
+            v = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
+            return np.ascontiguousarray(v, dtype=np.float32)
+
+        groups = ([("user_profile_embedding_dict", f) for f in user_feats]
+                  + [("item_embedding_dict", f) for f in item_feats]
+                  + [("context_embedding_dict", f) for f in ctx_feats])
+        tabs = [arr(f"{g}.{f}.weight") for g, f in groups]
+        for t in tabs:
+            if t.shape[1] != 32:
+                raise NotImplementedError("the DIN kernels are compiled for embedding dim 32")
+        base = np.cumsum([0] + [t.shape[0] for t in tabs[:-1]]).astype(np.int64)
+        table = torch.from_numpy(np.concatenate(tabs, 0))
+        if table_dtype == "bf16":
+            self.table = table.to(torch.bfloat16).to(device).contiguous()
+            self.table_code = 1
+        elif table_dtype == "fp32":
+            self.table = table.to(device).contiguous()
+            self.table_code = 0
+        else:
+            raise ValueError("table_dtype must be 'fp32' or 'bf16'")
+        self.row_base = torch.from_numpy(base).to(device)
+        self.vocab = [t.shape[0] for t in tabs]
+        self.n_user, self.n_item, self.n_ctx = len(user_feats), len(item_feats), len(ctx_feats)
+        d = lambda k: torch.from_numpy(arr(k)).to(device).contiguous()  # noqa: E731
+        self.att_w0 = d("activation_unit.mlp.0.weight")
+        self.att_b0 = d("activation_unit.mlp.0.bias")
+        self.att_w1 = d("activation_unit.mlp.2.weight").reshape(-1).contiguous()
+        self.att_b1 = d("activation_unit.mlp.2.bias")
+        self.mlp_w0, self.mlp_b0 = d("mlp.0.weight"), d("mlp.0.bias")
+        self.mlp_w1, self.mlp_b1 = d("mlp.2.weight"), d("mlp.2.bias")
+        self.mlp_w2 = d("mlp.4.weight").reshape(-1).contiguous()
+        self.mlp_b2 = d("mlp.4.bias")
+        self.h1, self.h2 = self.mlp_w0.shape[0], self.mlp_w1.shape[0]
+        in_dim = 32 * (self.n_user + self.n_ctx + 2 * self.n_item)
+        if self.att_w0.shape != (36, 4 * 32 * self.n_item) or self.mlp_w0.shape[1] != in_dim:
+            raise ValueError("state_dict shapes do not match the feature lists")
+        nb = _lib.lib().nrk_din_prep_bytes(self.n_item)
+        self.prep = torch.empty(nb, dtype=torch.uint8, device=device)
+        _lib.call("nrk_din_prepare", _ptr(self.att_w0), self.n_item, _ptr(self.prep), _stream())
+
+
+def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspace=None):
+    """One DIN batch (B >= 2): int32 index tensors user [B,Fu], item [B,Fi],
+    hist [B,T,Fi], ctx [B,Fc], mask [B,T] f32 -> probs [B] (+ logits)."""
+    _dev(user, item, hist, ctx, mask)
+    B, T = mask.shape
+    _need(user, torch.int32, (B, p.n_user), "user")
+    _need(item, torch.int32, (B, p.n_item), "item")
+    _need(hist, torch.int32, (B, T, p.n_item), "hist")
+    _need(ctx, torch.int32, (B, p.n_ctx), "ctx")
+    _need(mask, torch.float32, (B, T), "mask")
+    for t, off in ((user, 0), (item, p.n_user), (ctx, p.n_user + p.n_item)):
+        if t.numel():
+            mx = t.amax(0).cpu().tolist()
+            mn = int(t.min())
+            if mn < 0 or any(m >= p.vocab[off + f] for f, m in enumerate(mx)):
+                raise ValueError("feature index out of its embedding table")
+    if hist.numel():
+        mx = hist.reshape(-1, p.n_item).amax(0).cpu().tolist()
+        if int(hist.min()) < 0 or any(m >= p.vocab[p.n_user + f] for f, m in enumerate(mx)):
+            raise ValueError("history index out of its embedding table")
+    probs = torch.empty(B, dtype=torch.float32, device=mask.device)
+    lg = torch.empty(B, dtype=torch.float32, device=mask.device) if logits else None
+    nb = _lib.lib().nrk_din_workspace_bytes(B, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
+    if workspace is None or workspace.numel() < nb:
+        workspace = torch.empty(nb, dtype=torch.uint8, device=mask.device)
+    _lib.call("nrk_din_forward", _ptr(p.table), p.table_code, _ptr(p.row_base), p.n_user, p.n_item,
+              p.n_ctx, _ptr(user), _ptr(item), _ptr(hist), _ptr(ctx), _ptr(mask), B, T,
+              _ptr(p.prep), _ptr(p.att_b0), _ptr(p.att_w1), _ptr(p.att_b1), _ptr(p.mlp_w0),
+              _ptr(p.mlp_b0), p.h1, _ptr(p.mlp_w1), _ptr(p.mlp_b1), p.h2, _ptr(p.mlp_w2),
+              _ptr(p.mlp_b2), _ptr(probs), _ptr(lg), _ptr(workspace), workspace.numel(), _stream())
+    return (probs, lg) if logits else probs
+
+
+def din_workspace(p: DinParams, B, T, device):
+    nb = _lib.lib().nrk_din_workspace_bytes(B, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
+    return torch.empty(nb, dtype=torch.uint8, device=device)

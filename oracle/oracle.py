@@ -222,7 +222,8 @@ def din_forward(sd, user, item, hist, ctx, mask, feats, round_bf16=False):
     U = np.concatenate([tab("user_profile_embedding_dict", f)[user[:, n]] for n, f in enumerate(uf)], 1)
     Q = np.concatenate([tab("item_embedding_dict", f)[item[:, n]] for n, f in enumerate(itf)], 1)
     K = np.concatenate([tab("item_embedding_dict", f)[hist[:, :, n]] for n, f in enumerate(itf)], 2)
-    C = np.concatenate([tab("context_embedding_dict", f)[ctx[:, n]] for n, f in enumerate(cf)], 1)
+    C = (np.concatenate([tab("context_embedding_dict", f)[ctx[:, n]] for n, f in enumerate(cf)], 1)
+         if len(cf) else np.zeros((len(user), 0), f32))
     B, T, d = K.shape
     q = np.broadcast_to(Q[:, None, :], (B, T, d))
     X = np.concatenate([K, q, q - K, q * K], 2).astype(f32)

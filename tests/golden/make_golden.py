@@ -439,6 +439,15 @@ def gen_din_encode(tmp):
         enc[f] = le
     ds = DINDataset(main, upd, ifd, uhd, USER_FEATS, ITEM_FEATS, CTX_FEATS, "label", enc)
     b = collate_fn([ds[i] for i in range(len(ds))], seq_max_len=T)
+    # Second case: context columns held as strings -> main_df.iloc[i] is an
+    # object row, user_id/item_id stay ints and str() finds the dict keys.
+    # (In the float case above the row is upcast to float64, str(user_id) is
+    # "1013.0" and every user/item/history feature encodes to 0.)
+    main_obj = main.copy()
+    for f in CTX_FEATS:
+        main_obj[f] = main_obj[f].astype(str)
+    ds2 = DINDataset(main_obj, upd, ifd, uhd, USER_FEATS, ITEM_FEATS, CTX_FEATS, "label", enc)
+    b2 = collate_fn([ds2[i] for i in range(len(ds2))], seq_max_len=T)
     out = {
         "main_user": main["user_id"].to_numpy(np.int64),
         "main_item": main["item_id"].to_numpy(np.int64),
@@ -458,6 +467,11 @@ def gen_din_encode(tmp):
         "out_ctx": np.stack([b["context"][f].numpy() for f in CTX_FEATS], 1),
         "out_mask": b["history_mask"].numpy(),
         "out_labels": b["labels"].numpy(),
+        "obj_user": np.stack([b2["user_profile"][f].numpy() for f in USER_FEATS], 1),
+        "obj_item": np.stack([b2["recall_item"][f].numpy() for f in ITEM_FEATS], 1),
+        "obj_hist": np.stack([b2["history_items"][f].numpy() for f in ITEM_FEATS], 2),
+        "obj_ctx": np.stack([b2["context"][f].numpy() for f in CTX_FEATS], 1),
+        "obj_mask": b2["history_mask"].numpy(),
     }
     for f in USER_FEATS + ITEM_FEATS + CTX_FEATS:
         out[f"classes::{f}"] = np.array([str(c) for c in enc[f].classes_])

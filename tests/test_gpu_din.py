@@ -1,0 +1,181 @@
+"""GPU parity: DIN forward (src/rank/DIN.py:29-212 DINModel.forward in eval
+mode) through the C ABI (nrk_din_forward).
+
+Checker: the reference's own outputs (tests/golden/din_small.npz, fp32
+tables) and the CPU oracle (oracle.din_forward) for other shapes and for
+bf16-stored tables.  Tolerance: 1e-5 on probabilities and logits (the
+north_star floating-point bar; absolute, plus 1e-5 relative for logits).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _sd(g):
+    return {k[4:]: g[k] for k in g.files if k.startswith("sd::")}
+
+
+def _feats(g):
+    return [list(map(str, g[k])) for k in ("user_feats", "item_feats", "ctx_feats")]
+
+
+def _run(sd, feats, batch, table_dtype="fp32"):
+    from nrk import ops
+
+    p = ops.DinParams(sd, *feats, table_dtype=table_dtype, device="cuda")
+    d = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to("cuda", dt)  # noqa: E731
+    probs, lg = ops.din_forward(p, d(batch["user"], torch.int32), d(batch["item"], torch.int32),
+                                d(batch["hist"], torch.int32), d(batch["ctx"], torch.int32),
+                                d(batch["mask"], torch.float32), logits=True)
+    torch.cuda.synchronize()
+    return probs.cpu().numpy(), lg.cpu().numpy()
+
+
+def _batch(g, tag):
+    return {k: g[f"{tag}_{k}"].astype(np.int64 if k != "mask" else np.float32)
+            for k in ("user", "item", "hist", "ctx", "mask")}
+
+
+@pytest.mark.parametrize("tag", ["b512", "b4096", "b37"])
+def test_din_golden(golden, tag):
+    g = golden("din_small")
+    probs, lg = _run(_sd(g), _feats(g), _batch(g, tag))
+    np.testing.assert_allclose(probs, g[f"{tag}_probs"], atol=TOL, rtol=0)
+    np.testing.assert_allclose(lg, g[f"{tag}_logits"], atol=TOL, rtol=TOL)
+
+
+@pytest.mark.parametrize("tag", ["b512", "b37"])
+def test_din_bf16_tables_vs_oracle(golden, tag):
+    g = golden("din_small")
+    sd, feats, b = _sd(g), _feats(g), _batch(g, tag)
+    probs, lg = _run(sd, feats, b, table_dtype="bf16")
+    po, lo, _ = oracle.din_forward(sd, b["user"], b["item"], b["hist"], b["ctx"], b["mask"], feats,
+                                   round_bf16=True)
+    np.testing.assert_allclose(probs, po, atol=TOL, rtol=0)
+    np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
+
+
+def synth_model(rng, vocab_u, vocab_i, vocab_c, h1=200, h2=80, scale=0.05):
+    """Random DINModel-shaped state_dict (DIN.py:133-212 parameter names)."""
+    f32 = np.float32
+    uf = [f"u{n}" for n in range(len(vocab_u))]
+    itf = [f"i{n}" for n in range(len(vocab_i))]
+    cf = [f"c{n}" for n in range(len(vocab_c))]
+    sd = {}
+    for grp, names, voc in (("user_profile_embedding_dict", uf, vocab_u),
+                            ("item_embedding_dict", itf, vocab_i),
+                            ("context_embedding_dict", cf, vocab_c)):
+        for f, v in zip(names, voc):
+            sd[f"{grp}.{f}.weight"] = (rng.standard_normal((v, 32)) * 0.1).astype(f32)
+    ni = len(itf)
+    in_dim = 32 * (len(uf) + len(cf) + 2 * ni)
+    lin = lambda o, i: (rng.standard_normal((o, i)) * (scale * 8 / np.sqrt(i))).astype(f32)  # noqa: E731
+    sd["activation_unit.mlp.0.weight"] = lin(36, 128 * ni)
+    sd["activation_unit.mlp.0.bias"] = (rng.standard_normal(36) * 0.1).astype(f32)
+    sd["activation_unit.mlp.2.weight"] = lin(1, 36)
+    sd["activation_unit.mlp.2.bias"] = np.array([0.1], f32)
+    sd["mlp.0.weight"], sd["mlp.0.bias"] = lin(h1, in_dim), (rng.standard_normal(h1) * 0.1).astype(f32)
+    sd["mlp.2.weight"], sd["mlp.2.bias"] = lin(h2, h1), (rng.standard_normal(h2) * 0.1).astype(f32)
+    sd["mlp.4.weight"], sd["mlp.4.bias"] = lin(1, h2), np.array([-0.2], f32)
+    return sd, (uf, itf, cf)
+
+
+def synth_batch(rng, B, T, vocab_u, vocab_i, vocab_c, p_empty=0.05):
+    L = rng.integers(0, T + 1, B)
+    L[rng.random(B) < p_empty] = 0
+    mask = (np.arange(T)[None] < L[:, None]).astype(np.float32)
+    hist = np.stack([rng.integers(0, v, (B, T)) for v in vocab_i], 2) * mask[:, :, None].astype(np.int64)
+    return {
+        "user": np.stack([rng.integers(0, v, B) for v in vocab_u], 1),
+        "item": np.stack([rng.integers(0, v, B) for v in vocab_i], 1),
+        "hist": hist,
+        "ctx": np.stack([rng.integers(0, v, B) for v in vocab_c], 1) if vocab_c else np.zeros((B, 0), np.int64),
+        "mask": mask,
+    }
+
+
+@pytest.mark.parametrize(
+    "B,T,n_item,n_ctx,h1,h2",
+    [
+        (2, 1, 4, 16, 200, 80),
+        (3, 50, 4, 16, 200, 80),
+        (100, 7, 1, 0, 64, 32),
+        (257, 128, 2, 3, 128, 64),
+        (1000, 50, 4, 11, 200, 80),
+        (5000, 33, 4, 16, 256, 100),
+    ],
+)
+@pytest.mark.parametrize("table_dtype", ["fp32", "bf16"])
+def test_din_vs_oracle(B, T, n_item, n_ctx, h1, h2, table_dtype):
+    rng = np.random.default_rng(B * 131 + T)
+    vu, vi, vc = [50, 300, 7, 2000, 90], [60, 900, 5000, 70][:n_item], [12] * n_ctx
+    sd, feats = synth_model(rng, vu, vi, vc, h1, h2)
+    b = synth_batch(rng, B, T, vu, vi, vc)
+    probs, lg = _run(sd, feats, b, table_dtype)
+    po, lo, _ = oracle.din_forward(sd, b["user"], b["item"], b["hist"], b["ctx"], b["mask"], feats,
+                                   round_bf16=table_dtype == "bf16")
+    np.testing.assert_allclose(probs, po, atol=TOL, rtol=0)
+    np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
+
+
+def test_din_all_history_masked():
+    rng = np.random.default_rng(5)
+    vu, vi, vc = [50, 300], [60, 900, 5000, 70], [12, 12]
+    sd, feats = synth_model(rng, vu, vi, vc)
+    b = synth_batch(rng, 64, 50, vu, vi, vc, p_empty=1.0)
+    probs, lg = _run(sd, feats, b)
+    po, lo, _ = oracle.din_forward(sd, b["user"], b["item"], b["hist"], b["ctx"], b["mask"], feats)
+    np.testing.assert_allclose(probs, po, atol=TOL, rtol=0)
+
+
+def test_din_errors():
+    from nrk import ops
+
+    rng = np.random.default_rng(1)
+    vu, vi, vc = [50], [60, 900, 5000, 70], [12]
+    sd, feats = synth_model(rng, vu, vi, vc)
+    b = synth_batch(rng, 8, 10, vu, vi, vc)
+    b["item"][3, 2] = 5000  # out of the table
+    with pytest.raises(ValueError):
+        _run(sd, feats, b)
+    p = ops.DinParams(sd, *feats, device="cuda")
+    one = {k: torch.from_numpy(np.ascontiguousarray(v[:1])).cuda() for k, v in b.items()}
+    with pytest.raises(ValueError):  # batch of one: Dice std undefined, rejected at the boundary
+        ops.din_forward(p, one["user"].int(), one["item"].int(), one["hist"].int(),
+                        one["ctx"].int(), one["mask"].float())
+
+
+def test_din_config3_batch():
+    """Config 3 shapes: B=4096, T=50, Tianchi-sized vocabularies, bf16 tables."""
+    rng = np.random.default_rng(3)
+    vu, vi, vc = [200, 5000, 6, 200000, 3000], [462, 3000, 300000, 1500], [11] * 16
+    sd, feats = synth_model(rng, vu, vi, vc)
+    b = synth_batch(rng, 4096, 50, vu, vi, vc)
+    probs, lg = _run(sd, feats, b, "bf16")
+    po, lo, _ = oracle.din_forward(sd, b["user"], b["item"], b["hist"], b["ctx"], b["mask"], feats,
+                                   round_bf16=True)
+    np.testing.assert_allclose(probs, po, atol=TOL, rtol=0)
+    np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
+
+
+def test_din_ranker_predict_batches(golden):
+    """DINRanker.predict batching: short last batch scored with its own
+    statistics; a trailing batch of one row is NaN as in the reference."""
+    from nrk.rank.din import DINScorer
+
+    g = golden("din_small")
+    sd, feats, b = _sd(g), _feats(g), _batch(g, "b512")
+    sc = DINScorer(sd, *feats)
+    out = sc.predict(b, 100)
+    for s in range(0, 512, 100):
+        e = min(512, s + 100)
+        po, _, _ = oracle.din_forward(sd, *(b[k][s:e] for k in ("user", "item", "hist", "ctx", "mask")),
+                                      feats)
+        np.testing.assert_allclose(out[s:e], po, atol=TOL, rtol=0)
+    out2 = sc.predict({k: v[:201] for k, v in b.items()}, 100)
+    assert np.isnan(out2[200]) and not np.isnan(out2[:200]).any()
