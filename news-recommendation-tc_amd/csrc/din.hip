@@ -124,15 +124,23 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
 
 // ---------------------------------------------------------- 2. col stats --
 // mean and unbiased std (torch.std default) of each column over the batch,
-// from per-block fp64 (sum, sumsq) partials summed in block order.
-__global__ void col_stats_kernel(const double* __restrict__ partial, int nblk, int ncol,
-                                 int64_t B, float2* __restrict__ stats) {
-    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < ncol; c += gridDim.x * blockDim.x) {
-        double s = 0.0, ss = 0.0;
-        for (int k = 0; k < nblk; ++k) {
-            s += partial[((size_t)k * ncol + c) * 2];
-            ss += partial[((size_t)k * ncol + c) * 2 + 1];
-        }
+// from per-block fp64 (sum, sumsq) partials.  One wave per column: lane l
+// sums partials l, l+64, ... in order, then a fixed butterfly -- the same
+// order on every run (bitwise reproducible).
+__global__ __launch_bounds__(256) void col_stats_kernel(const double* __restrict__ partial, int nblk,
+                                                        int ncol, int64_t B, float2* __restrict__ stats) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= ncol) return;
+    double s = 0.0, ss = 0.0;
+    for (int k = lane; k < nblk; k += WAVE) {
+        const double2 v = *reinterpret_cast<const double2*>(partial + ((size_t)k * ncol + c) * 2);
+        s += v.x;
+        ss += v.y;
+    }
+    s = wave_sum_f64(s);
+    ss = wave_sum_f64(ss);
+    if (lane == 0) {
         const double mean = s / (double)B;
         double var = (ss - s * mean) / (double)(B - 1);
         if (var < 0.0) var = 0.0;
@@ -439,7 +447,7 @@ int nrk_din_forward(const void* table, int table_dtype, const int64_t* row_base,
     }
 #undef NRK_ATT_H
     const int ncol_att = T * DIN_H;
-    col_stats_kernel<<<(ncol_att + 255) / 256, 256, 0, s>>>(w.hpart, nb_att, ncol_att, batch, w.hstats);
+    col_stats_kernel<<<(ncol_att + 3) / 4, 256, 0, s>>>(w.hpart, nb_att, ncol_att, batch, w.hstats);
     const int gb = (int)((batch + 3) / 4);
     if (table_dtype == 0)
         din_att_out_kernel<float><<<gb, 256, 0, s>>>(
@@ -452,10 +460,10 @@ int nrk_din_forward(const void* table, int table_dtype, const int64_t* row_base,
     const int nb_m = (int)((batch + 63) / 64);
     din_gemm_kernel<false><<<dim3(nb_m, (h1 + 63) / 64), 256, 0, s>>>(
         w.mlp_in, nullptr, mlp_w0, mlp_b0, batch, h1, IN, w.z1, w.z1part);
-    col_stats_kernel<<<(h1 + 255) / 256, 256, 0, s>>>(w.z1part, nb_m, h1, batch, w.z1stats);
+    col_stats_kernel<<<(h1 + 3) / 4, 256, 0, s>>>(w.z1part, nb_m, h1, batch, w.z1stats);
     din_gemm_kernel<true><<<dim3(nb_m, (h2 + 63) / 64), 256, 0, s>>>(
         w.z1, w.z1stats, mlp_w1, mlp_b1, batch, h2, h1, w.z2, w.z2part);
-    col_stats_kernel<<<(h2 + 255) / 256, 256, 0, s>>>(w.z2part, nb_m, h2, batch, w.z2stats);
+    col_stats_kernel<<<(h2 + 3) / 4, 256, 0, s>>>(w.z2part, nb_m, h2, batch, w.z2stats);
     din_head_kernel<<<gb, 256, 0, s>>>(w.z2, w.z2stats, batch, h2, mlp_w2, mlp_b2, out_probs,
                                        out_logits);
     NRK_CHECK_LAUNCH();

@@ -1,0 +1,522 @@
+// itemcf.hip -- ItemCF co-occurrence similarity on gfx950.
+//
+// Reference: ItemCFSimilarity.calculate, src/similarity/item_cf.py:17-89,
+// weights from src/utils/weights.py:7-60 (time_decay_weight, log_penalty);
+// top-n per item: ItemCFRecaller._precompute_topk_similar_items,
+// src/recall/itemcf_recaller.py:41-54.
+//
+// The reference walks users in dict order, then (loc1, loc2) and does
+// S[i][j] += w.  Every ordered position pair (u, loc1, loc2) therefore has a
+// global sequence number ("slot") = pair_off[u] + loc1 * L_u + loc2, and the
+// reference's fp64 sum for (i, j) is the sum of its pair weights in slot
+// order.  The GPU reproduces exactly that order without a hash table:
+//   1. cf_pairs        one wave per user: weight w[slot] and key
+//                      (i << b | j) per slot (i == j -> sentinel), item_cnt.
+//   2. LSD radix sort  of (key, slot) -- stable, so equal keys keep slot
+//                      order (rs_upsweep / rs_scan_rows / rs_downsweep,
+//                      8 bits per pass, 2b bits total).
+//   3. cf_emit         one entry per distinct key: sequential fp64 sum of
+//                      w[slot] in slot order, / sqrt(cnt_i * cnt_j), and the
+//                      first slot (= dict insertion order, the reference's
+//                      stable-sort tie-break).
+// Memory-bound integer/byte work: no MFMA; tiles of 4096 keys per 256-thread
+// workgroup, coalesced 16-element strips.
+#include "nrk_common.h"
+
+namespace nrk {
+
+constexpr int RS_THREADS = 256;
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys per workgroup
+
+// ------------------------------------------------------ pair offsets --
+// pair_off[u] = sum_{v<u} L_v^2 (exclusive), pair_off[n] = total.  One
+// workgroup of 1024 threads: contiguous chunks, block scan of chunk sums.
+__global__ __launch_bounds__(1024) void cf_pair_offsets_kernel(const int64_t* __restrict__ offsets,
+                                                               int64_t n, int64_t* __restrict__ pair_off) {
+    __shared__ int64_t part[1024];
+    const int tid = threadIdx.x;
+    const int64_t chunk = (n + 1023) / 1024;
+    const int64_t a = tid * chunk, e = a + chunk < n ? a + chunk : n;
+    int64_t s = 0;
+    for (int64_t u = a; u < e; ++u) {
+        const int64_t L = offsets[u + 1] - offsets[u];
+        s += L * L;
+    }
+    part[tid] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int64_t v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int64_t run = part[tid] - s;  // exclusive
+    for (int64_t u = a; u < e; ++u) {
+        pair_off[u] = run;
+        const int64_t L = offsets[u + 1] - offsets[u];
+        run += L * L;
+    }
+    if (tid == 1023) pair_off[n] = part[1023];
+}
+
+// ------------------------------------------------------------- 1. pairs --
+struct CfParams {
+    double loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha;
+};
+
+__global__ __launch_bounds__(256) void cf_pairs_kernel(
+    const int64_t* __restrict__ offsets, int64_t n_users, const int32_t* __restrict__ items,
+    const int64_t* __restrict__ ts, const double* __restrict__ created,
+    const int64_t* __restrict__ pair_off, CfParams prm, int bj, uint64_t sentinel,
+    uint64_t* __restrict__ keys, int32_t* __restrict__ vals, double* __restrict__ w,
+    unsigned long long* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < n_users; u += nw) {
+        const int64_t b = offsets[u];
+        const int64_t L = offsets[u + 1] - b;
+        const int64_t base = pair_off[u];
+        // user_penalty = 1 / log_penalty(len) = 1 / log(L + 1) (item_cf.py:69-71)
+        const double pen = 1.0 / log((double)(L + 1));
+        for (int64_t l = lane; l < L; l += 64) atomicAdd(&cnt[items[b + l]], 1ull);
+        for (int64_t s = lane; s < L * L; s += 64) {
+            const int64_t l1 = s / L, l2 = s - l1 * L;
+            const int32_t i = items[b + l1], j = items[b + l2];
+            uint64_t key = sentinel;
+            double wt = 0.0;
+            if (i != j) {
+                const double la = l2 > l1 ? prm.loc_alpha : prm.loc_alpha_rev;
+                const int64_t dl = (l2 > l1 ? l2 - l1 : l1 - l2) - 1;
+                const double loc_w = la * pow(prm.loc_beta, (double)dl);
+                const int64_t ti = ts[b + l1], tj = ts[b + l2];
+                const int64_t dt = ti > tj ? ti - tj : tj - ti;
+                const double click_w = exp(pow(prm.time_alpha, (double)dt));
+                const double created_w = exp(pow(prm.created_alpha, fabs(created[i] - created[j])));
+                wt = loc_w * click_w * created_w * pen;
+                key = ((uint64_t)(uint32_t)i << bj) | (uint32_t)j;
+            }
+            keys[base + s] = key;
+            vals[base + s] = (int32_t)(base + s);
+            w[base + s] = wt;
+        }
+    }
+}
+
+// ------------------------------------------------------- 2. radix sort --
+// Stable LSD radix sort of (u64 key, i32 value), 8 bits per pass.
+// counts is digit-major [256][nblk] so each digit's row scans contiguously.
+__global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const uint64_t* __restrict__ keys, int64_t n,
+                                                        int shift, int nblk,
+                                                        uint32_t* __restrict__ counts) {
+    __shared__ uint32_t hist[256];
+    const int tid = threadIdx.x;
+    hist[tid] = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const int64_t e = t0 + r * RS_THREADS + tid;
+        if (e < n) atomicAdd(&hist[(keys[e] >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    counts[(size_t)tid * nblk + blockIdx.x] = hist[tid];
+}
+
+// One workgroup per digit: exclusive scan of its row in place + row total.
+__global__ __launch_bounds__(256) void rs_scan_rows(uint32_t* __restrict__ counts, int nblk,
+                                                   uint32_t* __restrict__ totals) {
+    __shared__ uint32_t part[256];
+    const int tid = threadIdx.x;
+    uint32_t* row = counts + (size_t)blockIdx.x * nblk;
+    const int chunk = (nblk + 255) / 256;
+    const int a = tid * chunk, e = a + chunk < nblk ? a + chunk : nblk;
+    uint32_t s = 0;
+    for (int k = a; k < e; ++k) s += row[k];
+    part[tid] = s;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        const uint32_t v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[tid] - s;
+    for (int k = a; k < e; ++k) {
+        const uint32_t c = row[k];
+        row[k] = run;
+        run += c;
+    }
+    if (tid == 255) totals[blockIdx.x] = part[255];
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int lane = threadIdx.x & 63;
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__global__ __launch_bounds__(RS_THREADS) void rs_downsweep(
+    const uint64_t* __restrict__ kin, const int32_t* __restrict__ vin, uint64_t* __restrict__ kout,
+    int32_t* __restrict__ vout, int64_t n, int shift, int nblk, const uint32_t* __restrict__ counts,
+    const uint32_t* __restrict__ totals) {
+    __shared__ uint32_t base[256];
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wc[4][256];
+    const int tid = threadIdx.x, wv = tid >> 6;
+    // digit base = exclusive scan of totals + this block's offset in the row
+    {
+        const uint32_t t = totals[tid];
+        base[tid] = t;
+        __syncthreads();
+        for (int d = 1; d < 256; d <<= 1) {
+            const uint32_t v = tid >= d ? base[tid - d] : 0;
+            __syncthreads();
+            base[tid] += v;
+            __syncthreads();
+        }
+        const uint32_t excl = base[tid] - t;
+        __syncthreads();
+        base[tid] = excl + counts[(size_t)tid * nblk + blockIdx.x];
+        run[tid] = 0;
+    }
+    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wc[k][tid] = 0;
+        const int64_t e = t0 + r * RS_THREADS + tid;
+        const bool ok = e < n;
+        uint64_t key = 0;
+        int32_t val = 0;
+        if (ok) {
+            key = kin[e];
+            val = vin[e];
+        }
+        const uint32_t d = (uint32_t)(key >> shift) & 255u;
+        uint64_t m = __ballot(ok);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const bool on = (d >> bit) & 1u;
+            const uint64_t bb = __ballot(on);
+            m &= on ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+        __syncthreads();
+        if (ok && rank == 0) wc[wv][d] = (uint32_t)__popcll(m);
+        __syncthreads();
+        {
+            const uint32_t c0 = wc[0][tid], c1 = wc[1][tid], c2 = wc[2][tid], c3 = wc[3][tid];
+            const uint32_t r0 = run[tid];
+            wc[0][tid] = r0;
+            wc[1][tid] = r0 + c0;
+            wc[2][tid] = r0 + c0 + c1;
+            wc[3][tid] = r0 + c0 + c1 + c2;
+            run[tid] = r0 + c0 + c1 + c2 + c3;
+        }
+        __syncthreads();
+        if (ok) {
+            const uint32_t pos = base[d] + wc[wv][d] + rank;
+            kout[pos] = key;
+            vout[pos] = val;
+        }
+    }
+}
+
+// -------------------------------------------------------------- 3. emit --
+__device__ __forceinline__ bool cf_head(const uint64_t* keys, int64_t e, uint64_t sentinel) {
+    const uint64_t k = keys[e];
+    return k != sentinel && (e == 0 || keys[e - 1] != k);
+}
+
+__global__ __launch_bounds__(RS_THREADS) void cf_head_count(const uint64_t* __restrict__ keys, int64_t n,
+                                                          uint64_t sentinel, uint32_t* __restrict__ blkcnt) {
+    __shared__ uint32_t c;
+    if (threadIdx.x == 0) c = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    uint32_t my = 0;
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const int64_t e = t0 + r * RS_THREADS + threadIdx.x;
+        if (e < n && cf_head(keys, e, sentinel)) ++my;
+    }
+    atomicAdd(&c, my);
+    __syncthreads();
+    if (threadIdx.x == 0) blkcnt[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(1024) void cf_head_scan(const uint32_t* __restrict__ blkcnt, int nblk,
+                                                   uint32_t* __restrict__ blkoff, int64_t* __restrict__ out_n) {
+    __shared__ uint32_t part[1024];
+    const int tid = threadIdx.x;
+    const int chunk = (nblk + 1023) / 1024;
+    const int a = tid * chunk, e = a + chunk < nblk ? a + chunk : nblk;
+    uint32_t s = 0;
+    for (int k = a; k < e; ++k) s += blkcnt[k];
+    part[tid] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const uint32_t v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[tid] - s;
+    for (int k = a; k < e; ++k) {
+        blkoff[k] = run;
+        run += blkcnt[k];
+    }
+    if (tid == 1023) *out_n = part[1023];
+}
+
+__global__ __launch_bounds__(RS_THREADS) void cf_emit(
+    const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, const double* __restrict__ w,
+    int64_t n, uint64_t sentinel, const uint32_t* __restrict__ blkoff,
+    const unsigned long long* __restrict__ cnt, int bj, int32_t* __restrict__ out_i,
+    int32_t* __restrict__ out_j, double* __restrict__ out_v, int64_t* __restrict__ out_first) {
+    __shared__ uint32_t part[RS_THREADS];
+    const int tid = threadIdx.x;
+    const int64_t a = (int64_t)blockIdx.x * RS_TILE + (int64_t)tid * RS_ITEMS;
+    uint32_t my = 0;
+    for (int r = 0; r < RS_ITEMS; ++r)
+        if (a + r < n && cf_head(keys, a + r, sentinel)) ++my;
+    part[tid] = my;
+    __syncthreads();
+    for (int d = 1; d < RS_THREADS; d <<= 1) {
+        const uint32_t v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t idx = blkoff[blockIdx.x] + part[tid] - my;
+    const uint64_t jmask = (1ull << bj) - 1;
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const int64_t e = a + r;
+        if (e >= n || !cf_head(keys, e, sentinel)) continue;
+        const uint64_t k = keys[e];
+        // sum in slot order: the reference's S[i][j] += w sequence (item_cf.py:73-79)
+        double s = 0.0;
+        for (int64_t q = e; q < n && keys[q] == k; ++q) s += w[vals[q]];
+        const int32_t i = (int32_t)(k >> bj), j = (int32_t)(k & jmask);
+        const unsigned long long ci = cnt[i], cj = cnt[j];
+        // wij / math.sqrt(item_cnt[i] * item_cnt[j])  (item_cf.py:81-84)
+        out_i[idx] = i;
+        out_j[idx] = j;
+        out_v[idx] = s / sqrt((double)(ci * cj));
+        out_first[idx] = vals[e];
+        ++idx;
+    }
+}
+
+// -------------------------------------------------------------- top-n --
+// One wave per row: running top-64 by (score desc, first asc), 64-entry
+// chunks bitonic-sorted and merged.
+struct CfEnt {
+    double s;
+    int64_t f;
+    int32_t c;
+};
+
+__device__ __forceinline__ bool cf_better(double as, int64_t af, double bs, int64_t bf) {
+    return as > bs || (as == bs && af < bf);
+}
+
+__device__ __forceinline__ void cf_cmpx(CfEnt& x, int j, bool keep_better) {
+    const double ys = __shfl_xor(x.s, j, WAVE);
+    const int64_t yf = __shfl_xor(x.f, j, WAVE);
+    const int32_t yc = __shfl_xor(x.c, j, WAVE);
+    const bool xb = cf_better(x.s, x.f, ys, yf);
+    if (keep_better != xb) {
+        x.s = ys;
+        x.f = yf;
+        x.c = yc;
+    }
+}
+
+__device__ __forceinline__ void cf_sort64(CfEnt& x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const bool lower = (lane & j) == 0;
+            const bool up = (lane & k) == 0;
+            cf_cmpx(x, j, lower == up);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void cf_topn_kernel(const int64_t* __restrict__ row_off, int64_t n_rows,
+                                                    const int32_t* __restrict__ cols,
+                                                    const double* __restrict__ vals,
+                                                    const int64_t* __restrict__ first, int topn,
+                                                    int32_t* __restrict__ out_cols,
+                                                    double* __restrict__ out_vals,
+                                                    int32_t* __restrict__ out_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_rows; row += nw) {
+        const int64_t a = row_off[row], n = row_off[row + 1] - a;
+        CfEnt cur{-INFINITY, INT64_MAX, -1};
+        for (int64_t c0 = 0; c0 < n; c0 += 64) {
+            CfEnt x{-INFINITY, INT64_MAX, -1};
+            if (c0 + lane < n) {
+                x.s = vals[a + c0 + lane];
+                x.f = first[a + c0 + lane];
+                x.c = cols[a + c0 + lane];
+            }
+            cf_sort64(x);
+            if (c0 == 0) {
+                cur = x;
+            } else {
+                // top 64 of two sorted lists: cur[l] vs x[63 - l] -> bitonic, then clean
+                const double ys = __shfl(x.s, 63 - lane, WAVE);
+                const int64_t yf = __shfl(x.f, 63 - lane, WAVE);
+                const int32_t yc = __shfl(x.c, 63 - lane, WAVE);
+                if (cf_better(ys, yf, cur.s, cur.f)) {
+                    cur.s = ys;
+                    cur.f = yf;
+                    cur.c = yc;
+                }
+#pragma unroll
+                for (int j = 32; j > 0; j >>= 1) cf_cmpx(cur, j, (lane & j) == 0);
+            }
+        }
+        const int64_t m = n < topn ? n : topn;
+        if (lane < topn) {
+            const bool ok = lane < m;
+            out_cols[row * topn + lane] = ok ? cur.c : -1;
+            out_vals[row * topn + lane] = ok ? cur.s : 0.0;
+        }
+        if (lane == 0) out_cnt[row] = (int32_t)m;
+    }
+}
+
+// ---------------------------------------------------------- workspace --
+struct CfWs {
+    uint64_t *ka, *kb;
+    int32_t *va, *vb;
+    double* w;
+    uint32_t *counts, *totals, *blkcnt, *blkoff;
+    size_t bytes;
+};
+
+static inline size_t cf_al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static CfWs cf_ws_layout(void* base, int64_t P) {
+    CfWs w;
+    uint8_t* p = reinterpret_cast<uint8_t*>(base);
+    size_t o = 0;
+    const size_t n = (size_t)(P > 0 ? P : 1);
+    const size_t nblk = (n + RS_TILE - 1) / RS_TILE;
+    auto take = [&](size_t b) { uint8_t* r = p + o; o += cf_al(b); return r; };
+    w.ka = (uint64_t*)take(n * 8);
+    w.kb = (uint64_t*)take(n * 8);
+    w.va = (int32_t*)take(n * 4);
+    w.vb = (int32_t*)take(n * 4);
+    w.w = (double*)take(n * 8);
+    w.counts = (uint32_t*)take(256 * nblk * 4);
+    w.totals = (uint32_t*)take(256 * 4);
+    w.blkcnt = (uint32_t*)take(nblk * 4);
+    w.blkoff = (uint32_t*)take(nblk * 4);
+    w.bytes = o;
+    return w;
+}
+
+static int bits_for(int64_t n) {  // smallest b with 2^b > n
+    int b = 1;
+    while ((int64_t(1) << b) <= n) ++b;
+    return b;
+}
+
+}  // namespace nrk
+
+using namespace nrk;
+
+extern "C" {
+
+int nrk_itemcf_pair_offsets(const int64_t* offsets, int64_t n_users, int64_t* pair_off,
+                            nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(offsets && pair_off, "null pointer");
+    NRK_REQUIRE(n_users >= 0, "n_users < 0");
+    cf_pair_offsets_kernel<<<1, 1024, 0, as_stream(stream)>>>(offsets, n_users, pair_off);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+size_t nrk_itemcf_workspace_bytes(int64_t n_pairs, int32_t n_items) {
+    (void)n_items;
+    if (n_pairs < 0) return 0;
+    return cf_ws_layout(nullptr, n_pairs).bytes;
+}
+
+int nrk_itemcf_sim(const int64_t* offsets, int64_t n_users, const int32_t* items, const int64_t* ts,
+                   const double* created, int32_t n_items, const int64_t* pair_off, int64_t n_pairs,
+                   double loc_alpha, double loc_alpha_rev, double loc_beta, double time_alpha,
+                   double created_alpha, int32_t* out_i, int32_t* out_j, double* out_v,
+                   int64_t* out_first, int64_t* out_n, int64_t* out_cnt, void* workspace,
+                   size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_users >= 0 && n_pairs >= 0, "negative size");
+    NRK_REQUIRE(n_items >= 1, "n_items must be >= 1");
+    NRK_REQUIRE(n_pairs < (int64_t(1) << 31) - RS_TILE, "n_pairs must be < 2^31 (int32 slots)");
+    NRK_REQUIRE(offsets && items && ts && created && pair_off && out_i && out_j && out_v &&
+                    out_first && out_n && out_cnt && workspace,
+                "null pointer");
+    const CfWs w = cf_ws_layout(workspace, n_pairs);
+    NRK_REQUIRE(workspace_bytes >= w.bytes, "workspace too small");
+    hipStream_t s = as_stream(stream);
+    const int bj = bits_for(n_items);  // 2^bj > n_items - 1 + 1: i = 2^bj - 1 is never an item
+    const int nbits = 2 * bj;
+    const uint64_t sentinel = (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
+    (void)hipMemsetAsync(out_cnt, 0, sizeof(int64_t) * (size_t)n_items, s);
+    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha};
+    const int64_t ugrid = (n_users + 3) / 4;
+    if (n_users > 0)
+        cf_pairs_kernel<<<(int)(ugrid < 65536 ? ugrid : 65536), 256, 0, s>>>(
+            offsets, n_users, items, ts, created, pair_off, prm, bj, sentinel, w.ka, w.va, w.w,
+            reinterpret_cast<unsigned long long*>(out_cnt));
+    const int64_t n = n_pairs;
+    const int nblk = (int)((n + RS_TILE - 1) / RS_TILE);
+    uint64_t* kin = w.ka;
+    uint64_t* kout = w.kb;
+    int32_t* vin = w.va;
+    int32_t* vout = w.vb;
+    if (n > 0) {
+        for (int shift = 0; shift < nbits; shift += 8) {
+            rs_upsweep<<<nblk, RS_THREADS, 0, s>>>(kin, n, shift, nblk, w.counts);
+            rs_scan_rows<<<256, 256, 0, s>>>(w.counts, nblk, w.totals);
+            rs_downsweep<<<nblk, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n, shift, nblk, w.counts,
+                                                     w.totals);
+            uint64_t* tk = kin; kin = kout; kout = tk;
+            int32_t* tv = vin; vin = vout; vout = tv;
+        }
+        cf_head_count<<<nblk, RS_THREADS, 0, s>>>(kin, n, sentinel, w.blkcnt);
+        cf_head_scan<<<1, 1024, 0, s>>>(w.blkcnt, nblk, w.blkoff, out_n);
+        cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, w.w, n, sentinel, w.blkoff,
+                                             reinterpret_cast<const unsigned long long*>(out_cnt), bj,
+                                             out_i, out_j, out_v, out_first);
+    } else {
+        (void)hipMemsetAsync(out_n, 0, sizeof(int64_t), s);
+    }
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols, const double* vals,
+                    const int64_t* first, int topn, int32_t* out_cols, double* out_vals,
+                    int32_t* out_cnt, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(topn >= 1, "topn must be >= 1");
+    if (topn > 64) NRK_UNSUPPORTED("topn must be <= 64");
+    NRK_REQUIRE(n_rows >= 0, "n_rows < 0");
+    if (n_rows == 0) return NRK_OK;
+    NRK_REQUIRE(row_off && cols && vals && first && out_cols && out_vals && out_cnt, "null pointer");
+    const int64_t g = (n_rows + 3) / 4;
+    cf_topn_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, as_stream(stream)>>>(
+        row_off, n_rows, cols, vals, first, topn, out_cols, out_vals, out_cnt);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+}  // extern "C"

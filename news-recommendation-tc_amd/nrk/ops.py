@@ -217,19 +217,12 @@ class DinParams:
         _lib.call("nrk_din_prepare", _ptr(self.att_w0), self.n_item, _ptr(self.prep), _stream())
 
 
-def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspace=None):
-    """One DIN batch (B >= 2): int32 index tensors user [B,Fu], item [B,Fi],
-    hist [B,T,Fi], ctx [B,Fc], mask [B,T] f32 -> probs [B] (+ logits)."""
-    _dev(user, item, hist, ctx, mask)
-    B, T = mask.shape
-    _need(user, torch.int32, (B, p.n_user), "user")
-    _need(item, torch.int32, (B, p.n_item), "item")
-    _need(hist, torch.int32, (B, T, p.n_item), "hist")
-    _need(ctx, torch.int32, (B, p.n_ctx), "ctx")
-    _need(mask, torch.float32, (B, T), "mask")
+def din_validate(p: DinParams, user, item, hist, ctx):
+    """Raise ValueError if any index falls outside its embedding table (the
+    kernels gather without bounds checks)."""
     for t, off in ((user, 0), (item, p.n_user), (ctx, p.n_user + p.n_item)):
         if t.numel():
-            mx = t.amax(0).cpu().tolist()
+            mx = t.reshape(-1, t.shape[-1]).amax(0).cpu().tolist()
             mn = int(t.min())
             if mn < 0 or any(m >= p.vocab[off + f] for f, m in enumerate(mx)):
                 raise ValueError("feature index out of its embedding table")
@@ -237,7 +230,28 @@ def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspa
         mx = hist.reshape(-1, p.n_item).amax(0).cpu().tolist()
         if int(hist.min()) < 0 or any(m >= p.vocab[p.n_user + f] for f, m in enumerate(mx)):
             raise ValueError("history index out of its embedding table")
-    probs = torch.empty(B, dtype=torch.float32, device=mask.device)
+
+
+def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspace=None,
+                out=None, validate=True):
+    """One DIN batch (B >= 2): int32 index tensors user [B,Fu], item [B,Fi],
+    hist [B,T,Fi], ctx [B,Fc], mask [B,T] f32 -> probs [B] (+ logits).
+    ``validate=False`` skips the host-side index range check (one device sync)
+    for callers that validated the resident index tensors once up front."""
+    _dev(user, item, hist, ctx, mask)
+    B, T = mask.shape
+    _need(user, torch.int32, (B, p.n_user), "user")
+    _need(item, torch.int32, (B, p.n_item), "item")
+    _need(hist, torch.int32, (B, T, p.n_item), "hist")
+    _need(ctx, torch.int32, (B, p.n_ctx), "ctx")
+    _need(mask, torch.float32, (B, T), "mask")
+    if validate:
+        din_validate(p, user, item, hist, ctx)
+    if out is not None:
+        _need(out, torch.float32, (B,), "out")
+        probs = out
+    else:
+        probs = torch.empty(B, dtype=torch.float32, device=mask.device)
     lg = torch.empty(B, dtype=torch.float32, device=mask.device) if logits else None
     nb = _lib.lib().nrk_din_workspace_bytes(B, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
     if workspace is None or workspace.numel() < nb:
@@ -253,3 +267,79 @@ def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspa
 def din_workspace(p: DinParams, B, T, device):
     nb = _lib.lib().nrk_din_workspace_bytes(B, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
     return torch.empty(nb, dtype=torch.uint8, device=device)
+
+
+# ----------------------------------------------------------------- itemcf --
+class ItemCFSim:
+    """Device result of nrk_itemcf_sim: one entry per distinct (i, j), sorted
+    by (i, j), dense item ids.  ``first`` is the entry's first-encounter slot
+    (the reference's dict insertion order); ``cnt`` the per-item click count."""
+
+    def __init__(self, i, j, v, first, cnt, n_items):
+        self.i, self.j, self.v, self.first, self.cnt = i, j, v, first, cnt
+        self.n_items = n_items
+
+    def row_offsets(self):
+        """CSR offsets over dense item rows (entries are sorted by i)."""
+        c = torch.bincount(self.i.long(), minlength=self.n_items)
+        off = torch.zeros(self.n_items + 1, dtype=torch.int64, device=self.i.device)
+        off[1:] = torch.cumsum(c, 0)
+        return off
+
+
+def itemcf_sim(offsets, items, ts, created, n_items, loc_alpha=1.0, loc_alpha_rev=0.7,
+               loc_beta=0.9, time_alpha=0.7, created_alpha=0.8):
+    """ItemCF similarity (item_cf.py:17-89) over user click lists in CSR:
+    offsets int64 [U+1], items int32 dense ids [N], ts int64 ms [N], created
+    float64 per dense item [n_items]."""
+    _dev(offsets, items, ts, created)
+    _need(offsets, torch.int64, name="offsets")
+    _need(items, torch.int32, (items.numel(),), "items")
+    _need(ts, torch.int64, (items.numel(),), "ts")
+    _need(created, torch.float64, (n_items,), "created")
+    if offsets.dim() != 1 or offsets.numel() < 1:
+        raise ValueError("offsets must be 1-D with n_users + 1 entries")
+    n_users = offsets.numel() - 1
+    dev = offsets.device
+    if items.numel():
+        if int(items.min()) < 0 or int(items.max()) >= n_items:
+            raise ValueError("item id out of [0, n_items)")
+    if int(offsets[0]) != 0 or int(offsets[-1]) != items.numel() or bool((offsets[1:] < offsets[:-1]).any()):
+        raise ValueError("offsets must be non-decreasing from 0 to len(items)")
+    pair_off = torch.empty(n_users + 1, dtype=torch.int64, device=dev)
+    _lib.call("nrk_itemcf_pair_offsets", _ptr(offsets), n_users, _ptr(pair_off), _stream())
+    n_pairs = int(pair_off[-1])
+    cap = max(n_pairs, 1)
+    oi = torch.empty(cap, dtype=torch.int32, device=dev)
+    oj = torch.empty(cap, dtype=torch.int32, device=dev)
+    ov = torch.empty(cap, dtype=torch.float64, device=dev)
+    of = torch.empty(cap, dtype=torch.int64, device=dev)
+    on = torch.zeros(1, dtype=torch.int64, device=dev)
+    cnt = torch.empty(n_items, dtype=torch.int64, device=dev)
+    nb = _lib.lib().nrk_itemcf_workspace_bytes(n_pairs, n_items)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    _lib.call("nrk_itemcf_sim", _ptr(offsets), n_users, _ptr(items), _ptr(ts), _ptr(created),
+              n_items, _ptr(pair_off), n_pairs, float(loc_alpha), float(loc_alpha_rev),
+              float(loc_beta), float(time_alpha), float(created_alpha), _ptr(oi), _ptr(oj),
+              _ptr(ov), _ptr(of), _ptr(on), _ptr(cnt), _ptr(ws), nb, _stream())
+    n = int(on.item())
+    return ItemCFSim(oi[:n], oj[:n], ov[:n], of[:n], cnt, n_items)
+
+
+def itemcf_topn(row_off, cols, vals, first, topn=20):
+    """Per-row top-n by (score desc, first asc) -- the reference's stable
+    ``sorted(..., reverse=True)[:topn]`` (itemcf_recaller.py:41-54).
+    Returns (cols [R, topn] int32 -1 padded, vals [R, topn] f64, cnt [R])."""
+    _dev(row_off, cols, vals, first)
+    _need(row_off, torch.int64, name="row_off")
+    _need(cols, torch.int32, name="cols")
+    _need(vals, torch.float64, (cols.numel(),), "vals")
+    _need(first, torch.int64, (cols.numel(),), "first")
+    n_rows = row_off.numel() - 1
+    dev = row_off.device
+    oc = torch.empty((n_rows, topn), dtype=torch.int32, device=dev)
+    ov = torch.empty((n_rows, topn), dtype=torch.float64, device=dev)
+    cnt = torch.empty(n_rows, dtype=torch.int32, device=dev)
+    _lib.call("nrk_itemcf_topn", _ptr(row_off), n_rows, _ptr(cols), _ptr(vals), _ptr(first), int(topn),
+              _ptr(oc), _ptr(ov), _ptr(cnt), _stream())
+    return oc, ov, cnt

@@ -1,0 +1,168 @@
+"""GPU parity: ItemCF similarity (item_cf.py:17-89), per-item top-n
+(itemcf_recaller.py:41-54) and the recaller built on them, through the C ABI
+(nrk_itemcf_sim / nrk_itemcf_topn).
+
+Checker: the oracle (oracle/nrk_oracle.c, glibc exp/pow) and the reference's
+own outputs (tests/golden/itemcf_small.npz).  Keys, dict order, counts and
+top-n membership/order are exact; fp64 similarity values agree to rtol 1e-12
+(the device exp/pow and libm / numpy's SIMD exp differ in the last ulp).
+"""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from nrk.data import synth
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-12
+
+
+def _inputs(g):
+    log = synth.ClickLog(g["click_user"], g["click_item"], g["click_ts"])
+    users, offs, items_raw, ts = synth.user_lists(log)
+    ids = g["created_ids"]
+    dense = np.searchsorted(ids, items_raw).astype(np.int32)
+    return users, offs, dense, ts, ids
+
+
+def _gpu_sim(offs, dense, ts, created, n_items):
+    from nrk import ops
+
+    d = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dt)).cuda()  # noqa: E731
+    return ops.itemcf_sim(d(offs, np.int64), d(dense, np.int32), d(ts, np.int64), d(created, np.float64), n_items)
+
+
+def _check_vs_oracle(offs, dense, ts, created, n_items):
+    sim = _gpu_sim(offs, dense, ts, created, n_items)
+    gi, gj, gv, gf = (t.cpu().numpy() for t in (sim.i, sim.j, sim.v, sim.first))
+    oi, oj, ov, rank, cnt = oracle.itemcf_sim(offs, dense, ts, created, n_items)
+    assert len(gi) == len(oi)
+    # GPU order is (i, j); the oracle's is first insertion -> compare both ways
+    order = np.argsort(gf, kind="stable")
+    assert np.array_equal(gi[order], oi) and np.array_equal(gj[order], oj)
+    np.testing.assert_allclose(gv[order], ov, rtol=RTOL, atol=0)
+    assert np.all(np.diff(gi.astype(np.int64) * n_items + gj) > 0)
+    assert np.array_equal(sim.cnt.cpu().numpy(), cnt)
+    return sim, (oi, oj, ov)
+
+
+def test_itemcf_sim_vs_oracle_golden_inputs(golden):
+    g = golden("itemcf_small")
+    users, offs, dense, ts, ids = _inputs(g)
+    _check_vs_oracle(offs, dense, ts, g["created_vals"], len(ids))
+
+
+def test_itemcf_similarity_plugin_matches_reference(golden):
+    from nrk.similarity.item_cf import ItemCFSimilarity
+
+    g = golden("itemcf_small")
+    df = pd.DataFrame({"user_id": g["click_user"], "click_article_id": g["click_item"],
+                       "click_timestamp": g["click_ts"]})
+    created = dict(zip(g["created_ids"].tolist(), g["created_vals"].tolist()))
+    sim = ItemCFSimilarity().calculate(df, created)
+    assert list(sim.keys()) == g["sim_rows"].tolist()
+    fi = [i for i, row in sim.items() for _ in row]
+    fj = [j for row in sim.values() for j in row]
+    fv = [v for row in sim.values() for v in row.values()]
+    assert fi == g["sim_i"].tolist() and fj == g["sim_j"].tolist()
+    np.testing.assert_allclose(fv, g["sim_v"], rtol=RTOL, atol=0)
+
+
+def test_itemcf_recall_matches_reference(golden):
+    from nrk.config import RecallConfig
+    from nrk.data.extractors import csr_to_dict
+    from nrk.recall.itemcf_recaller import ItemCFRecaller
+    from nrk.similarity.item_cf import ItemCFSimilarity
+
+    g = golden("itemcf_small")
+    cfg = RecallConfig(itemcf_sim_item_topk=int(g["sim_item_topk"]))
+    log = synth.ClickLog(g["click_user"], g["click_item"], g["click_ts"])
+    users, offs, items, ts = synth.user_lists(log)
+    created = dict(zip(g["created_ids"].tolist(), g["created_vals"].tolist()))
+    res = ItemCFSimilarity(cfg).compute(users, offs, items, ts, created)
+    uit = csr_to_dict(users, offs, items, ts)
+    hot = g["hot"].tolist()
+    for rec in (ItemCFRecaller.from_result(cfg, res, created, uit, hot),
+                ItemCFRecaller(cfg, res.to_dict(), created, uit, hot)):
+        out = rec.batch_recall([int(u) for u in g["recall_users"]], topk=int(g["topk"]))
+        ro = g["recall_offsets"]
+        for n, u in enumerate(g["recall_users"]):
+            got = out[int(u)]
+            assert [a for a, _ in got] == g["recall_items"][ro[n]:ro[n + 1]].tolist(), n
+            np.testing.assert_allclose([b for _, b in got], g["recall_scores"][ro[n]:ro[n + 1]], rtol=RTOL)
+
+
+def _random_lists(rng, n_users, n_items, max_len, repeat_p=0.1):
+    L = rng.integers(0, max_len + 1, n_users)
+    offs = np.zeros(n_users + 1, np.int64)
+    offs[1:] = np.cumsum(L)
+    items = rng.integers(0, n_items, offs[-1]).astype(np.int32)
+    rep = rng.random(offs[-1]) < repeat_p  # repeated clicks on the previous item
+    rep[offs[:-1][L > 0]] = False
+    idx = np.nonzero(rep)[0]
+    items[idx] = items[idx - 1]
+    ts = np.zeros(offs[-1], np.int64)
+    for u in range(n_users):
+        a, b = offs[u], offs[u + 1]
+        ts[a:b] = 1_500_000_000_000 + np.cumsum(rng.integers(0, 4, b - a))  # ties and 1-ms gaps
+    created = rng.random(n_items)
+    created[rng.integers(0, n_items, n_items // 10)] = 0.5  # equal created times
+    return offs, items, ts, created
+
+
+@pytest.mark.parametrize("n_users,n_items,max_len", [(1, 3, 1), (5, 4, 6), (300, 50, 40),
+                                                     (2000, 20000, 25), (50, 1_100_000, 300)])
+def test_itemcf_sim_vs_oracle_random(n_users, n_items, max_len):
+    rng = np.random.default_rng(n_users + n_items)
+    offs, items, ts, created = _random_lists(rng, n_users, n_items, max_len)
+    _check_vs_oracle(offs, items, ts, created, n_items)
+
+
+def test_itemcf_no_pairs():
+    offs = np.array([0, 1, 1, 2], np.int64)
+    sim = _gpu_sim(offs, np.array([3, 3], np.int32), np.array([5, 6], np.int64), np.zeros(4), 4)
+    assert sim.i.numel() == 0
+    assert sim.cnt.cpu().tolist() == [0, 0, 0, 2]
+
+
+@pytest.mark.parametrize("topn", [1, 20, 64])
+def test_itemcf_topn_vs_oracle(topn):
+    from nrk import ops
+
+    rng = np.random.default_rng(topn)
+    n_rows = 700
+    lens = rng.integers(0, 300, n_rows)
+    lens[:5] = [0, 1, 63, 64, 65]
+    off = np.zeros(n_rows + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    n = int(off[-1])
+    vals = np.round(rng.random(n) * 50) / 50  # many exact ties -> insertion order decides
+    cols = rng.integers(0, 10**6, n).astype(np.int32)
+    first = np.arange(n, dtype=np.int64)
+    d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    gc, gv, gn = ops.itemcf_topn(d(off), d(cols), d(vals), d(first), topn)
+    oc, ov, on = oracle.itemcf_topn(off, cols, vals, topn)
+    assert np.array_equal(gn.cpu().numpy(), on)
+    assert np.array_equal(gc.cpu().numpy(), oc)
+    assert np.array_equal(gv.cpu().numpy(), ov)
+
+
+def test_itemcf_full_size():
+    """250k-user / 364,047-item synthetic Tianchi log (BASELINE sizes): the
+    whole similarity against the oracle, plus top-20 per item."""
+    from nrk import ops
+
+    log = synth.make_click_log(n_users=250_000, n_items=364_047, seed=23)
+    users, offs, items_raw, ts = synth.user_lists(log)
+    ids, dense = np.unique(items_raw, return_inverse=True)
+    created = np.random.default_rng(1).random(len(ids))
+    sim, (oi, oj, ov) = _check_vs_oracle(offs, dense.astype(np.int32), ts, created, len(ids))
+    gc, gv, gn = ops.itemcf_topn(sim.row_offsets(), sim.j, sim.v, sim.first, 20)
+    roff, cols, vals = oracle.sim_to_rows(oi, oj, ov, len(ids))
+    oc, ovv, on = oracle.itemcf_topn(roff, cols, vals, 20)
+    assert np.array_equal(gn.cpu().numpy(), on)
+    same = gc.cpu().numpy() == oc
+    # identical except where device/libm last-ulp differences reorder near-ties
+    assert same.mean() > 0.9999
