@@ -177,3 +177,31 @@ def test_full_size_topk_properties(ops):
     so, ro = oracle.ip_topk(users[sample].cpu().numpy(), items.cpu().numpy(), K, nthreads=8)
     assert np.array_equal(r[sample].cpu().numpy().astype(np.int64), ro)
     assert np.array_equal(s[sample].cpu().numpy(), so)
+
+
+@pytest.mark.parametrize("n_shards", [2, 3, 8])
+def test_catalog_shards_merge_equals_single(ops, n_shards):
+    """Config-4 data path on one GPU: per-shard exact top-k with global rows
+    (row_offset) + nrk_topk_merge == the unsharded result, incl. a cross-shard
+    exact tie (lower global row wins)."""
+    from nrk.dist import catalog_sharded_topk, shard_range
+
+    rng = np.random.default_rng(n_shards)
+    users = _unit(rng.standard_normal((300, 32)))
+    items = _unit(rng.standard_normal((5000, 32)))
+    items[4990] = items[10]
+    K = 31
+    so, ro = oracle.ip_topk(users, items, K)
+    es, rs = [], []
+    for r in range(n_shards):
+        lo, hi = shard_range(len(items), n_shards, r)
+        cat = ops.Catalog(_dev(items[lo:hi]))
+        _, rr, ee = ops.ip_topk(_dev(users), cat, K, row_offset=lo, exact=True)
+        es.append(ee)
+        rs.append(rr)
+    s, r, e = ops.topk_merge(torch.stack(es).contiguous(), torch.stack(rs).contiguous(), K)
+    assert np.array_equal(r.cpu().numpy(), ro)
+    assert np.array_equal(s.cpu().numpy(), so)
+    # the single-rank code path of nrk.dist (no process group)
+    s1, r1, _ = catalog_sharded_topk(_dev(users), ops.Catalog(_dev(items)), 0, K)
+    assert np.array_equal(r1.cpu().numpy(), ro)
