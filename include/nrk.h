@@ -161,11 +161,14 @@ int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
  * att_b0 [36], att_w1 [36], att_b1 [1]; mlp_w0 [h1, in], mlp_b0 [h1],
  * mlp_w1 [h2, h1], mlp_b1 [h2], mlp_w2 [h2], mlp_b2 [1]
  * with in = 32 * (n_user + n_ctx + 2 * n_item).
- * nrk_din_prepare derives the batch-invariant attention matrices once per
- * weight load into prep (nrk_din_prep_bytes).  B >= 2 (B = 1 is NaN in the
+ * nrk_din_prepare derives the batch-invariant attention matrices and the
+ * power-of-two scales of the split-fp16 attention product (from max|table|)
+ * once per weight load into prep (nrk_din_prep_bytes); call it again if
+ * the table changes.  B >= 2 (B = 1 is NaN in the
  * reference too). */
 size_t nrk_din_prep_bytes(int n_item);
-int nrk_din_prepare(const float* att_w0, int n_item, void* prep, nrk_stream_t stream);
+int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int table_dtype,
+                    int64_t n_table_rows, void* prep, nrk_stream_t stream);
 size_t nrk_din_workspace_bytes(int64_t batch, int seq_len, int n_user, int n_item, int n_ctx,
                                int h1, int h2);
 int nrk_din_forward(const void* table, int table_dtype, const int64_t* row_base, int n_user,

@@ -41,85 +41,255 @@ __device__ __forceinline__ float dice(float x, float mean, float std) {
 }
 
 // ------------------------------------------------------------- 1. att h --
-// One workgroup processes SPB samples in turn.  LDS: M_b [36][ID], keys
-// [T][ID], query [ID], c [36], and the block's fp64 column sums [T*36][2].
-template <typename TT, int ID>
+// h[b, t, :] = M_b k_t + c_b with M_b = (Wk - Wd) + Wp diag(q_b) [36 x ID]
+// and c_b = (Wq + Wd) q_b + b0: per sample a [T x ID] x [ID x 36] product,
+// run on the fp16 MFMA (v_mfma_f32_16x16x32_f16) as an exact-f32-class
+// split product:
+//   * bf16 tables: k is exactly representable in fp16 (scaled by the
+//     power-of-two s_k), M_b = M_hi + M_lo (two fp16 terms, scaled by s_m)
+//     -> 2 MFMAs per fragment, error ~2^-22 |M| |k| per product + the fp32
+//     accumulation (the same class as an f32 GEMM);
+//   * fp32 tables: k = k_hi + k_lo too -> 3 MFMAs (k_lo * M_lo dropped).
+// The scales live in the prep header (nrk_din_prepare, from the table and
+// weight maxima) so that every scaled value is a normal fp16.
+// Workgroup = 4 waves; wave w owns t-tiles {w, w+4} (16 rows each) and all
+// three 16-column j-tiles (36 -> 48).  M_b's fragments are built once per
+// sample into LDS by the whole workgroup; each wave gathers its own k rows
+// straight from the table into A fragments.  Column statistics of h
+// (fp64 sum / sumsq per (t, j)) stay in registers across the workgroup's
+// samples (grid-strided), one partial row per workgroup.
+typedef _Float16 din_half8 __attribute__((ext_vector_type(8)));
+typedef float din_f4 __attribute__((ext_vector_type(4)));
+
+constexpr int DIN_JT = 3;  // 36 columns -> 3 tiles of 16
+
+struct DinScales {
+    float s_k, s_m, inv, pad;
+};
+
+template <typename TT>
+__device__ __forceinline__ void load8(const TT* p, float (&v)[8]);
+template <>
+__device__ __forceinline__ void load8<float>(const float* p, float (&v)[8]) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0];
+    const float4 b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <>
+__device__ __forceinline__ void load8<uint16_t>(const uint16_t* p, float (&v)[8]) {
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+}
+
+__device__ __forceinline__ void split8(const float (&x)[8], float s, din_half8& hi, din_half8& lo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float v = x[e] * s;
+        const _Float16 h = (_Float16)v;
+        hi[e] = h;
+        lo[e] = (_Float16)(v - (float)h);
+    }
+}
+
+template <typename TT, int NI, int NTW>
 __global__ __launch_bounds__(256) void din_att_h_kernel(
-    const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user, int n_item,
+    const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
     const int32_t* __restrict__ item_idx, const int32_t* __restrict__ hist_idx, int64_t B, int T,
-    const float* __restrict__ prep, const float* __restrict__ att_b0, int spb,
-    float* __restrict__ h_out, double* __restrict__ partial) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* M = lds;                       // [36][ID]
-    float* Kt = M + DIN_H * ID;           // [T][ID]
-    float* q = Kt + (size_t)T * ID;       // [ID]
-    float* c = q + ID;                    // [36] (+ pad)
-    double* acc = reinterpret_cast<double*>(c + 48);  // [T*36][2]
-    const float* A = prep;                // (Wk - Wd)   [36][ID]
-    const float* Bq = prep + DIN_H * ID;  // (Wq + Wd)   [36][ID]
-    const float* P = prep + 2 * DIN_H * ID;  // Wp       [36][ID]
-    const int tid = threadIdx.x;
-    const int ncol = T * DIN_H;
-    for (int i = tid; i < 2 * ncol; i += 256) acc[i] = 0.0;
-    const int64_t b0 = (int64_t)blockIdx.x * spb;
-    const int64_t b1 = b0 + spb < B ? b0 + spb : B;
-    for (int64_t b = b0; b < b1; ++b) {
-        __syncthreads();
-        // gather the candidate (query) and the history keys
-        for (int i = tid; i < ID; i += 256) {
-            const int f = i / DIN_E, e = i % DIN_E;
-            const int64_t r = row_base[n_user + f] + item_idx[b * n_item + f];
-            q[i] = tload(table + r * DIN_E + e);
-        }
-        for (int i = tid; i < T * ID; i += 256) {
-            const int t = i / ID, f = (i % ID) / DIN_E, e = i % DIN_E;
-            const int64_t r = row_base[n_user + f] + hist_idx[(b * T + t) * n_item + f];
-            Kt[i] = tload(table + r * DIN_E + e);
-        }
-        __syncthreads();
-        for (int i = tid; i < DIN_H * ID; i += 256) M[i] = A[i] + P[i] * q[i % ID];
-        if (tid < DIN_H) {
-            float s = att_b0[tid];
-            for (int i = 0; i < ID; ++i) s += Bq[tid * ID + i] * q[i];
-            c[tid] = s;
-        }
-        __syncthreads();
-        // h[t][j] = sum_i Kt[t][i] M[j][i] + c[j]; thread tile 2 t x 4 j
-        const int ntj = ((T + 1) / 2) * (DIN_H / 4);
-        for (int w = tid; w < ntj; w += 256) {
-            const int t0 = (w / (DIN_H / 4)) * 2, j0 = (w % (DIN_H / 4)) * 4;
-            const bool t1ok = t0 + 1 < T;
-            float s[2][4] = {};
-            const float4* k0 = reinterpret_cast<const float4*>(Kt + t0 * ID);
-            const float4* k1 = reinterpret_cast<const float4*>(Kt + (t1ok ? t0 + 1 : t0) * ID);
-#pragma unroll 4
-            for (int i4 = 0; i4 < ID / 4; ++i4) {
-                const float4 a0 = k0[i4], a1 = k1[i4];
+    const float* __restrict__ prep, const float* __restrict__ att_b0, float* __restrict__ h_out,
+    double* __restrict__ partial) {
+    constexpr int ID = NI * DIN_E;
+    constexpr bool F32 = sizeof(TT) == 4;
+    constexpr int NSLOT = DIN_JT * NI * 64;               // fragment lane-slots per pass
+    constexpr int SPT = (NSLOT + 255) / 256;              // slots per thread
+    __shared__ __attribute__((aligned(16))) din_half8 mf[2][DIN_JT][NI][64];  // M_b hi / lo
+    __shared__ float qs[ID];
+    __shared__ float cs[48];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const float* A = prep;
+    const float* Bq = prep + DIN_H * ID;
+    const float* P = prep + 2 * DIN_H * ID;
+    const DinScales sc = *reinterpret_cast<const DinScales*>(prep + 3 * DIN_H * ID);
+
+    // this thread's M slots: fixed (j, k..k+8) -> A, P in registers
+    float ra[SPT][8], rp[SPT][8];
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const float4 m = reinterpret_cast<const float4*>(M + (j0 + jj) * ID)[i4];
-                    s[0][jj] += a0.x * m.x + a0.y * m.y + a0.z * m.z + a0.w * m.w;
-                    s[1][jj] += a1.x * m.x + a1.y * m.y + a1.z * m.z + a1.w * m.w;
+    for (int m = 0; m < SPT; ++m) {
+        const int q = tid + 256 * m;
+        const int jt = q / (NI * 64), s = (q / 64) % NI, l = q % 64;
+        const int j = 16 * jt + (l & 15), k = 32 * s + 8 * (l >> 4);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const bool ok = q < NSLOT && j < DIN_H;
+            ra[m][e] = ok ? A[j * ID + k + e] : 0.0f;
+            rp[m][e] = ok ? P[j * ID + k + e] : 0.0f;
+        }
+    }
+    // c_b partials: thread -> (j = tid / 4, quarter of k)
+    constexpr int CQ = ID / 4;
+    float rbq[CQ];
+    {
+        const int j = tid >> 2, k0 = (tid & 3) * CQ;
+#pragma unroll
+        for (int e = 0; e < CQ; ++e) rbq[e] = j < DIN_H ? Bq[j * ID + k0 + e] : 0.0f;
+    }
+    double ssum[NTW][DIN_JT][4], ssq[NTW][DIN_JT][4];
+#pragma unroll
+    for (int a = 0; a < NTW; ++a)
+#pragma unroll
+        for (int b = 0; b < DIN_JT; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ssum[a][b][r] = ssq[a][b][r] = 0.0;
+
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        // (1) this wave's k rows -> A fragments (issued first: latency overlaps (2)-(4))
+        din_half8 ahi[NTW][NI], alo[NTW][NI];
+#pragma unroll
+        for (int a = 0; a < NTW; ++a) {
+            const int t = 16 * (wv + 4 * a) + (lane & 15);
+#pragma unroll
+            for (int s = 0; s < NI; ++s) {
+                float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (t < T) {
+                    const int64_t r = row_base[n_user + s] + hist_idx[(b * T + t) * NI + s];
+                    load8<TT>(table + r * DIN_E + 8 * (lane >> 4), v);
                 }
+                split8(v, sc.s_k, ahi[a][s], alo[a][s]);
             }
+        }
+        // (2) query embedding
+        if (tid < ID) {
+            const int s = tid / DIN_E, e = tid % DIN_E;
+            const int64_t r = row_base[n_user + s] + item_idx[b * NI + s];
+            qs[tid] = tload(table + r * DIN_E + e);
+        }
+        __syncthreads();
+        // (3) M_b fragments (hi / lo, scaled by s_m) and c_b
 #pragma unroll
-            for (int tt = 0; tt < 2; ++tt) {
-                if (tt == 1 && !t1ok) break;
-                const int t = t0 + tt;
+        for (int m = 0; m < SPT; ++m) {
+            const int q = tid + 256 * m;
+            if (q < NSLOT) {
+                const int jt = q / (NI * 64), s = (q / 64) % NI, l = q % 64;
+                const int k = 32 * s + 8 * (l >> 4);
+                float mv[8];
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const float v = s[tt][jj] + c[j0 + jj];
-                    h_out[(b * T + t) * DIN_H + j0 + jj] = v;
-                    const int col = t * DIN_H + j0 + jj;
-                    acc[2 * col] += (double)v;
-                    acc[2 * col + 1] += (double)v * (double)v;
+                for (int e = 0; e < 8; ++e) mv[e] = fmaf(rp[m][e], qs[k + e], ra[m][e]);
+                din_half8 hi, lo;
+                split8(mv, sc.s_m, hi, lo);
+                mf[0][jt][s][l] = hi;
+                mf[1][jt][s][l] = lo;
+            }
+        }
+        {
+            const int k0 = (tid & 3) * CQ;
+            float c = 0.0f;
+#pragma unroll
+            for (int e = 0; e < CQ; ++e) c = fmaf(rbq[e], qs[k0 + e], c);
+            c += __shfl_xor(c, 1, WAVE);
+            c += __shfl_xor(c, 2, WAVE);
+            const int j = tid >> 2;
+            if ((tid & 3) == 0 && j < DIN_H) cs[j] = c + att_b0[j];
+        }
+        __syncthreads();
+        // (4) MFMAs + epilogue
+#pragma unroll
+        for (int a = 0; a < NTW; ++a) {
+            const int tt = wv + 4 * a;
+            if (16 * tt >= T) continue;
+#pragma unroll
+            for (int jt = 0; jt < DIN_JT; ++jt) {
+                din_f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int s = 0; s < NI; ++s) {
+                    const din_half8 bh = mf[0][jt][s][lane];
+                    const din_half8 bl = mf[1][jt][s][lane];
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[a][s], bh, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[a][s], bl, acc, 0, 0, 0);
+                    if (F32) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[a][s], bh, acc, 0, 0, 0);
+                }
+                const int j = 16 * jt + (lane & 15);
+                const float cj = j < DIN_H ? cs[j] : 0.0f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int t = 16 * tt + 4 * (lane >> 4) + r;
+                    if (t < T && j < DIN_H) {
+                        const float v = acc[r] * sc.inv + cj;
+                        h_out[(b * T + t) * DIN_H + j] = v;
+                        ssum[a][jt][r] += (double)v;
+                        ssq[a][jt][r] += (double)v * (double)v;
+                    }
                 }
             }
         }
     }
+    // per-workgroup partial column sums (every (t, j) is owned by one lane)
+    double2* dst = reinterpret_cast<double2*>(partial) + (size_t)blockIdx.x * T * DIN_H;
+#pragma unroll
+    for (int a = 0; a < NTW; ++a)
+#pragma unroll
+        for (int jt = 0; jt < DIN_JT; ++jt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int t = 16 * (wv + 4 * a) + 4 * (lane >> 4) + r;
+                const int j = 16 * jt + (lane & 15);
+                if (t < T && j < DIN_H) dst[t * DIN_H + j] = make_double2(ssum[a][jt][r], ssq[a][jt][r]);
+            }
+}
+
+// Scales for the split-fp16 products: s_k puts max|table| at <= 2^14, s_m
+// puts max|M_b| <= max(|A| + |P| max|q|) at <= 2^14 (powers of two, so
+// inv = 1 / (s_k s_m) is exact).
+__global__ void din_absmax_kernel(const void* __restrict__ table, int dtype, int64_t n,
+                                  unsigned int* __restrict__ out) {
+    float m = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = dtype == 0 ? reinterpret_cast<const float*>(table)[i]
+                                   : bf16_to_f32(reinterpret_cast<const uint16_t*>(table)[i]);
+        m = fmaxf(m, fabsf(v));
+    }
+    m = fmaxf(m, __shfl_xor(m, 32, WAVE));
+    m = fmaxf(m, __shfl_xor(m, 16, WAVE));
+    m = fmaxf(m, __shfl_xor(m, 8, WAVE));
+    m = fmaxf(m, __shfl_xor(m, 4, WAVE));
+    m = fmaxf(m, __shfl_xor(m, 2, WAVE));
+    m = fmaxf(m, __shfl_xor(m, 1, WAVE));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // m >= 0: bit order == value order
+}
+
+__device__ __forceinline__ float pow2_scale(float mx) {
+    if (!(mx > 0.0f)) return 1.0f;
+    int e;
+    frexpf(mx, &e);  // mx in [2^(e-1), 2^e)
+    return ldexpf(1.0f, 14 - e);
+}
+
+__global__ void din_scales_kernel(const float* __restrict__ prep_ap, int ID, const unsigned int* __restrict__ mx,
+                                  DinScales* __restrict__ out) {
+    const float tmax = __uint_as_float(mx[0]), qmax = tmax;  // q rows come from the same table
+    const int n = DIN_H * ID;
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        m = fmaxf(m, fabsf(prep_ap[i]) + fabsf(prep_ap[2 * n + i]) * qmax);
+    __shared__ float red[256];
+    red[threadIdx.x] = m;
     __syncthreads();
-    double* dst = partial + (size_t)blockIdx.x * 2 * ncol;
-    for (int i = tid; i < 2 * ncol; i += 256) dst[i] = acc[i];
+    for (int d = 128; d > 0; d >>= 1) {
+        if ((int)threadIdx.x < d) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + d]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        DinScales s;
+        s.s_k = pow2_scale(tmax);
+        s.s_m = pow2_scale(red[0] * 1.0001f);
+        s.inv = 1.0f / (s.s_k * s.s_m);
+        s.pad = 0.0f;
+        *out = s;
+    }
 }
 
 // ---------------------------------------------------------- 2. col stats --
@@ -149,9 +319,12 @@ __global__ __launch_bounds__(256) void col_stats_kernel(const double* __restrict
 }
 
 // --------------------------------------------------------- 3. att out --
-// One wave per sample: lane t < T computes the attention weight of history
-// position t; lanes then split the item dim for the weighted sum.  Writes the
-// MLP input row [user, ctx, cand, wh].
+// One workgroup per sample (grid-strided): the 36-wide Dice rows of h are
+// read coalesced and reduced per history slot in a fixed order
+// (w_t = (sum_j w1_j Dice(h_tj) + b1) * mask_t, DIN.py:117-124); then
+// thread i < ID forms wh_i = sum_t w_t k_t[i] (t ascending, :276) from the
+// re-gathered history rows, and the rest of the workgroup copies the user /
+// context / candidate embeddings: MLP input row [user, ctx, cand, wh].
 template <typename TT>
 __global__ __launch_bounds__(256) void din_att_out_kernel(
     const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user, int n_item,
@@ -160,139 +333,172 @@ __global__ __launch_bounds__(256) void din_att_out_kernel(
     const float* __restrict__ mask, int64_t B, int T, const float* __restrict__ h,
     const float2* __restrict__ hstats, const float* __restrict__ att_w1,
     const float* __restrict__ att_b1, float* __restrict__ mlp_in) {
-    const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= B) return;
+    __shared__ float prod[128 * DIN_H];
+    __shared__ float wt[128];
+    __shared__ int64_t hrow[128 * 8];
+    const int tid = threadIdx.x;
     const int ID = n_item * DIN_E;
     const int IN = (n_user + n_ctx + 2 * n_item) * DIN_E;
-    float* row = mlp_in + b * IN;
-    // attention weight of history slot t (lanes t and t + 64 for T <= 128)
-    float w0 = 0.0f, w1 = 0.0f;
-    for (int half = 0; half < 2; ++half) {
-        const int t = lane + 64 * half;
-        if (t < T) {
-            const float* hr = h + (b * T + t) * DIN_H;
+    const int ncol = T * DIN_H;
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        __syncthreads();
+        const float* hb = h + b * ncol;
+        for (int e = tid; e < ncol; e += 256) {
+            const int j = e % DIN_H;
+            const float2 st = hstats[e];
+            prod[e] = att_w1[j] * dice(hb[e], st.x, st.y);
+        }
+        for (int e = tid; e < T * n_item; e += 256) {
+            const int f = e % n_item;
+            hrow[e] = (row_base[n_user + f] + hist_idx[b * T * n_item + e]) * DIN_E;
+        }
+        __syncthreads();
+        if (tid < T) {
             float s = 0.0f;
-            for (int j = 0; j < DIN_H; ++j) {
-                const float2 st = hstats[t * DIN_H + j];
-                s += att_w1[j] * dice(hr[j], st.x, st.y);
+            for (int j = 0; j < DIN_H; ++j) s += prod[tid * DIN_H + j];
+            wt[tid] = (s + att_b1[0]) * mask[b * T + tid];
+        }
+        __syncthreads();
+        float* row = mlp_in + b * IN;
+        if (tid < ID) {
+            const int f = tid / DIN_E, e = tid % DIN_E;
+            float s = 0.0f;
+            for (int t = 0; t < T; ++t) s += wt[t] * tload(table + hrow[t * n_item + f] + e);
+            row[(n_user + n_ctx + n_item) * DIN_E + tid] = s;
+            row[(n_user + n_ctx) * DIN_E + tid] =
+                tload(table + (row_base[n_user + f] + item_idx[b * n_item + f]) * DIN_E + e);
+        } else {
+            for (int i = tid - ID; i < (n_user + n_ctx) * DIN_E; i += 256 - ID) {
+                const int f = i / DIN_E, e = i % DIN_E;
+                const int64_t r = f < n_user ? row_base[f] + user_idx[b * n_user + f]
+                                             : row_base[n_item + f] + ctx_idx[b * n_ctx + (f - n_user)];
+                row[i] = tload(table + r * DIN_E + e);
             }
-            s = (s + att_b1[0]) * mask[b * T + t];
-            if (half == 0) w0 = s; else w1 = s;
         }
-    }
-    // weighted history sum: lane owns dims lane, lane + 64 (ID <= 128 per pass)
-    for (int i = lane; i < ID; i += 64) {
-        const int f = i / DIN_E, e = i % DIN_E;
-        const int64_t base = row_base[n_user + f];
-        float s = 0.0f;
-        for (int t = 0; t < T; ++t) {
-            const float wt = __shfl(t < 64 ? w0 : w1, t & 63, 64);
-            const int64_t r = base + hist_idx[(b * T + t) * n_item + f];
-            s += wt * tload(table + r * DIN_E + e);
-        }
-        row[(n_user + n_ctx + n_item) * DIN_E + i] = s;
-        // candidate embedding
-        row[(n_user + n_ctx) * DIN_E + i] = tload(table + (row_base[n_user + f] + item_idx[b * n_item + f]) * DIN_E + e);
-    }
-    for (int i = lane; i < n_user * DIN_E; i += 64) {
-        const int f = i / DIN_E, e = i % DIN_E;
-        row[i] = tload(table + (row_base[f] + user_idx[b * n_user + f]) * DIN_E + e);
-    }
-    for (int i = lane; i < n_ctx * DIN_E; i += 64) {
-        const int f = i / DIN_E, e = i % DIN_E;
-        row[n_user * DIN_E + i] = tload(table + (row_base[n_user + n_item + f] + ctx_idx[b * n_ctx + f]) * DIN_E + e);
     }
 }
 
 // ---------------------------------------------------------- 4/6. gemm --
-// C[M][N] = f(A)[M][K] W[N][K]^T + bias, f = Dice with per-column stats of A
-// (or identity).  64x64 output tile per 256-thread block, 4x4 per thread,
-// K staged through LDS 32 at a time.  Writes per-row-block fp64 column sums
-// (sum, sumsq) of C for the next Dice.
+// C[M][N] = f(A)[M][K] W[N][K]^T + bias on the f32-input MFMA
+// (v_mfma_f32_32x32x2_f32, exact f32 fma chains), f = Dice with per-column
+// stats of A (GEMM2, Dice-on-load) or identity (GEMM1).
+// Workgroup = 8 waves = 64x64 output tile: waves (wm, wn) own 32x32 blocks,
+// kh in {0,1} splits K in two interleaved halves (2 waves / SIMD); the two
+// partial accumulators are added in a fixed order through LDS.  Operands go
+// global -> registers directly: within an 8-wide k chunk, MFMA step s of
+// lane half h uses k = 8h + s, so each lane loads 8 contiguous floats of its
+// A row and W row (two float4) -- the k order inside the chunk is permuted
+// identically for both operands.  Loads run two chunks ahead.
+// Writes per-row-block fp64 column sums (sum, sumsq) of C for the next Dice.
+typedef float din_f16v __attribute__((ext_vector_type(16)));
+
 template <bool DICE_A>
-__global__ __launch_bounds__(256) void din_gemm_kernel(
+__device__ __forceinline__ void gemm_load(const float* __restrict__ A, const float2* __restrict__ astats,
+                                          const float* __restrict__ W, int64_t m, bool mok, int n,
+                                          bool nok, int K, int k, float (&a)[8], float (&w)[8]) {
+    const bool full = k + 8 <= K;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        a[e] = 0.0f;
+        w[e] = 0.0f;
+    }
+    if (full && ((K & 3) == 0)) {
+        if (mok) {
+            const float4 x = *reinterpret_cast<const float4*>(A + m * K + k);
+            const float4 y = *reinterpret_cast<const float4*>(A + m * K + k + 4);
+            a[0] = x.x; a[1] = x.y; a[2] = x.z; a[3] = x.w;
+            a[4] = y.x; a[5] = y.y; a[6] = y.z; a[7] = y.w;
+        }
+        if (nok) {
+            const float4 x = *reinterpret_cast<const float4*>(W + (int64_t)n * K + k);
+            const float4 y = *reinterpret_cast<const float4*>(W + (int64_t)n * K + k + 4);
+            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+            w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if (k + e < K) {
+                if (mok) a[e] = A[m * K + k + e];
+                if (nok) w[e] = W[(int64_t)n * K + k + e];
+            }
+        }
+    }
+    if (DICE_A && mok) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (k + e < K) {
+                const float2 st = astats[k + e];
+                a[e] = dice(a[e], st.x, st.y);
+            }
+    }
+}
+
+template <bool DICE_A>
+__global__ __launch_bounds__(512) void din_gemm_kernel(
     const float* __restrict__ A, const float2* __restrict__ astats, const float* __restrict__ W,
     const float* __restrict__ bias, int64_t M, int N, int K, float* __restrict__ C,
     double* __restrict__ partial) {
-    __shared__ float As[32][64 + 4];
-    __shared__ float Ws[32][64 + 4];
-    __shared__ double cs[2][16][64];
-    const int tid = threadIdx.x;
-    const int tx = tid & 15, ty = tid >> 4;  // 16 x 16 threads
-    const int64_t m0 = (int64_t)blockIdx.x * 64;
-    const int n0 = blockIdx.y * 64;
-    float acc[4][4] = {};
-    for (int k0 = 0; k0 < K; k0 += 32) {
-        // load A tile [64 rows][32 k] transposed into As[k][m]
-        for (int i = tid; i < 64 * 32; i += 256) {
-            const int r = i / 32, kk = i % 32;
-            const int64_t m = m0 + r;
-            const int k = k0 + kk;
-            float v = 0.0f;
-            if (m < M && k < K) {
-                v = A[m * K + k];
-                if (DICE_A) {
-                    const float2 st = astats[k];
-                    v = dice(v, st.x, st.y);
-                }
-            }
-            As[kk][r] = v;
-        }
-        for (int i = tid; i < 64 * 32; i += 256) {
-            const int r = i / 32, kk = i % 32;
-            const int n = n0 + r;
-            const int k = k0 + kk;
-            Ws[kk][r] = (n < N && k < K) ? W[(int64_t)n * K + k] : 0.0f;
-        }
-        __syncthreads();
-#pragma unroll 8
-        for (int kk = 0; kk < 32; ++kk) {
-            float a[4], w[4];
+    __shared__ float red[4][16][64];
+    __shared__ double cs[2][2][64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wm = wv & 1, wn = (wv >> 1) & 1, kh = wv >> 2;
+    const int64_t m = (int64_t)blockIdx.x * 64 + wm * 32 + (lane & 31);
+    const int n = blockIdx.y * 64 + wn * 32 + (lane & 31);
+    const bool mok = m < M, nok = n < N;
+    const int half = lane >> 5;
+    din_f16v acc;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                a[i] = As[kk][ty * 4 + i];
-                w[i] = Ws[kk][tx * 4 + i];
-            }
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    // chunks c = kh, kh + 2, kh + 4, ... of 16 k each: lane half h takes k = 16c + 8h + [0, 8)
+    const int nch = (K + 15) / 16;
+    float a0[8], w0[8], a1[8], w1[8];
+    int c = kh;
+    if (c < nch) gemm_load<DICE_A>(A, astats, W, m, mok, n, nok, K, 16 * c + 8 * half, a0, w0);
+    if (c + 2 < nch) gemm_load<DICE_A>(A, astats, W, m, mok, n, nok, K, 16 * (c + 2) + 8 * half, a1, w1);
+    for (; c < nch; c += 4) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+        for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], w0[e], acc, 0, 0, 0);
+        if (c + 4 < nch) gemm_load<DICE_A>(A, astats, W, m, mok, n, nok, K, 16 * (c + 4) + 8 * half, a0, w0);
+        if (c + 2 < nch) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * w[j];
-        }
-        __syncthreads();
-    }
-    double csum[4] = {}, csq[4] = {};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int64_t m = m0 + ty * 4 + i;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + tx * 4 + j;
-            if (m < M && n < N) {
-                const float v = acc[i][j] + bias[n];
-                C[m * N + n] = v;
-                csum[j] += (double)v;
-                csq[j] += (double)v * (double)v;
-            }
+            for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], w1[e], acc, 0, 0, 0);
+            if (c + 6 < nch) gemm_load<DICE_A>(A, astats, W, m, mok, n, nok, K, 16 * (c + 6) + 8 * half, a1, w1);
         }
     }
-    // column sums over the block's 64 rows, in a fixed order
+    // K halves: kh = 1 hands its accumulator to kh = 0 (fixed order)
+    if (kh == 1) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        cs[0][ty][tx * 4 + j] = csum[j];
-        cs[1][ty][tx * 4 + j] = csq[j];
+        for (int r = 0; r < 16; ++r) red[wv - 4][r][lane] = acc[r];
+    }
+    __syncthreads();
+    if (kh == 0) {
+        const int64_t mrow0 = (int64_t)blockIdx.x * 64 + wm * 32;
+        double s = 0.0, ss = 0.0;
+        const float bn = nok ? bias[n] : 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t mr = mrow0 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            const float v = (acc[r] + red[wv][r][lane]) + bn;
+            if (nok && mr < M) {
+                C[mr * N + n] = v;
+                s += (double)v;
+                ss += (double)v * (double)v;
+            }
+        }
+        s += __shfl_xor(s, 32, WAVE);
+        ss += __shfl_xor(ss, 32, WAVE);
+        if (lane < 32) {
+            cs[0][wm][wn * 32 + lane] = s;
+            cs[1][wm][wn * 32 + lane] = ss;
+        }
     }
     __syncthreads();
     if (tid < 64) {
-        const int n = n0 + tid;
-        double s = 0.0, ss = 0.0;
-        for (int r = 0; r < 16; ++r) {
-            s += cs[0][r][tid];
-            ss += cs[1][r][tid];
-        }
-        if (n < N) {
-            partial[((size_t)blockIdx.x * N + n) * 2] = s;
-            partial[((size_t)blockIdx.x * N + n) * 2 + 1] = ss;
+        const int nn = blockIdx.y * 64 + tid;
+        if (nn < N) {
+            partial[((size_t)blockIdx.x * N + nn) * 2] = cs[0][0][tid] + cs[0][1][tid];
+            partial[((size_t)blockIdx.x * N + nn) * 2 + 1] = cs[1][0][tid] + cs[1][1][tid];
         }
     }
 }
@@ -333,7 +539,7 @@ __global__ void din_prepare_kernel(const float* __restrict__ w0, int ID, float* 
 }
 
 // ------------------------------------------------------------- workspace --
-constexpr int DIN_SPB = 16;  // samples per block in din_att_h
+constexpr int64_t DIN_ATT_GRID = 512;  // din_att_h workgroups (grid-strided over samples)
 
 struct DinWs {
     float* h;
@@ -356,7 +562,7 @@ static DinWs din_ws_layout(void* base, int64_t B, int T, int n_user, int n_item,
     DinWs w;
     uint8_t* p = reinterpret_cast<uint8_t*>(base);
     size_t o = 0;
-    const int64_t nb_att = (B + DIN_SPB - 1) / DIN_SPB;
+    const int64_t nb_att = B < DIN_ATT_GRID ? B : DIN_ATT_GRID;
     const int64_t nb_m = (B + 63) / 64;
     const int IN = (n_user + n_ctx + 2 * n_item) * DIN_E;
     auto take = [&](size_t bytes) { uint8_t* r = p + o; o += al(bytes); return r; };
@@ -382,15 +588,27 @@ extern "C" {
 
 size_t nrk_din_prep_bytes(int n_item) {
     if (n_item <= 0) return 0;
-    return (size_t)3 * DIN_H * n_item * DIN_E * sizeof(float);
+    return (size_t)3 * DIN_H * n_item * DIN_E * sizeof(float) + 64;
 }
 
-int nrk_din_prepare(const float* att_w0, int n_item, void* prep, nrk_stream_t stream) {
+int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int table_dtype,
+                    int64_t n_table_rows, void* prep, nrk_stream_t stream) {
     clear_error();
-    NRK_REQUIRE(att_w0 && prep, "null pointer");
+    NRK_REQUIRE(att_w0 && prep && table, "null pointer");
     NRK_REQUIRE(n_item >= 1 && n_item <= 8, "n_item must be in [1, 8]");
+    NRK_REQUIRE(table_dtype == 0 || table_dtype == 1, "table_dtype must be 0 (f32) or 1 (bf16)");
+    NRK_REQUIRE(n_table_rows >= 1, "n_table_rows must be >= 1");
     const int ID = n_item * DIN_E;
-    din_prepare_kernel<<<64, 256, 0, as_stream(stream)>>>(att_w0, ID, reinterpret_cast<float*>(prep));
+    hipStream_t s = as_stream(stream);
+    float* pf = reinterpret_cast<float*>(prep);
+    DinScales* sc = reinterpret_cast<DinScales*>(pf + 3 * DIN_H * ID);
+    unsigned int* mx = reinterpret_cast<unsigned int*>(sc + 1);
+    din_prepare_kernel<<<64, 256, 0, s>>>(att_w0, ID, pf);
+    (void)hipMemsetAsync(mx, 0, 8, s);
+    const int64_t n = n_table_rows * DIN_E;
+    const int64_t g = (n + 255) / 256;
+    din_absmax_kernel<<<(int)(g < 2048 ? g : 2048), 256, 0, s>>>(table, table_dtype, n, mx);
+    din_scales_kernel<<<1, 256, 0, s>>>(pf, ID, mx, sc);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -426,42 +644,43 @@ int nrk_din_forward(const void* table, int table_dtype, const int64_t* row_base,
     NRK_REQUIRE(workspace_bytes >= w.bytes, "workspace too small");
     hipStream_t s = as_stream(stream);
     const int T = seq_len;
-    const int ID = n_item * DIN_E;
     const int IN = (n_user + n_ctx + 2 * n_item) * DIN_E;
-    const int nb_att = (int)((batch + DIN_SPB - 1) / DIN_SPB);
-    const size_t lds_att = sizeof(float) * ((size_t)DIN_H * ID + (size_t)T * ID + ID + 48) +
-                           sizeof(double) * 2 * (size_t)T * DIN_H;
+    const int nb_att = (int)(batch < DIN_ATT_GRID ? batch : DIN_ATT_GRID);
     const float* pf = reinterpret_cast<const float*>(prep);
-#define NRK_ATT_H(TT, IDV)                                                                          \
+#define NRK_ATT_H(TT, NI)                                                                           \
     do {                                                                                            \
-        (void)hipFuncSetAttribute((const void*)din_att_h_kernel<TT, IDV>,                           \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_att);        \
-        din_att_h_kernel<TT, IDV><<<nb_att, 256, lds_att, s>>>(                                     \
-            reinterpret_cast<const TT*>(table), row_base, n_user, n_item, item_idx, hist_idx,       \
-            batch, T, pf, att_b0, DIN_SPB, w.h, w.hpart);                                           \
+        if (T <= 64)                                                                                \
+            din_att_h_kernel<TT, NI, 1><<<nb_att, 256, 0, s>>>(                                     \
+                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, T, \
+                pf, att_b0, w.h, w.hpart);                                                          \
+        else                                                                                        \
+            din_att_h_kernel<TT, NI, 2><<<nb_att, 256, 0, s>>>(                                     \
+                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, T, \
+                pf, att_b0, w.h, w.hpart);                                                          \
     } while (0)
     if (table_dtype == 0) {
-        if (ID == 128) NRK_ATT_H(float, 128); else if (ID == 64) NRK_ATT_H(float, 64); else NRK_ATT_H(float, 32);
+        if (n_item == 4) NRK_ATT_H(float, 4); else if (n_item == 2) NRK_ATT_H(float, 2); else NRK_ATT_H(float, 1);
     } else {
-        if (ID == 128) NRK_ATT_H(uint16_t, 128); else if (ID == 64) NRK_ATT_H(uint16_t, 64); else NRK_ATT_H(uint16_t, 32);
+        if (n_item == 4) NRK_ATT_H(uint16_t, 4); else if (n_item == 2) NRK_ATT_H(uint16_t, 2); else NRK_ATT_H(uint16_t, 1);
     }
 #undef NRK_ATT_H
     const int ncol_att = T * DIN_H;
     col_stats_kernel<<<(ncol_att + 3) / 4, 256, 0, s>>>(w.hpart, nb_att, ncol_att, batch, w.hstats);
     const int gb = (int)((batch + 3) / 4);
+    const int go = (int)(batch < 4096 ? batch : 4096);
     if (table_dtype == 0)
-        din_att_out_kernel<float><<<gb, 256, 0, s>>>(
+        din_att_out_kernel<float><<<go, 256, 0, s>>>(
             reinterpret_cast<const float*>(table), row_base, n_user, n_item, n_ctx, user_idx,
             item_idx, hist_idx, ctx_idx, mask, batch, T, w.h, w.hstats, att_w1, att_b1, w.mlp_in);
     else
-        din_att_out_kernel<uint16_t><<<gb, 256, 0, s>>>(
+        din_att_out_kernel<uint16_t><<<go, 256, 0, s>>>(
             reinterpret_cast<const uint16_t*>(table), row_base, n_user, n_item, n_ctx, user_idx,
             item_idx, hist_idx, ctx_idx, mask, batch, T, w.h, w.hstats, att_w1, att_b1, w.mlp_in);
     const int nb_m = (int)((batch + 63) / 64);
-    din_gemm_kernel<false><<<dim3(nb_m, (h1 + 63) / 64), 256, 0, s>>>(
+    din_gemm_kernel<false><<<dim3(nb_m, (h1 + 63) / 64), 512, 0, s>>>(
         w.mlp_in, nullptr, mlp_w0, mlp_b0, batch, h1, IN, w.z1, w.z1part);
     col_stats_kernel<<<(h1 + 3) / 4, 256, 0, s>>>(w.z1part, nb_m, h1, batch, w.z1stats);
-    din_gemm_kernel<true><<<dim3(nb_m, (h2 + 63) / 64), 256, 0, s>>>(
+    din_gemm_kernel<true><<<dim3(nb_m, (h2 + 63) / 64), 512, 0, s>>>(
         w.z1, w.z1stats, mlp_w1, mlp_b1, batch, h2, h1, w.z2, w.z2part);
     col_stats_kernel<<<(h2 + 3) / 4, 256, 0, s>>>(w.z2part, nb_m, h2, batch, w.z2stats);
     din_head_kernel<<<gb, 256, 0, s>>>(w.z2, w.z2stats, batch, h2, mlp_w2, mlp_b2, out_probs,

@@ -41,7 +41,7 @@ SIGNATURES = {
                              P, P, P, P, P, P, P, SZ, P]),
     "nrk_itemcf_topn": (INT, [P, I64, P, P, P, INT, P, P, P, P]),
     "nrk_din_prep_bytes": (SZ, [INT]),
-    "nrk_din_prepare": (INT, [P, INT, P, P]),
+    "nrk_din_prepare": (INT, [P, INT, P, INT, I64, P, P]),
     "nrk_din_workspace_bytes": (SZ, [I64, INT, INT, INT, INT, INT, INT]),
     "nrk_din_forward": (INT, [P, INT, P, INT, INT, INT, P, P, P, P, P, I64, INT, P, P, P, P,
                               P, P, INT, P, P, INT, P, P, P, P, P, SZ, P]),

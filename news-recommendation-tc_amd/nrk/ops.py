@@ -214,7 +214,8 @@ class DinParams:
             raise ValueError("state_dict shapes do not match the feature lists")
         nb = _lib.lib().nrk_din_prep_bytes(self.n_item)
         self.prep = torch.empty(nb, dtype=torch.uint8, device=device)
-        _lib.call("nrk_din_prepare", _ptr(self.att_w0), self.n_item, _ptr(self.prep), _stream())
+        _lib.call("nrk_din_prepare", _ptr(self.att_w0), self.n_item, _ptr(self.table), self.table_code,
+                  self.table.shape[0], _ptr(self.prep), _stream())
 
 
 def din_validate(p: DinParams, user, item, hist, ctx):
