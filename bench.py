@@ -4,17 +4,19 @@
 One "step" = one pass of the recall hot path over one batch:
   YouTubeDNN user tower for U = 250,000 users (HIP, nrk_tt_user_fwd)
   + exact top-31 inner-product search over the 364,047-item catalog, D = 32
-    (HIP: bf16 MFMA screen + fp64 exact refine, nrk_ip_topk_screen/_finish),
+    (HIP: fp16 MFMA screen + fp64 exact refine, nrk_ip_topk_screen/_finish),
 i.e. BASELINE config 2 ("YouTubeDNN recall: 250k users x 364k items,
 emb_dim=32, top-30, bf16, 1 MI355X").  The item tower + catalog build is the
 index build (faiss add) and happens once, before the timed region.
 value = recalled user-item pairs / s = users x 30 / step time (rank 0 of the
 31 is dropped by recall(), youtubednn_recaller.py:524).
 
-With --gpus N > 1 (torch.distributed.run, one process per GPU, RCCL): every
-rank processes its own 250k users against the full catalog (weak scaling,
-no data-path collective); the timed region is bracketed by barriers and the
-max over ranks is used.
+With --gpus N > 1 (torch.distributed.run, one process per GPU, RCCL): by
+default every rank processes its own 250k users against the full catalog
+(weak scaling, no data-path collective); --shard catalog runs BASELINE
+config 4 instead (catalog split N-way, all_to_all of the shard-local top-31
++ nrk_topk_merge, strong scaling).  The timed region is bracketed by
+barriers and the max over ranks is used.
 
 Extra fields on the JSON line: "roofline" for the dominant kernel
 (ip_screen), "cpu_baseline" (the oracle's per-user exact scan -- the
@@ -41,6 +43,25 @@ import torch  # noqa: E402
 METRIC = "recalled pairs/sec (YouTubeDNN top-30) + DIN scored pairs/sec, 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+
+
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
+
+
+def pmc_traffic(kernels, default_config):
+    """HBM-side bytes per launch of ``kernels`` (summed) from the committed
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench at its default
+    config (tools/pmc_traffic.py applies the gfx950 corrections); None when
+    the run is not at that config or the file is absent."""
+    if not default_config or not os.path.exists(TRAFFIC_FILE):
+        return None
+    ks = json.load(open(TRAFFIC_FILE))["kernels"]
+    tot = 0.0
+    for k in kernels:
+        if k not in ks:
+            return None
+        tot += ks[k]["traffic_bytes_per_launch"]
+    return tot
 
 
 def log(*a):
@@ -166,10 +187,17 @@ def run_din(args, device, rank, world):
     batch_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     value = n / dt
     achieved = DIN_BYTES_PER_PAIR * B / (batch_ms * 1e-3) / 1e9
+    t = pmc_traffic(["nrk::din_att_h_kernel<unsigned short, 4, 1>", "nrk::col_stats_kernel",
+                     "nrk::din_att_out_kernel<unsigned short>", "nrk::din_gemm_kernel<false>",
+                     "nrk::din_gemm_kernel<true>", "nrk::din_head_kernel"], n == DIN_SAMPLES)
+    if t is not None:
+        t += 2 * pmc_traffic(["nrk::col_stats_kernel"], True)  # three col_stats launches per batch
+    din_traffic = round(t) if t else None
     out = {"value": round(value * world, 1), "unit": "DIN scored pairs/s", "ms_per_pass": round(dt * 1e3, 3),
            "samples": n, "batch": B, "seq_len": T, "dtype": "fp32 math, bf16 tables",
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": din_traffic,
+                        "traffic_unit": "bytes/launch, all 8 kernels (profiles/r01_traffic.json)",
                         "kernel": "nrk_din_forward (one 4096-sample batch, 8 kernels)",
                         "kernel_ms": round(batch_ms, 4),
                         "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * B}}
@@ -312,8 +340,12 @@ def main():
 
     flops = 2.0 * U * cat.n * D
     achieved = flops / (screen_ms * 1e-3) / 1e12
+    default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and not catalog_mode
+    traffic = pmc_traffic(["nrk::ip_screen_kernel<32>"], default_cfg)
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                "traffic": round(traffic) if traffic else None,
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_traffic.json)",
                 "kernel": "ip_screen_kernel<32> (fp16 MFMA 32x32x16)", "kernel_ms": round(screen_ms, 4),
                 "algorithmic_flop_per_launch": flops}
 
