@@ -313,68 +313,123 @@ __global__ __launch_bounds__(256, 1) void ip_screen_kernel(
     const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
     // this lane's list slot 0 (entry j at + j * 512)
     const uint32_t list_lds = lds_base + NSLOT * TILE_BYTES + (wave * IP_CL * WAVE + lane) * 8;
-    // Fragment reads as inline asm: hipcc's waitcnt pass would otherwise put
-    // a vmcnt(0) (drain every LDS-DMA in flight, i.e. the prefetch) in front
-    // of any ds_read of the ring.  Ordering is explicit: the caller's counted
-    // vmcnt + barrier retire the slot's DMA; lgkmcnt(0) retires these reads.
-    auto compute_tile = [&](int t, auto slot_c) {
-        constexpr int SLOT = decltype(slot_c)::value;
-        static_assert(SLOT * TILE_BYTES + TILE_BYTES <= 65536, "ds offset range");
-        const uint32_t lds0 = lds_base + lane * 16;
-        u32x4 afr[TB][DS];
+    // Software pipeline across tiles: the MFMAs of tile t+1 (accumulator set
+    // B) are issued before the max/append VALU work of tile t (set A), in one
+    // basic block, so the matrix core runs while the lane reduces the
+    // previous tile.  Fragment reads are inline asm: hipcc's waitcnt pass
+    // would otherwise put a vmcnt(0) (drain every LDS-DMA in flight, i.e. the
+    // prefetch) in front of any ds_read of the ring.  Ordering is explicit:
+    // the counted vmcnt + barrier retire the slot's DMA; lgkmcnt(0) retires
+    // these reads (and the previous tile's list appends).
+    const uint32_t lds0 = lds_base + lane * 16;
+    // All reads and their lgkmcnt(0) sit in ONE asm statement: with the
+    // wait in a separate statement the compiler may copy an output register
+    // between the ds_read and the wait, i.e. before the data has landed.
+    auto read_frags = [&](int t, u32x4 (&afr)[TB][DS]) {
+        const uint32_t base = lds0 + (uint32_t)((t % NSLOT) * TILE_BYTES);
+        u32x4* f = &afr[0][0];
+        if constexpr (TB * DS == 4) {
+            asm volatile(
+                "ds_read_b128 %0, %4 offset:0\n\tds_read_b128 %1, %4 offset:1024\n\t"
+                "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3])
+                : "v"(base)
+                : "memory");
+        } else if constexpr (TB * DS == 8) {
+            asm volatile(
+                "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:1024\n\t"
+                "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
+                "ds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:5120\n\t"
+                "ds_read_b128 %6, %8 offset:6144\n\tds_read_b128 %7, %8 offset:7168\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]),
+                  "=&v"(f[6]), "=&v"(f[7])
+                : "v"(base)
+                : "memory");
+        } else {
+            static_assert(TB * DS == 16, "fragment count");
 #pragma unroll
-        for (int b = 0; b < TB; ++b)
-#pragma unroll
-            for (int s = 0; s < DS; ++s)
-                asm volatile("ds_read_b128 %0, %1 offset:%2"
-                             : "=v"(afr[b][s])
-                             : "v"(lds0), "i"(SLOT * TILE_BYTES + (b * DS + s) * 1024));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);  // no MFMA hoisted above the wait
-#ifdef NRK_SCREEN_STATS
-        const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-#endif
-        f32x16 acc[TB];
-#pragma unroll
-        for (int b = 0; b < TB; ++b) {
-            acc[b] = f32x16{};
-#pragma unroll
-            for (int s = 0; s < DS; ++s)
-                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afr[b][s]), ufrag[s], acc[b], 0, 0, 0);
+            for (int half = 0; half < 2; ++half)
+                asm volatile(
+                    "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:1024\n\t"
+                    "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
+                    "ds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:5120\n\t"
+                    "ds_read_b128 %6, %8 offset:6144\n\tds_read_b128 %7, %8 offset:7168\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&v"(f[8 * half + 0]), "=&v"(f[8 * half + 1]), "=&v"(f[8 * half + 2]),
+                      "=&v"(f[8 * half + 3]), "=&v"(f[8 * half + 4]), "=&v"(f[8 * half + 5]),
+                      "=&v"(f[8 * half + 6]), "=&v"(f[8 * half + 7])
+                    : "v"(base + 8192u * half)
+                    : "memory");
         }
-#pragma unroll
-        for (int b = 0; b < TB; ++b) {
-            const int blk = t * TB + b;
-            if (blk >= tail_blk) {  // uniform: partial / padding block(s) of the last tile
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (row >= n_items) acc[b][r] = -INFINITY;
-                }
-            }
-            float mx = fmaxf(fmaxf(acc[b][0], acc[b][1]), acc[b][2]);
-#pragma unroll
-            for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, acc[b][r]), acc[b][r + 1]);
-            mx = fmaxf(mx, acc[b][15]);
-            // inline-asm store: invisible to hipcc's waitcnt pass, which would
-            // otherwise drain the in-flight LDS-DMA before every list append
-            const uint2 ent = make_uint2(__float_as_uint(mx), (uint32_t)(blk * 2 + h));
-            asm volatile("ds_write_b64 %0, %1" ::"v"(list_lds + (uint32_t)n * (WAVE * 8)), "v"(ent)
-                         : "memory");
-            n += (mx > tau) ? 1 : 0;
-        }
-#ifdef NRK_SCREEN_STATS
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        st_cyc_slow += __builtin_amdgcn_s_memtime() - c0;  // MFMA + max + append
-#endif
     };
-
-    // one ring phase: tile t lives in ring slot slot_c (compile-time, so the
-    // fragment reads use immediate offsets)
-    auto phase = [&](int t, auto slot_c) {
-        // tile t landed (this wave's pieces; the younger tiles stay in flight),
-        // then the barrier makes every wave's pieces visible and retires every
-        // read of the slot about to be refilled ((t - 1) % NSLOT)
+    // Block-level software pipeline (one block of lag, carried across
+    // tiles): the two k-step MFMAs of block j are interleaved with the
+    // max/append VALU work of block j-1, so the matrix core and the VALU run
+    // together and only two 16-register accumulators are live.
+    // pend: the previous block's scores; pblk: its block index.
+    // (starts as an all -inf dummy: its append is written but never counted)
+    f32x16 pend;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pend[r] = -INFINITY;
+    int pblk = 0;
+    // half-block max of the pending block; MASK zeroes rows >= n_items
+    auto reduce_lo = [&](auto mask_c) {
+        constexpr bool MASK = decltype(mask_c)::value;
+        if constexpr (MASK) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = pblk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row >= n_items) pend[r] = -INFINITY;
+            }
+        }
+        float m = fmaxf(fmaxf(pend[0], pend[1]), pend[2]);
+        m = fmaxf(fmaxf(m, pend[3]), pend[4]);
+        m = fmaxf(fmaxf(m, pend[5]), pend[6]);
+        return fmaxf(m, pend[7]);
+    };
+    auto reduce_hi_append = [&](float m) {
+        m = fmaxf(fmaxf(m, pend[8]), pend[9]);
+        m = fmaxf(fmaxf(m, pend[10]), pend[11]);
+        m = fmaxf(fmaxf(m, pend[12]), pend[13]);
+        m = fmaxf(fmaxf(m, pend[14]), pend[15]);
+        // inline-asm store: invisible to hipcc's waitcnt pass, which would
+        // otherwise drain the in-flight LDS-DMA before every list append
+        const uint2 ent = make_uint2(__float_as_uint(m), (uint32_t)(pblk * 2 + h));
+        asm volatile("ds_write_b64 %0, %1" ::"v"(list_lds + (uint32_t)n * (WAVE * 8)), "v"(ent)
+                     : "memory");
+        n += (m > tau) ? 1 : 0;
+    };
+    auto tile_body = [&](int t, const u32x4 (&afr)[TB][DS], auto mask_c) {
+#pragma unroll
+        for (int b = 0; b < TB; ++b) {
+            f32x16 acc = f32x16{};
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afr[b][0]), ufrag[0], acc, 0, 0, 0);
+            const float m = reduce_lo(mask_c);
+#pragma unroll
+            for (int s = 1; s < DS; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afr[b][s]), ufrag[s], acc, 0, 0, 0);
+            reduce_hi_append(m);
+            pend = acc;
+            pblk = t * TB + b;
+        }
+        if constexpr (!decltype(mask_c)::value && DS == 2) {
+            // per block: MFMA k0 | 8 VALU (low-half max of the pending block)
+            // | MFMA k1 | the rest (high-half max, compare, append): the
+            // pending block's reduction runs under this block's MFMAs
+#pragma unroll
+            for (int b = 0; b < TB; ++b) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            }
+        }
+    };
+    // tiles whose blocks (and the pending block before them) are all full
+    const int full_tiles = tail_blk / TB;
+    auto step = [&](int t) {
 #ifdef NRK_SCREEN_STATS
         const unsigned long long w0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -383,26 +438,38 @@ __global__ __launch_bounds__(256, 1) void ip_screen_kernel(
         __builtin_amdgcn_s_barrier();
 #ifdef NRK_SCREEN_STATS
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        st_slow += __builtin_amdgcn_s_memtime() - w0;  // cycles in vmcnt wait + barrier
+        const unsigned long long w1 = __builtin_amdgcn_s_memtime();
+        st_slow += w1 - w0;
 #endif
         issue_tile(t + NSLOT - 1);
-        compute_tile(t, slot_c);
+        u32x4 afr[TB][DS];
+        read_frags(t, afr);
+        __builtin_amdgcn_sched_barrier(0);  // no MFMA hoisted above the fragment wait
+        if (t < full_tiles) tile_body(t, afr, std::false_type{});
+        else tile_body(t, afr, std::true_type{});
+#ifdef NRK_SCREEN_STATS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        st_cyc_slow += __builtin_amdgcn_s_memtime() - w1;
+#endif
     };
 #pragma unroll
     for (int p = 0; p < NSLOT - 1; ++p) issue_tile(p);
-    for (int t = 0;; t += NSLOT) {
-        if (t < ntile) phase(t, std::integral_constant<int, 0>{});
-        if (t + 1 < ntile) phase(t + 1, std::integral_constant<int, 1>{});
-        if constexpr (NSLOT == 3)
-            if (t + 2 < ntile) phase(t + 2, std::integral_constant<int, 2>{});
+    for (int t = 0;; t += 2) {
+        step(t);
+        if (t + 1 < ntile) step(t + 1);
+        const bool fin = t + 2 >= ntile;
+        if (fin) {  // the last block's max (masked path: it may be partial)
+            const float m = reduce_lo(std::true_type{});
+            reduce_hi_append(m);
+        }
         // compaction (one code site; the final pass always compacts): keep
-        // room for the next NSLOT tiles' appends
-        const bool fin = t + NSLOT >= ntile;
-        if (fin || __ballot(active && n > IP_CL - NSLOT * TB)) {
+        // room for the next two tiles' appends
+        if (fin || __ballot(active && n > IP_CL - 2 * TB)) {
 #ifdef NRK_SCREEN_STATS
             const unsigned long long st_f0 = __builtin_amdgcn_s_memtime();
 #endif
-            lanes_flush<IP_CL - NSLOT * TB>(L, n, tau, theta, ovf, k, eps_s, active);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lanes_flush<IP_CL - 2 * TB>(L, n, tau, theta, ovf, k, eps_s, active);
 #ifdef NRK_SCREEN_STATS
             ++st_flush;
             st_cyc_flush += __builtin_amdgcn_s_memtime() - st_f0;
