@@ -86,13 +86,16 @@ int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const v
                 nrk_stream_t stream);
 
 /* The two phases of nrk_ip_topk, for callers that pipeline or time them:
- * screen (bf16 MFMA scan -> per-user candidate band in the workspace) and
+ * screen (fp16 MFMA scan -> per-user candidate band in the workspace) and
  * finish (exact fp64 rescoring + ordering, exact fallback for overflowed
- * users).  finish must follow screen on the same workspace. */
+ * users).  finish must follow screen on the same workspace.  finish reads
+ * the packed catalog (may be NULL) for an fp16 prefilter of the candidate
+ * band before the exact fp32-row rescoring. */
 int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
                        int dim, int k, void* workspace, size_t workspace_bytes,
                        nrk_stream_t stream);
-int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items, int64_t n_items,
+int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
+                       const void* catalog, int64_t n_items,
                        int dim, int k, int64_t row_offset, float* out_scores, int32_t* out_rows,
                        double* out_exact, void* workspace, size_t workspace_bytes,
                        nrk_stream_t stream);

@@ -535,14 +535,23 @@ __device__ __forceinline__ double exact_dot(const float* __restrict__ a, const f
 
 constexpr int IP_SURV = 128;  // exact survivors per user held by the refine
 
+// DS4 = dim / 4 when the candidate rows are staged through LDS (dim 16, 32,
+// 64): every 64-item round loads the rows with whole-row coalesced float4
+// pieces (64 / DS4 rows per instruction) into a padded per-wave LDS stage,
+// then each lane sums its own row sequentially (the oracle's order).
+// DS4 = 0: the generic per-lane gather.
+template <int DS4>
 __global__ __launch_bounds__(256) void ip_refine_kernel(
     const float* __restrict__ users, int64_t n_users, const float* __restrict__ items,
-    int64_t n_items, int dim, int k, int64_t row_offset, const uint2* __restrict__ cand,
+    const uint8_t* __restrict__ catalog, int64_t n_items, int dim, int k, int64_t row_offset,
+    const uint2* __restrict__ cand,
     const int32_t* __restrict__ cand_cnt, const float2* __restrict__ ucut,
     const int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
     int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
     double* __restrict__ out_e) {
     __shared__ Cand surv[4][IP_SURV];
+    constexpr int RS = DS4 + 1;  // staged row stride in float4 (one float4 of padding)
+    __shared__ float4 stage[DS4 > 0 ? 4 : 1][DS4 > 0 ? 64 * RS : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users || ovf_flag[u]) return;
@@ -568,6 +577,28 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         thr = thr - fabs(thr) * 1e-15 - 1e-300;  // round down
     }
     const int nitem = (n0 + n1) * 16;
+    // fp16 prefilter (DS4 > 0 with a packed catalog): recompute every band
+    // item's scaled fp16 score from the 64-B packed row and keep it when it
+    // reaches the screen's cut -- |fp16 score - exact| <= eps as in the
+    // screen, so every item with exact >= cut + eps passes.  Only those rows
+    // are then fetched in fp32 for the exact score.
+    constexpr int DSK = DS4 / 4;  // 16-dim k-steps of the packed layout
+    bool pre = DS4 > 0 && catalog != nullptr && ce.x != -INFINITY;
+    float ush[DS4 > 0 ? 4 * DS4 : 1];
+    float pcut = 0.0f;
+    if constexpr (DS4 > 0) {
+        if (pre) {
+            const int nblk_c = (int)((n_items + 31) >> 5);
+            const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk_c * 64 * (4 * DS4));
+            float ua = 0.0f;
+#pragma unroll
+            for (int d = 0; d < 4 * DS4; ++d) ua = fmaxf(ua, fabsf(uv[d]));
+            const float su = pow2_scale(ua);
+#pragma unroll
+            for (int d = 0; d < 4 * DS4; ++d) ush[d] = (float)(_Float16)(uv[d] * su);
+            pcut = ce.x * (su * hdr->scale);  // exact power-of-two rescale
+        }
+    }
     int cnt = 0;
     for (int base = 0; base < nitem; base += WAVE) {
         const int idx = base + lane;
@@ -578,9 +609,60 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
             const int b = idx >> 4, r = idx & 15;
             const uint32_t q = (b < n0) ? cand[(2 * u) * IP_CW + b].y : cand[(2 * u + 1) * IP_CW + (b - n0)].y;
             const int64_t rr = (int64_t)(q >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (q & 1);
-            if (rr < n_items) {
-                row = (int32_t)rr;
-                s = exact_dot(uv, items + rr * dim, dim);
+            if (rr < n_items) row = (int32_t)rr;
+            keep = rr < n_items;
+            if constexpr (DS4 > 0) {
+                if (pre && keep) {
+                    const int blk = (int)(rr >> 5), il = (int)(rr & 31);
+                    const uint8_t* bp = catalog + (size_t)blk * (64 * 4 * DS4);
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int st = 0; st < DSK; ++st)
+#pragma unroll
+                        for (int hh = 0; hh < 2; ++hh) {
+                            const uint4 pc = *reinterpret_cast<const uint4*>(bp + st * 1024 + (il + 32 * hh) * 16);
+                            const f16x8 hv = __builtin_bit_cast(f16x8, pc);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e)
+                                acc = fmaf((float)hv[e], ush[16 * st + 8 * hh + e], acc);
+                        }
+                    keep = acc >= pcut;
+                }
+            }
+        }
+        if constexpr (DS4 > 0) {
+            // coalesced staging of this round's 64 rows
+#pragma unroll
+            for (int it = 0; it < DS4; ++it) {
+                const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
+                const int r_item = __shfl(row, item, WAVE);
+                const bool ok_item = __shfl((int)keep, item, WAVE) != 0;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (ok_item) v = reinterpret_cast<const float4*>(items + (int64_t)r_item * dim)[part];
+                stage[wave][item * RS + part] = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (keep) {
+                const float4* a4 = reinterpret_cast<const float4*>(uv);
+                const float4* b4 = &stage[wave][lane * RS];
+                double acc = 0.0;
+#pragma unroll
+                for (int t = 0; t < DS4; ++t) {
+                    const float4 x = a4[t], y = b4[t];
+                    acc += (double)x.x * (double)y.x;
+                    acc += (double)x.y * (double)y.y;
+                    acc += (double)x.z * (double)y.z;
+                    acc += (double)x.w * (double)y.w;
+                }
+                s = acc + 0.0;
+                keep = s >= thr;
+            }
+            __builtin_amdgcn_wave_barrier();  // the stage is rewritten next round
+        } else {
+            if (keep) {
+                s = exact_dot(uv, items + (int64_t)row * dim, dim);
                 keep = s >= thr;
             }
         }
@@ -882,7 +964,8 @@ int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog,
     return NRK_OK;
 }
 
-int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items, int64_t n_items,
+int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
+                       const void* catalog, int64_t n_items,
                        int dim, int k, int64_t row_offset, float* out_scores, int32_t* out_rows,
                        double* out_exact, void* workspace, size_t workspace_bytes,
                        nrk_stream_t stream) {
@@ -893,9 +976,17 @@ int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items, 
     const IpWs w = ip_ws_layout(workspace, n_users);
     hipStream_t s = as_stream(stream);
     const int g2 = (int)((n_users + 3) / 4);
-    ip_refine_kernel<<<g2, 256, 0, s>>>(users, n_users, items, n_items, dim, k, row_offset, w.cand,
-                                        w.cnt, w.ucut, w.ovf_flag, w.ovf_list, w.ovf_count,
-                                        out_scores, out_rows, out_exact);
+#define NRK_REFINE(DS4)                                                                        \
+    ip_refine_kernel<DS4><<<g2, 256, 0, s>>>(users, n_users, items,                             \
+                                             reinterpret_cast<const uint8_t*>(catalog), n_items, \
+                                             dim, k, row_offset,                                 \
+                                             w.cand, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,      \
+                                             w.ovf_count, out_scores, out_rows, out_exact)
+    if (dim == 32) NRK_REFINE(8);
+    else if (dim == 16) NRK_REFINE(4);
+    else if (dim == 64) NRK_REFINE(16);
+    else NRK_REFINE(0);
+#undef NRK_REFINE
     if (n_items > 0)
         ip_fallback_kernel<<<256, 256, 0, s>>>(users, items, n_items, dim, k, row_offset, w.ovf_list,
                                                w.ovf_count, out_scores, out_rows, out_exact);
@@ -910,7 +1001,7 @@ int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const v
     int rc = nrk_ip_topk_screen(users, n_users, catalog, n_items, dim, k, workspace,
                                 workspace_bytes, stream);
     if (rc != NRK_OK) return rc;
-    return nrk_ip_topk_finish(users, n_users, items, n_items, dim, k, row_offset, out_scores,
+    return nrk_ip_topk_finish(users, n_users, items, catalog, n_items, dim, k, row_offset, out_scores,
                               out_rows, out_exact, workspace, workspace_bytes, stream);
 }
 

@@ -159,7 +159,7 @@ def ip_topk_finish(users, catalog: Catalog, k: int, workspace, out_scores, out_r
     """Phase 2 of ip_topk (exact rescoring + ordering) into preallocated outputs."""
     _dev(users, workspace, out_scores, out_rows, out_exact)
     n = users.shape[0]
-    _lib.call("nrk_ip_topk_finish", _ptr(users), n, _ptr(catalog.items), catalog.n, catalog.d, k,
+    _lib.call("nrk_ip_topk_finish", _ptr(users), n, _ptr(catalog.items), _ptr(catalog.packed), catalog.n, catalog.d, k,
               int(row_offset), _ptr(out_scores), _ptr(out_rows), _ptr(out_exact), _ptr(workspace),
               workspace.numel(), _stream())
 
