@@ -97,16 +97,20 @@ def recall_workload(seed: int, n_users: int, n_items: int, dim: int, device):
     }
 
 
-def cpu_baseline_recall(users_np, items_np, k, sample, threads):
-    """The oracle's exact per-user scan (reference nq=1 IndexFlatIP shape)."""
+def cpu_baseline_recall(users_np, items_np, k, sample, threads, seconds):
+    """The oracle's exact per-user scan (reference nq=1 IndexFlatIP shape),
+    chunks of `sample` users until `seconds` of CPU work have been timed."""
     from oracle import oracle
 
-    q = users_np[:sample]
-    oracle.ip_topk(q[:8], items_np, k, nthreads=threads)  # warm
-    t0 = time.perf_counter()
-    oracle.ip_topk(q, items_np, k, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return sample * (k - 1) / dt, dt
+    oracle.ip_topk(users_np[:8], items_np, k, nthreads=threads)  # warm
+    done, dt = 0, 0.0
+    while dt < seconds and done < len(users_np):
+        q = users_np[done:done + sample]
+        t0 = time.perf_counter()
+        oracle.ip_topk(q, items_np, k, nthreads=threads)
+        dt += time.perf_counter() - t0
+        done += len(q)
+    return done * (k - 1) / dt, dt, done
 
 
 DIN_SAMPLES = 675_653  # README.md:28 (BASELINE config 3)
@@ -205,15 +209,21 @@ def run_din(args, device, rank, world):
         from oracle import oracle
 
         m = args.din_cpu_sample
-        sl = {k: v[:m] for k, v in enc.items()}
         sdn = {k: v.numpy() for k, v in sd.items()}
-        t1 = time.perf_counter()
-        po, _, _ = oracle.din_forward(sdn, sl["user"], sl["item"], sl["hist"], sl["ctx"], sl["mask"], feats,
-                                      round_bf16=True)
-        cdt = time.perf_counter() - t1
-        out["cpu_baseline"] = {"value": round(m / cdt, 1), "unit": "DIN scored pairs/s",
+        cdt, nb = 0.0, 0
+        while cdt < args.cpu_seconds and (nb + 1) * m <= n:  # whole B-sample batches, like the reference
+            sl = {k: v[nb * m:(nb + 1) * m] for k, v in enc.items()}
+            t1 = time.perf_counter()
+            pb, _, _ = oracle.din_forward(sdn, sl["user"], sl["item"], sl["hist"], sl["ctx"], sl["mask"], feats,
+                                          round_bf16=True)
+            cdt += time.perf_counter() - t1
+            if nb == 0:
+                po = pb
+            nb += 1
+        out["cpu_baseline"] = {"value": round(nb * m / cdt, 1), "unit": "DIN scored pairs/s",
                                "cores": torch.get_num_threads(), "kind": "port",
-                               "sample": f"one {m}-sample batch, numpy fp32 forward (oracle/oracle.py), {cdt:.1f}s"}
+                               "sample": f"{nb} batches x {m} samples of the same workload, numpy fp32 forward "
+                                         f"(oracle/oracle.py), {cdt:.1f}s"}
         gp = ops.din_forward(p, *(dev[k][:m] for k in ("user", "item", "hist", "ctx", "mask")), workspace=ws)
         err = float(np.abs(gp.cpu().numpy() - po).max())
         log(f"DIN spot-check vs oracle ({m} samples): max |dp| = {err:.2e}")
@@ -230,6 +240,8 @@ def main():
     ap.add_argument("--dim", type=int, default=32)
     ap.add_argument("--topk", type=int, default=30)
     ap.add_argument("--cpu-sample", type=int, default=2048)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU work timed for each cpu_baseline leg (chunks of --cpu-sample users / batches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-din", action="store_true")
     ap.add_argument("--shard", choices=["users", "catalog"], default="users",
@@ -354,10 +366,10 @@ def main():
         threads = min(16, os.cpu_count() or 1)
         u = step()
         torch.cuda.synchronize()
-        v, dt = cpu_baseline_recall(u.cpu().numpy(), item_vec.cpu().numpy(), K,
-                                    args.cpu_sample, threads)
+        v, dt, nu = cpu_baseline_recall(u.cpu().numpy(), item_vec.cpu().numpy(), K,
+                                        args.cpu_sample, threads, args.cpu_seconds)
         cpu = {"value": round(v, 1), "unit": "recalled pairs/s", "cores": threads, "kind": "port",
-               "sample": f"{args.cpu_sample} users x {I} items exact fp64 top-{K} scan "
+               "sample": f"first {nu} of the same {U} users x {I} items, exact fp64 top-{K} scan "
                          f"(oracle/nrk_oracle.c, {dt:.1f}s)"}
         # correctness spot check of the timed outputs against the oracle
         from oracle import oracle

@@ -36,10 +36,8 @@ namespace nrk {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int IP_CL = 64;          // per-lane candidate list capacity (LDS)
-constexpr int IP_CW = IP_CL - 16;  // entries kept per lane after the final flush
+constexpr int IP_CW = 48;  // candidate entries per (user, half) slot of the workspace
 constexpr int IP_KMAX = 32;
-constexpr int IP_USERS_PER_WG = 128;  // 4 waves x 32 users
 constexpr size_t CATALOG_HDR = 256;
 
 static inline int pad_dim(int d) {
@@ -139,14 +137,62 @@ __device__ __forceinline__ float round_down_sub(float theta, float two_eps) {
                                     : (c == 0.0f ? 0x80000001u : __float_as_uint(c) + 1u));
 }
 
-// Register bitonic sort of 64 floats, descending (per lane, no cross-lane).
-__device__ __forceinline__ void sort64_desc(float (&x)[64]) {
+// ---- per-user candidate lists ---------------------------------------------
+// Each wave owns 32 users; user q's list lives in LDS as two SoA planes
+// (scores f32, half-block ids u32), entry j at plane + (j * 32 + q) * 4, so
+// the 32 lanes of a half-wave touch 128 consecutive bytes.  Both lanes of a
+// user (h = 0, 1: the two 16-item halves of every 32-item block) append to
+// the same list and keep identical copies of its count n, cut tau and theta.
+constexpr int SC_CL = 64;  // entries per user list
+
+__device__ __forceinline__ float lds_rd(uint32_t a) {
+    float v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_wr(uint32_t a, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+// 16 dwords at a + i * stride (i = 0..15), one wait for all of them.  Inline
+// asm: hipcc's waitcnt pass would drain the in-flight LDS-DMA (the ring
+// prefetch) in front of any compiler-visible LDS access.
+template <int STRIDE>
+__device__ __forceinline__ void lds_rd16(uint32_t a, uint32_t (&o)[16]) {
+    asm volatile(
+        "ds_read_b32 %0, %16 offset:%c17*0\n\tds_read_b32 %1, %16 offset:%c17*1\n\t"
+        "ds_read_b32 %2, %16 offset:%c17*2\n\tds_read_b32 %3, %16 offset:%c17*3\n\t"
+        "ds_read_b32 %4, %16 offset:%c17*4\n\tds_read_b32 %5, %16 offset:%c17*5\n\t"
+        "ds_read_b32 %6, %16 offset:%c17*6\n\tds_read_b32 %7, %16 offset:%c17*7\n\t"
+        "ds_read_b32 %8, %16 offset:%c17*8\n\tds_read_b32 %9, %16 offset:%c17*9\n\t"
+        "ds_read_b32 %10, %16 offset:%c17*10\n\tds_read_b32 %11, %16 offset:%c17*11\n\t"
+        "ds_read_b32 %12, %16 offset:%c17*12\n\tds_read_b32 %13, %16 offset:%c17*13\n\t"
+        "ds_read_b32 %14, %16 offset:%c17*14\n\tds_read_b32 %15, %16 offset:%c17*15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]),
+          "=&v"(o[6]), "=&v"(o[7]), "=&v"(o[8]), "=&v"(o[9]), "=&v"(o[10]), "=&v"(o[11]),
+          "=&v"(o[12]), "=&v"(o[13]), "=&v"(o[14]), "=&v"(o[15])
+        : "v"(a), "n"(STRIDE)
+        : "memory");
+}
+
+// value of lane l ^ 32 (v_permlane32_swap: lanes 32-63 of vdst <-> lanes
+// 0-31 of src; with vdst = src = v, r[0] = [lo, lo], r[1] = [hi, hi])
+__device__ __forceinline__ uint32_t partner32(uint32_t v, int h) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return h ? (uint32_t)r[0] : (uint32_t)r[1];
+}
+__device__ __forceinline__ float partner32f(float v, int h) {
+    return __uint_as_float(partner32(__float_as_uint(v), h));
+}
+
+// Register bitonic sort of 32 floats, descending (per lane).
+__device__ __forceinline__ void sort32_desc(float (&x)[32]) {
 #pragma unroll
-    for (int kl = 1; kl <= 6; ++kl) {
+    for (int kl = 1; kl <= 5; ++kl) {
 #pragma unroll
         for (int jl = kl - 1; jl >= 0; --jl) {
 #pragma unroll
-            for (int i = 0; i < 64; ++i) {
+            for (int i = 0; i < 32; ++i) {
                 const int p = i ^ (1 << jl);
                 if (p > i) {
                     const bool desc = ((i >> kl) & 1) == 0;
@@ -160,86 +206,120 @@ __device__ __forceinline__ void sort64_desc(float (&x)[64]) {
     }
 }
 
-struct LaneList {
-    uint2* base;  // this wave's list area: entry j of lane at base[j * 64 + lane]
-    int lane;
-    __device__ __forceinline__ uint2 get(int j) const { return base[j * WAVE + lane]; }
-    __device__ __forceinline__ void put(int j, uint2 v) const { base[j * WAVE + lane] = v; }
-};
-
-// Compact every lane's list: theta = k-th largest listed sub-block max,
-// keep entries >= theta - 2 eps (eps == 0: exactly the first k in list
-// order among ties -- the zero user, whose scores are exact).  Only the 64
-// scores live in registers; compaction re-reads the list in 16-entry chunks
-// (writes go to positions <= the chunk being read, so chunks stay intact).
-template <int CAP>  // entries a lane may keep: room for one tile of appends
-__device__ __forceinline__ void lanes_flush(const LaneList& L, int& n, float& tau, float& theta,
-                                            bool& ovf, int k, float eps, bool active) {
-    float x[IP_CL];
+// Compact user q's list (both lanes of the user run this in lock step):
+// theta = k-th largest listed half-block max (a lower bound of the user's
+// k-th largest score: k distinct half-blocks each hold an item with
+// fp16 score >= theta), keep the entries >= cut = theta - 2 eps.  Lane h
+// sorts entries [32h, 32h + 32); the top 32 of the union is max(own[i],
+// partner[31 - i]) (one bitonic merge step), sorted again to read the k-th.
+// A user whose kept band does not leave room for the next tile's appends
+// (dense exact ties) stops appending and is redone by the exact fallback.
+__device__ __forceinline__ void user_flush(uint32_t ls, uint32_t li, int h, int& n, float& tau,
+                                           float& theta, bool& ovf, int k, float eps, int cap) {
+    const uint32_t as = ls + (uint32_t)h * (32u * 32u * 4u), ai = li + (uint32_t)h * (32u * 32u * 4u);
+    uint32_t raw[16];
+    float x[32];
+    const int nv = n - 32 * h;  // valid entries in this lane's half
+    lds_rd16<128>(as, raw);
 #pragma unroll
-    for (int j = 0; j < IP_CL; ++j) {
-        const float v = __uint_as_float(L.base[j * WAVE + L.lane].x);
-        x[j] = (active && j < n) ? v : -INFINITY;
-    }
-    if (!(active && n >= k)) return;
-    sort64_desc(x);
-    float th = x[0];
-    int gt = 0;
+    for (int i = 0; i < 16; ++i) x[i] = i < nv ? __uint_as_float(raw[i]) : -INFINITY;
+    lds_rd16<128>(as + 16 * 128, raw);
 #pragma unroll
-    for (int j = 1; j < IP_CL; ++j) th = (j == k - 1) ? x[j] : th;
+    for (int i = 0; i < 16; ++i) x[16 + i] = 16 + i < nv ? __uint_as_float(raw[i]) : -INFINITY;
+    sort32_desc(x);
+    float z[32];
 #pragma unroll
-    for (int j = 0; j < IP_CL; ++j) gt += (x[j] > th) ? 1 : 0;
-    const float cut = (eps == 0.0f) ? th : round_down_sub(th, 2.0f * eps);
-    const int eq_allow = k - gt;
-    int m = 0, eq_seen = 0;
+    for (int i = 0; i < 32; ++i) z[i] = fmaxf(x[i], partner32f(x[31 - i], h));
+    // z is bitonic: merge it descending
 #pragma unroll
-    for (int c = 0; c < IP_CL; c += 16) {
-        uint2 e[16];
+    for (int jl = 4; jl >= 0; --jl) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) e[j] = L.get(c + j);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const float s = __uint_as_float(e[j].x);
-            bool keep = c + j < n;
-            if (eps == 0.0f) {
-                keep = keep && (s > th || (s == th && eq_seen < eq_allow));
-                eq_seen += (c + j < n && s == th) ? 1 : 0;
-            } else {
-                keep = keep && s >= cut;
-            }
-            if (keep && m < CAP) {
-                L.put(m, e[j]);
-                ++m;
-            } else if (keep) {
-                ovf = true;  // band denser than the list: the user is redone exactly
+        for (int i = 0; i < 32; ++i) {
+            const int p = i ^ (1 << jl);
+            if (p > i) {
+                const float a = z[i], b = z[p];
+                z[i] = fmaxf(a, b);
+                z[p] = fminf(a, b);
             }
         }
     }
-    n = m;
+    float th = z[0];
+#pragma unroll
+    for (int j = 1; j < 32; ++j) th = (j == k - 1) ? z[j] : th;
+    const float cut = (th == -INFINITY) ? -INFINITY : round_down_sub(th, 2.0f * eps);
+    // re-read (score, id) in list order and compact: lane 0's kept entries go
+    // to [0, c0), lane 1's to [c0, c0 + c1); a dropped entry is written to
+    // slot SC_CL - 1, which no kept entry reaches unless the user overflows.
+    uint32_t s[32], id[32];
+    lds_rd16<128>(as, raw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = raw[i];
+    lds_rd16<128>(as + 16 * 128, raw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[16 + i] = raw[i];
+    lds_rd16<128>(ai, raw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) id[i] = raw[i];
+    lds_rd16<128>(ai + 16 * 128, raw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) id[16 + i] = raw[i];
+    uint32_t keepm = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+        keepm |= (i < nv && __uint_as_float(s[i]) >= cut) ? (1u << i) : 0u;
+    const int c_own = __popc(keepm);
+    const int c_par = (int)partner32((uint32_t)c_own, h);
+    int pos = h ? c_par : 0;
+    const uint32_t ls0 = ls - (uint32_t)0, dump = (uint32_t)(SC_CL - 1) * 128u;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const bool kp = (keepm >> i) & 1u;
+        const uint32_t off = kp ? (uint32_t)pos * 128u : dump;
+        lds_wr(ls0 + off, s[i]);
+        lds_wr(li + off, id[i]);
+        pos += kp ? 1 : 0;
+    }
+    const int nn = c_own + c_par;
     theta = th;
-    tau = ovf ? INFINITY : fmaxf(tau, cut);  // an overflowed user is redone exactly
+    if (nn > cap) {
+        ovf = true;
+        tau = INFINITY;
+        n = 0;
+    } else {
+        n = nn;
+        tau = fmaxf(tau, cut);
+    }
 }
 
-template <int DP>
-__global__ __launch_bounds__(256, 1) void ip_screen_kernel(
+// Screen: 8 waves (2 per SIMD) x 32 users per workgroup share one LDS ring of
+// catalog tiles.  Per tile every wave runs TB x DS MFMAs, takes each lane's
+// half-block max and, when any lane beats its user's cut, appends those
+// maxima to the user lists (branch per tile).  Lists are compacted when one
+// is nearly full; a flush requested by any wave is joined by the others at
+// the same tile (they all meet at the per-tile barrier anyway), through an
+// LDS hint word.
+template <int DP, int NW>
+__global__ __launch_bounds__(NW * 64, NW / 4) void ip_screen_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog,
     int n_items, int dim, int k, uint2* __restrict__ cand, int32_t* __restrict__ cand_cnt,
     float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
     int32_t* __restrict__ ovf_count) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
-    constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : (8192 / BLOCK_BYTES > 4 ? 4 : 8192 / BLOCK_BYTES);
+    constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : 8192 / BLOCK_BYTES;
     constexpr int TILE_BYTES = TB * BLOCK_BYTES;
-    constexpr int LPT = TILE_BYTES / (256 * 16);  // 1-KB LDS-DMA pieces per wave per tile
-    constexpr int LIST_BYTES = 4 * IP_CL * WAVE * 8;
-    constexpr int NSLOT = (3 * TILE_BYTES + LIST_BYTES <= 163840) ? 3 : 2;  // LDS tile ring
-    // all LDS in ONE array (a second __shared__ object makes hipcc wait on
-    // the LDS-DMA before unrelated ds_reads)
-    __shared__ __attribute__((aligned(16))) uint8_t smem[NSLOT * TILE_BYTES + LIST_BYTES];
+    constexpr int LPT = TILE_BYTES / (NW * 64 * 16);  // 1-KB LDS-DMA pieces per wave per tile
+    static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
+    constexpr int NSLOT = 3;
+    constexpr int WLIST = 2 * SC_CL * 32 * 4;  // one wave's score + id planes
+    constexpr int CAP = SC_CL - 2 * TB;        // list size that still takes one tile of appends
+    constexpr int LDS = NSLOT * TILE_BYTES + NW * WLIST + 16;
+    static_assert(LDS <= 163840, "LDS budget");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[LDS];
 
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63, h = lane >> 5;
-    const int user = blockIdx.x * IP_USERS_PER_WG + wave * 32 + (lane & 31);
+    const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
+    const int user = blockIdx.x * (NW * 32) + wave * 32 + q;
     const bool active = user < n_users;
 
     const int nblk = (n_items + 31) >> 5;
@@ -249,7 +329,7 @@ __global__ __launch_bounds__(256, 1) void ip_screen_kernel(
     const float sv_scale = hdr->scale;
 
     // B operand: 32 users x DP dims, fp16 (scaled by a power of two); lane
-    // holds user (lane&31), dims 16s + 8h + [0, 8) for k-step s.
+    // holds user q, dims 16s + 8h + [0, 8) for k-step s.
     float uval[DS][8];
     float nrm2 = 0.0f, uabs = 0.0f;
     const float* urow = users + (size_t)(active ? user : 0) * dim;
@@ -278,28 +358,31 @@ __global__ __launch_bounds__(256, 1) void ip_screen_kernel(
     const float scl = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
     const float eps_s = eps * scl;
 
-    LaneList L{reinterpret_cast<uint2*>(smem + NSLOT * TILE_BYTES) + wave * IP_CL * WAVE, lane};
+    // zero users (all scores exactly 0) are answered by the refine directly
+    const bool live = active && nrm2 > 0.0f;
     int n = 0;
-    float tau = active ? -INFINITY : INFINITY, theta = -INFINITY;
+    float tau = live ? -INFINITY : INFINITY, theta = -INFINITY;
     bool ovf = false;
+
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
+    const uint32_t lst = lds_base + NSLOT * TILE_BYTES + wave * WLIST;
+    const uint32_t ls = lst + q * 4;                       // score plane, entry j at + j * 128
+    const uint32_t li = lst + SC_CL * 32 * 4 + q * 4;      // id plane
+    const uint32_t hint = lds_base + NSLOT * TILE_BYTES + NW * WLIST;
+    if (tid == 0) lds_wr(hint, 0xFFFFFFFFu);
 
     const int body_bytes = nblk * BLOCK_BYTES;
     const int tail_blk = n_items >> 5;  // first block holding a row >= n_items
     // Tile t -> ring slot t % NSLOT by LDS-DMA (global_load_lds_dwordx4: one
-    // 1-KB piece per wave-instruction, no VGPR staging, nothing for the
-    // compiler to sink); tiles past the end re-load the last piece (keeps
-    // the per-wave vmcnt accounting uniform, the data is never used).
-#ifdef NRK_SCREEN_STATS
-    // dev-only instrumentation (separate build): per wave flushes and cycles,
-    // written to ovf_list[n_users + 8 * gwave ...]
-    unsigned long long st_slow = 0, st_flush = 0, st_cyc_slow = 0, st_cyc_flush = 0;
-    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
-#endif
+    // 1-KB piece per wave-instruction, no VGPR staging); tiles past the end
+    // re-load the last piece (keeps the per-wave vmcnt accounting uniform,
+    // the data is never used).
     auto issue_tile = [&](int t) {
         uint8_t* slot = smem + (t % NSLOT) * TILE_BYTES;
 #pragma unroll
-        for (int q = 0; q < LPT; ++q) {
-            const int piece = q * 4 + wave;
+        for (int p = 0; p < LPT; ++p) {
+            const int piece = p * NW + wave;
             int off = t * TILE_BYTES + piece * 1024;
             off = off < body_bytes ? off : body_bytes - 1024;
             __builtin_amdgcn_global_load_lds(
@@ -307,209 +390,108 @@ __global__ __launch_bounds__(256, 1) void ip_screen_kernel(
                 (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16, 0, 0);
         }
     };
-    // one tile: TB blocks x DS k-steps of MFMA, then per block the lane's
-    // half-block max is appended branch-free (kept when it beats tau)
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
-    // this lane's list slot 0 (entry j at + j * 512)
-    const uint32_t list_lds = lds_base + NSLOT * TILE_BYTES + (wave * IP_CL * WAVE + lane) * 8;
-    // Software pipeline across tiles: the MFMAs of tile t+1 (accumulator set
-    // B) are issued before the max/append VALU work of tile t (set A), in one
-    // basic block, so the matrix core runs while the lane reduces the
-    // previous tile.  Fragment reads are inline asm: hipcc's waitcnt pass
-    // would otherwise put a vmcnt(0) (drain every LDS-DMA in flight, i.e. the
-    // prefetch) in front of any ds_read of the ring.  Ordering is explicit:
-    // the counted vmcnt + barrier retire the slot's DMA; lgkmcnt(0) retires
-    // these reads (and the previous tile's list appends).
     const uint32_t lds0 = lds_base + lane * 16;
-    // All reads and their lgkmcnt(0) sit in ONE asm statement: with the
-    // wait in a separate statement the compiler may copy an output register
-    // between the ds_read and the wait, i.e. before the data has landed.
-    auto read_frags = [&](int t, u32x4 (&afr)[TB][DS]) {
+    // all fragment reads and their wait in ONE asm statement (a separate wait
+    // statement lets the compiler copy an output before the data landed)
+    auto read_frags = [&](int t, u32x4 (&afr)[TB * DS]) {
         const uint32_t base = lds0 + (uint32_t)((t % NSLOT) * TILE_BYTES);
-        u32x4* f = &afr[0][0];
-        if constexpr (TB * DS == 4) {
+#pragma unroll
+        for (int g = 0; g < TB * DS; g += 4) {
+            u32x4* f = &afr[g];
             asm volatile(
                 "ds_read_b128 %0, %4 offset:0\n\tds_read_b128 %1, %4 offset:1024\n\t"
                 "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
                 "s_waitcnt lgkmcnt(0)"
                 : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3])
-                : "v"(base)
+                : "v"(base + 1024u * g)
                 : "memory");
-        } else if constexpr (TB * DS == 8) {
-            asm volatile(
-                "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:1024\n\t"
-                "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
-                "ds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:5120\n\t"
-                "ds_read_b128 %6, %8 offset:6144\n\tds_read_b128 %7, %8 offset:7168\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]),
-                  "=&v"(f[6]), "=&v"(f[7])
-                : "v"(base)
-                : "memory");
-        } else {
-            static_assert(TB * DS == 16, "fragment count");
-#pragma unroll
-            for (int half = 0; half < 2; ++half)
-                asm volatile(
-                    "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:1024\n\t"
-                    "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
-                    "ds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:5120\n\t"
-                    "ds_read_b128 %6, %8 offset:6144\n\tds_read_b128 %7, %8 offset:7168\n\t"
-                    "s_waitcnt lgkmcnt(0)"
-                    : "=&v"(f[8 * half + 0]), "=&v"(f[8 * half + 1]), "=&v"(f[8 * half + 2]),
-                      "=&v"(f[8 * half + 3]), "=&v"(f[8 * half + 4]), "=&v"(f[8 * half + 5]),
-                      "=&v"(f[8 * half + 6]), "=&v"(f[8 * half + 7])
-                    : "v"(base + 8192u * half)
-                    : "memory");
         }
     };
-    // Block-level software pipeline (one block of lag, carried across
-    // tiles): the two k-step MFMAs of block j are interleaved with the
-    // max/append VALU work of block j-1, so the matrix core and the VALU run
-    // together and only two 16-register accumulators are live.
-    // pend: the previous block's scores; pblk: its block index.
-    // (starts as an all -inf dummy: its append is written but never counted)
-    f32x16 pend;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) pend[r] = -INFINITY;
-    int pblk = 0;
-    // half-block max of the pending block; MASK zeroes rows >= n_items
-    auto reduce_lo = [&](auto mask_c) {
+    const int full_tiles = tail_blk / TB;  // tiles whose blocks are all full
+    auto tile = [&](int t, auto mask_c) {
         constexpr bool MASK = decltype(mask_c)::value;
-        if constexpr (MASK) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = pblk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row >= n_items) pend[r] = -INFINITY;
-            }
-        }
-        float m = fmaxf(fmaxf(pend[0], pend[1]), pend[2]);
-        m = fmaxf(fmaxf(m, pend[3]), pend[4]);
-        m = fmaxf(fmaxf(m, pend[5]), pend[6]);
-        return fmaxf(m, pend[7]);
-    };
-    auto reduce_hi_append = [&](float m) {
-        m = fmaxf(fmaxf(m, pend[8]), pend[9]);
-        m = fmaxf(fmaxf(m, pend[10]), pend[11]);
-        m = fmaxf(fmaxf(m, pend[12]), pend[13]);
-        m = fmaxf(fmaxf(m, pend[14]), pend[15]);
-        // inline-asm store: invisible to hipcc's waitcnt pass, which would
-        // otherwise drain the in-flight LDS-DMA before every list append
-        const uint2 ent = make_uint2(__float_as_uint(m), (uint32_t)(pblk * 2 + h));
-        asm volatile("ds_write_b64 %0, %1" ::"v"(list_lds + (uint32_t)n * (WAVE * 8)), "v"(ent)
-                     : "memory");
-        n += (m > tau) ? 1 : 0;
-    };
-    auto tile_body = [&](int t, const u32x4 (&afr)[TB][DS], auto mask_c) {
+        u32x4 afr[TB * DS];
+        read_frags(t, afr);
+        float m[TB];
 #pragma unroll
         for (int b = 0; b < TB; ++b) {
             f32x16 acc = f32x16{};
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afr[b][0]), ufrag[0], acc, 0, 0, 0);
-            const float m = reduce_lo(mask_c);
 #pragma unroll
-            for (int s = 1; s < DS; ++s)
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afr[b][s]), ufrag[s], acc, 0, 0, 0);
-            reduce_hi_append(m);
-            pend = acc;
-            pblk = t * TB + b;
+            for (int s = 0; s < DS; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afr[b * DS + s]),
+                                                             ufrag[s], acc, 0, 0, 0);
+            if constexpr (MASK) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = (t * TB + b) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row >= n_items) acc[r] = -INFINITY;
+                }
+            }
+            float v = fmaxf(fmaxf(acc[0], acc[1]), acc[2]);
+#pragma unroll
+            for (int r = 3; r < 15; r += 2) v = fmaxf(fmaxf(v, acc[r]), acc[r + 1]);
+            m[b] = fmaxf(v, acc[15]);
         }
-        if constexpr (!decltype(mask_c)::value && DS == 2) {
-            // per block: MFMA k0 | 8 VALU (low-half max of the pending block)
-            // | MFMA k1 | the rest (high-half max, compare, append): the
-            // pending block's reduction runs under this block's MFMAs
+        bool any = false;
+#pragma unroll
+        for (int b = 0; b < TB; ++b) any |= m[b] > tau;
+        if (__builtin_amdgcn_ballot_w64(any)) {
+            // both lanes of a user append in one go: lane 0 at n, lane 1 at
+            // n + (lane 0 appends)
 #pragma unroll
             for (int b = 0; b < TB; ++b) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                const bool c = m[b] > tau;
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(c);
+                const int c0 = (int)((bal >> q) & 1ull), c1 = (int)((bal >> (32 + q)) & 1ull);
+                const int pos = n + (h ? c0 : 0);
+                if (c) {
+                    lds_wr(ls + (uint32_t)pos * 128u, __float_as_uint(m[b]));
+                    lds_wr(li + (uint32_t)pos * 128u, (uint32_t)((t * TB + b) * 2 + h));
+                }
+                n += c0 + c1;
             }
         }
     };
-    // tiles whose blocks (and the pending block before them) are all full
-    const int full_tiles = tail_blk / TB;
-    auto step = [&](int t) {
-#ifdef NRK_SCREEN_STATS
-        const unsigned long long w0 = __builtin_amdgcn_s_memtime();
-#endif
-        if constexpr (NSLOT == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-#ifdef NRK_SCREEN_STATS
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const unsigned long long w1 = __builtin_amdgcn_s_memtime();
-        st_slow += w1 - w0;
-#endif
-        issue_tile(t + NSLOT - 1);
-        u32x4 afr[TB][DS];
-        read_frags(t, afr);
-        __builtin_amdgcn_sched_barrier(0);  // no MFMA hoisted above the fragment wait
-        if (t < full_tiles) tile_body(t, afr, std::false_type{});
-        else tile_body(t, afr, std::true_type{});
-#ifdef NRK_SCREEN_STATS
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        st_cyc_slow += __builtin_amdgcn_s_memtime() - w1;
-#endif
-    };
+
 #pragma unroll
     for (int p = 0; p < NSLOT - 1; ++p) issue_tile(p);
-    for (int t = 0;; t += 2) {
-        step(t);
-        if (t + 1 < ntile) step(t + 1);
-        const bool fin = t + 2 >= ntile;
-        if (fin) {  // the last block's max (masked path: it may be partial)
-            const float m = reduce_lo(std::true_type{});
-            reduce_hi_append(m);
-        }
-        // compaction (one code site; the final pass always compacts): keep
-        // room for the next two tiles' appends
-        if (fin || __ballot(active && n > IP_CL - 2 * TB)) {
-#ifdef NRK_SCREEN_STATS
-            const unsigned long long st_f0 = __builtin_amdgcn_s_memtime();
-#endif
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            lanes_flush<IP_CL - 2 * TB>(L, n, tau, theta, ovf, k, eps_s, active);
-#ifdef NRK_SCREEN_STATS
-            ++st_flush;
-            st_cyc_flush += __builtin_amdgcn_s_memtime() - st_f0;
-#endif
-        }
-        if (fin) break;
+    for (int t = 0; t < ntile; ++t) {
+        // own pieces of tile t landed (the next NSLOT-2 tiles' stay in
+        // flight), list appends done; the barrier publishes everyone's
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(LPT * (NSLOT - 2)) : "memory");
+        __builtin_amdgcn_s_barrier();
+        const int hv = (int)__builtin_amdgcn_readfirstlane((int)lds_rd(hint));
+        issue_tile(t + NSLOT - 1);
+        if (t < full_tiles) tile(t, std::false_type{});
+        else tile(t, std::true_type{});
+        // flush when a list cannot take the next tile's appends, or with the
+        // other waves when one of them flushes at this tile (hint)
+        const bool need = __builtin_amdgcn_ballot_w64(n > CAP) != 0;
+        const bool soon = __builtin_amdgcn_ballot_w64(n > CAP - 2 * TB) != 0;
+        if (soon && lane == 0) lds_wr(hint, (uint32_t)(t + 1));
+        if (need || (hv == t && __builtin_amdgcn_ballot_w64(n > SC_CL / 2) != 0))
+            user_flush(ls, li, h, n, tau, theta, ovf, k, eps_s, CAP);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
+    user_flush(ls, li, h, n, tau, theta, ovf, k, eps_s, CAP);
 
-#ifdef NRK_SCREEN_STATS
-    if (lane == 0) {
-        unsigned long long* st = reinterpret_cast<unsigned long long*>(ovf_list + n_users) +
-                                 8 * ((size_t)blockIdx.x * 4 + wave);
-        st[0] = st_slow;
-        st[1] = st_flush;
-        st[2] = st_cyc_slow;
-        st[3] = st_cyc_flush;
-        st[4] = __builtin_amdgcn_s_memtime() - st_t0;
-    }
-#endif
-    const float th_u = fmaxf(theta, __shfl_xor(theta, 32, WAVE));
-    const bool ovf_u = ovf || __shfl_xor((int)ovf, 32, WAVE);
     if (!active) return;
-    float cut = th_u;
-    if (eps_s != 0.0f && th_u != -INFINITY) cut = round_down_sub(th_u, 2.0f * eps_s);
-    int mcount = 0;
+    float cut = theta;
+    if (eps_s != 0.0f && theta != -INFINITY) cut = round_down_sub(theta, 2.0f * eps_s);
+    // lane 0 writes list entries [0, min(n, IP_CW)), lane 1 the rest
+    const int j0 = h ? IP_CW : 0, j1 = h ? n : (n < IP_CW ? n : IP_CW);
     uint2* dst = cand + ((size_t)user * 2 + h) * IP_CW;
-    for (int j = 0; j < n; ++j) {
-        const uint2 e = L.get(j);
-        if (!(__uint_as_float(e.x) >= cut)) continue;
-        if (mcount < IP_CW) dst[mcount] = e;
-        ++mcount;
+    for (int j = j0; j < j1; ++j) {
+        const float sc = lds_rd(ls + (uint32_t)j * 128u);
+        const uint32_t id = __float_as_uint(lds_rd(li + (uint32_t)j * 128u));
+        dst[j - j0] = make_uint2(__float_as_uint(sc), id);
     }
-    const bool ovf2 = ovf_u || (mcount > IP_CW) || __shfl_xor((int)(mcount > IP_CW), 32, WAVE);
-    cand_cnt[user * 2 + h] = mcount < IP_CW ? mcount : IP_CW;
+    cand_cnt[user * 2 + h] = j1 > j0 ? j1 - j0 : 0;
     if (h == 0) {
         // unscaled cut and eps for the refinement (exact power-of-two rescale)
         ucut[user] = make_float2(cut == -INFINITY ? -INFINITY : cut / scl, eps);
-        ovf_flag[user] = ovf2 ? 1 : 0;
-        if (ovf2) ovf_list[atomicAdd(ovf_count, 1)] = user;
+        ovf_flag[user] = ovf ? 1 : 0;
+        if (ovf) ovf_list[atomicAdd(ovf_count, 1)] = user;
     }
 }
 
@@ -941,22 +923,22 @@ int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog,
         return NRK_EHIP;
     }
     const int dp = pad_dim(dim);
-    const int grid = (int)((n_users + IP_USERS_PER_WG - 1) / IP_USERS_PER_WG);
     const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
     if (n_items == 0) {
         // nothing to search: every output row is padding
         (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * 2 * sizeof(int32_t), s);
         (void)hipMemsetAsync(w.ovf_flag, 0, (size_t)n_users * sizeof(int32_t), s);
     } else {
-#define NRK_SCREEN(DPV)                                                                     \
-    ip_screen_kernel<DPV><<<grid, 256, 0, s>>>(users, (int)n_users, cat, (int)n_items, dim, k, w.cand, \
-                                              w.cnt, w.ucut, w.ovf_flag, w.ovf_list, w.ovf_count)
+#define NRK_SCREEN(DPV, NWV)                                                               \
+    ip_screen_kernel<DPV, NWV><<<(int)((n_users + 32 * NWV - 1) / (32 * NWV)), 64 * NWV, 0, s>>>( \
+        users, (int)n_users, cat, (int)n_items, dim, k, w.cand, w.cnt, w.ucut, w.ovf_flag,       \
+        w.ovf_list, w.ovf_count)
         switch (dp) {
-            case 16: NRK_SCREEN(16); break;
-            case 32: NRK_SCREEN(32); break;
-            case 64: NRK_SCREEN(64); break;
-            case 128: NRK_SCREEN(128); break;
-            default: NRK_SCREEN(256); break;
+            case 16: NRK_SCREEN(16, 8); break;
+            case 32: NRK_SCREEN(32, 8); break;
+            case 64: NRK_SCREEN(64, 8); break;
+            case 128: NRK_SCREEN(128, 8); break;
+            default: NRK_SCREEN(256, 4); break;
         }
 #undef NRK_SCREEN
     }
