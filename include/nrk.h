@@ -184,6 +184,26 @@ int nrk_din_forward(const void* table, int table_dtype, const int64_t* row_base,
                     float* out_logits, void* workspace, size_t workspace_bytes,
                     nrk_stream_t stream);
 
+/* The whole of DINRanker.predict (DIN.py:1245-1283) in one call: n_samples
+ * rows scored as consecutive Dice batches of seg_len (the DataLoader's
+ * batch_size, shuffle=False), each batch with its own statistics -- the
+ * same result as nrk_din_forward once per batch, with every batch's phases
+ * in one launch each.  seg_len >= n_samples is one batch (n_samples >= 2);
+ * otherwise seg_len must be a multiple of 64.  A trailing batch of a single
+ * row has no std (NaN in the reference): its output is unspecified here and
+ * the caller marks it NaN.  Index tensors are [n_samples, ...] as above. */
+size_t nrk_din_segments_workspace_bytes(int64_t n_samples, int64_t seg_len, int seq_len, int n_user,
+                                        int n_item, int n_ctx, int h1, int h2);
+int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* row_base, int n_user,
+                             int n_item, int n_ctx, const int32_t* user_idx, const int32_t* item_idx,
+                             const int32_t* hist_idx, const int32_t* ctx_idx, const float* mask,
+                             int64_t n_samples, int64_t seg_len, int seq_len, const void* prep,
+                             const float* att_b0, const float* att_w1, const float* att_b1,
+                             const float* mlp_w0, const float* mlp_b0, int h1, const float* mlp_w1,
+                             const float* mlp_b1, int h2, const float* mlp_w2, const float* mlp_b2,
+                             float* out_probs, float* out_logits, void* workspace,
+                             size_t workspace_bytes, nrk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

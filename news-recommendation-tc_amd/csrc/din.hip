@@ -97,12 +97,16 @@ __device__ __forceinline__ void split8(const float (&x)[8], float s, din_half8& 
     }
 }
 
+// Segments: the N samples are scored as consecutive Dice batches of S
+// (DINRanker.predict's DataLoader batches, DIN.py:1245-1283); workgroup
+// blockIdx.x = seg * G + g strides over segment seg's samples, so partial row
+// blockIdx.x belongs to segment blockIdx.x / G.
 template <typename TT, int NI, int NTW>
 __global__ __launch_bounds__(256) void din_att_h_kernel(
     const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
-    const int32_t* __restrict__ item_idx, const int32_t* __restrict__ hist_idx, int64_t B, int T,
-    const float* __restrict__ prep, const float* __restrict__ att_b0, float* __restrict__ h_out,
-    double* __restrict__ partial) {
+    const int32_t* __restrict__ item_idx, const int32_t* __restrict__ hist_idx, int64_t N,
+    int64_t S, int G, int T, const float* __restrict__ prep, const float* __restrict__ att_b0,
+    float* __restrict__ h_out, double* __restrict__ partial) {
     constexpr int ID = NI * DIN_E;
     constexpr bool F32 = sizeof(TT) == 4;
     constexpr int NSLOT = DIN_JT * NI * 64;               // fragment lane-slots per pass
@@ -146,7 +150,9 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
 #pragma unroll
             for (int r = 0; r < 4; ++r) ssum[a][b][r] = ssq[a][b][r] = 0.0;
 
-    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    const int64_t seg = blockIdx.x / G;
+    const int64_t b_end = (seg + 1) * S < N ? (seg + 1) * S : N;
+    for (int64_t b = seg * S + blockIdx.x % G; b < b_end; b += G) {
         // (1) this wave's k rows -> A fragments (issued first: latency overlaps (2)-(4))
         din_half8 ahi[NTW][NI], alo[NTW][NI];
 #pragma unroll
@@ -293,17 +299,23 @@ __global__ void din_scales_kernel(const float* __restrict__ prep_ap, int ID, con
 }
 
 // ---------------------------------------------------------- 2. col stats --
-// mean and unbiased std (torch.std default) of each column over the batch,
-// from per-block fp64 (sum, sumsq) partials.  One wave per column: lane l
-// sums partials l, l+64, ... in order, then a fixed butterfly -- the same
-// order on every run (bitwise reproducible).
-__global__ __launch_bounds__(256) void col_stats_kernel(const double* __restrict__ partial, int nblk,
-                                                        int ncol, int64_t B, float2* __restrict__ stats) {
+// mean and unbiased std (torch.std default) of each column over one Dice
+// batch (segment blockIdx.x), from that segment's per-block fp64 (sum, sumsq)
+// partial rows [seg * bps, min((seg + 1) * bps, nblk)).  One wave per
+// column: lane l sums partials l, l+64, ... in order, then a fixed butterfly
+// -- the same order on every run (bitwise reproducible).  A one-sample
+// segment has no std (NaN in the reference); the host marks its output.
+__global__ __launch_bounds__(256) void col_stats_kernel(const double* __restrict__ partial, int bps,
+                                                        int nblk, int ncol, int64_t N, int64_t S,
+                                                        float2* __restrict__ stats) {
     const int lane = threadIdx.x & 63;
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int64_t seg = blockIdx.x;
     if (c >= ncol) return;
+    const int64_t k1 = (seg + 1) * bps < nblk ? (seg + 1) * bps : nblk;
+    const int64_t B = N - seg * S < S ? N - seg * S : S;
     double s = 0.0, ss = 0.0;
-    for (int k = lane; k < nblk; k += WAVE) {
+    for (int64_t k = seg * bps + lane; k < k1; k += WAVE) {
         const double2 v = *reinterpret_cast<const double2*>(partial + ((size_t)k * ncol + c) * 2);
         s += v.x;
         ss += v.y;
@@ -312,9 +324,9 @@ __global__ __launch_bounds__(256) void col_stats_kernel(const double* __restrict
     ss = wave_sum_f64(ss);
     if (lane == 0) {
         const double mean = s / (double)B;
-        double var = (ss - s * mean) / (double)(B - 1);
+        double var = B > 1 ? (ss - s * mean) / (double)(B - 1) : 0.0;
         if (var < 0.0) var = 0.0;
-        stats[c] = make_float2((float)mean, (float)sqrt(var));
+        stats[seg * ncol + c] = make_float2((float)mean, (float)sqrt(var));
     }
 }
 
@@ -330,8 +342,8 @@ __global__ __launch_bounds__(256) void din_att_out_kernel(
     const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user, int n_item,
     int n_ctx, const int32_t* __restrict__ user_idx, const int32_t* __restrict__ item_idx,
     const int32_t* __restrict__ hist_idx, const int32_t* __restrict__ ctx_idx,
-    const float* __restrict__ mask, int64_t B, int T, const float* __restrict__ h,
-    const float2* __restrict__ hstats, const float* __restrict__ att_w1,
+    const float* __restrict__ mask, int64_t B, int64_t S, int T, const float* __restrict__ h,
+    const float2* __restrict__ hstats_all, const float* __restrict__ att_w1,
     const float* __restrict__ att_b1, float* __restrict__ mlp_in) {
     __shared__ float prod[128 * DIN_H];
     __shared__ float wt[128];
@@ -343,6 +355,7 @@ __global__ __launch_bounds__(256) void din_att_out_kernel(
     for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
         __syncthreads();
         const float* hb = h + b * ncol;
+        const float2* hstats = hstats_all + (b / S) * ncol;
         for (int e = tid; e < ncol; e += 256) {
             const int j = e % DIN_H;
             const float2 st = hstats[e];
@@ -436,8 +449,8 @@ __device__ __forceinline__ void gemm_load(const float* __restrict__ A, const flo
 
 template <bool DICE_A>
 __global__ __launch_bounds__(512) void din_gemm_kernel(
-    const float* __restrict__ A, const float2* __restrict__ astats, const float* __restrict__ W,
-    const float* __restrict__ bias, int64_t M, int N, int K, float* __restrict__ C,
+    const float* __restrict__ A, const float2* __restrict__ astats_all, const float* __restrict__ W,
+    const float* __restrict__ bias, int64_t M, int64_t S, int N, int K, float* __restrict__ C,
     double* __restrict__ partial) {
     __shared__ float red[4][16][64];
     __shared__ double cs[2][2][64];
@@ -446,6 +459,8 @@ __global__ __launch_bounds__(512) void din_gemm_kernel(
     const int64_t m = (int64_t)blockIdx.x * 64 + wm * 32 + (lane & 31);
     const int n = blockIdx.y * 64 + wn * 32 + (lane & 31);
     const bool mok = m < M, nok = n < N;
+    // Dice statistics of row m's segment (its Dice batch)
+    const float2* astats = DICE_A ? astats_all + (mok ? m / S : 0) * K : nullptr;
     const int half = lane >> 5;
     din_f16v acc;
 #pragma unroll
@@ -504,13 +519,14 @@ __global__ __launch_bounds__(512) void din_gemm_kernel(
 }
 
 // ------------------------------------------------------------ 8. head --
-__global__ void din_head_kernel(const float* __restrict__ Z, const float2* __restrict__ zstats,
-                                int64_t B, int H, const float* __restrict__ w,
+__global__ void din_head_kernel(const float* __restrict__ Z, const float2* __restrict__ zstats_all,
+                                int64_t B, int64_t S, int H, const float* __restrict__ w,
                                 const float* __restrict__ bias, float* __restrict__ probs,
                                 float* __restrict__ logits) {
     const int lane = threadIdx.x & 63;
     const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= B) return;
+    const float2* zstats = zstats_all + (b / S) * H;
     float s = 0.0f;
     for (int j = lane; j < H; j += 64) {
         const float2 st = zstats[j];
@@ -539,7 +555,14 @@ __global__ void din_prepare_kernel(const float* __restrict__ w0, int ID, float* 
 }
 
 // ------------------------------------------------------------- workspace --
-constexpr int64_t DIN_ATT_GRID = 512;  // din_att_h workgroups (grid-strided over samples)
+// din_att_h workgroups per segment: about 2048 in the whole grid (8 per CU),
+// at most 512 per segment and never more than the segment has samples
+static inline int din_att_groups(int64_t N, int64_t S) {
+    const int64_t n_seg = (N + S - 1) / S;
+    int64_t g = (2048 + n_seg - 1) / n_seg;
+    g = g < 8 ? 8 : g > 512 ? 512 : g;
+    return (int)(g < S ? g : S);
+}
 
 struct DinWs {
     float* h;
@@ -557,25 +580,27 @@ struct DinWs {
 
 static inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static DinWs din_ws_layout(void* base, int64_t B, int T, int n_user, int n_item, int n_ctx, int h1,
-                           int h2) {
+// N samples in Dice batches (segments) of S
+static DinWs din_ws_layout(void* base, int64_t N, int64_t S, int T, int n_user, int n_item, int n_ctx,
+                           int h1, int h2) {
     DinWs w;
     uint8_t* p = reinterpret_cast<uint8_t*>(base);
     size_t o = 0;
-    const int64_t nb_att = B < DIN_ATT_GRID ? B : DIN_ATT_GRID;
-    const int64_t nb_m = (B + 63) / 64;
+    const int64_t n_seg = (N + S - 1) / S;
+    const int64_t nb_att = n_seg * din_att_groups(N, S);
+    const int64_t nb_m = (N + 63) / 64;
     const int IN = (n_user + n_ctx + 2 * n_item) * DIN_E;
     auto take = [&](size_t bytes) { uint8_t* r = p + o; o += al(bytes); return r; };
-    w.h = (float*)take((size_t)B * T * DIN_H * 4);
+    w.h = (float*)take((size_t)N * T * DIN_H * 4);
     w.hpart = (double*)take((size_t)nb_att * T * DIN_H * 16);
-    w.hstats = (float2*)take((size_t)T * DIN_H * 8);
-    w.mlp_in = (float*)take((size_t)B * IN * 4);
-    w.z1 = (float*)take((size_t)B * h1 * 4);
+    w.hstats = (float2*)take((size_t)n_seg * T * DIN_H * 8);
+    w.mlp_in = (float*)take((size_t)N * IN * 4);
+    w.z1 = (float*)take((size_t)N * h1 * 4);
     w.z1part = (double*)take((size_t)nb_m * h1 * 16);
-    w.z1stats = (float2*)take((size_t)h1 * 8);
-    w.z2 = (float*)take((size_t)B * h2 * 4);
+    w.z1stats = (float2*)take((size_t)n_seg * h1 * 8);
+    w.z2 = (float*)take((size_t)N * h2 * 4);
     w.z2part = (double*)take((size_t)nb_m * h2 * 16);
-    w.z2stats = (float2*)take((size_t)h2 * 8);
+    w.z2stats = (float2*)take((size_t)n_seg * h2 * 8);
     w.bytes = o;
     return w;
 }
@@ -613,10 +638,101 @@ int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int tabl
     return NRK_OK;
 }
 
+size_t nrk_din_segments_workspace_bytes(int64_t n_samples, int64_t seg_len, int seq_len, int n_user,
+                                        int n_item, int n_ctx, int h1, int h2) {
+    if (n_samples < 1 || seg_len < 1 || seq_len < 1) return 0;
+    if (seg_len > n_samples) seg_len = n_samples;
+    return din_ws_layout(nullptr, n_samples, seg_len, seq_len, n_user, n_item, n_ctx, h1, h2).bytes;
+}
+
 size_t nrk_din_workspace_bytes(int64_t batch, int seq_len, int n_user, int n_item, int n_ctx,
                                int h1, int h2) {
-    if (batch < 0 || seq_len < 1) return 0;
-    return din_ws_layout(nullptr, batch, seq_len, n_user, n_item, n_ctx, h1, h2).bytes;
+    return nrk_din_segments_workspace_bytes(batch, batch, seq_len, n_user, n_item, n_ctx, h1, h2);
+}
+
+int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* row_base, int n_user,
+                             int n_item, int n_ctx, const int32_t* user_idx, const int32_t* item_idx,
+                             const int32_t* hist_idx, const int32_t* ctx_idx, const float* mask,
+                             int64_t n_samples, int64_t seg_len, int seq_len, const void* prep,
+                             const float* att_b0, const float* att_w1, const float* att_b1,
+                             const float* mlp_w0, const float* mlp_b0, int h1, const float* mlp_w1,
+                             const float* mlp_b1, int h2, const float* mlp_w2, const float* mlp_b2,
+                             float* out_probs, float* out_logits, void* workspace,
+                             size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(table_dtype == 0 || table_dtype == 1, "table_dtype must be 0 (f32) or 1 (bf16)");
+    NRK_REQUIRE(n_samples >= 1 && seg_len >= 1, "n_samples and seg_len must be >= 1");
+    const int64_t batch = n_samples;
+    const int64_t S = seg_len < n_samples ? seg_len : n_samples;
+    const int64_t n_seg = (batch + S - 1) / S;
+    if (n_seg == 1)
+        NRK_REQUIRE(batch >= 2, "batch must be >= 2 (Dice uses the batch std; B = 1 is NaN in the reference)");
+    else
+        NRK_REQUIRE(S % 64 == 0, "seg_len must be a multiple of 64 when the samples span several segments");
+    NRK_REQUIRE(seq_len >= 1 && seq_len <= 128, "seq_len must be in [1, 128]");
+    NRK_REQUIRE(n_user >= 1 && n_ctx >= 0 && n_item >= 1, "bad feature counts");
+    if (n_item != 4 && n_item != 2 && n_item != 1) NRK_UNSUPPORTED("n_item must be 1, 2 or 4");
+    NRK_REQUIRE(h1 >= 1 && h1 <= 1024 && h2 >= 1 && h2 <= 1024, "hidden sizes out of range");
+    NRK_REQUIRE(table && row_base && user_idx && item_idx && hist_idx && mask && prep && att_b0 &&
+                    att_w1 && att_b1 && mlp_w0 && mlp_b0 && mlp_w1 && mlp_b1 && mlp_w2 && mlp_b2 &&
+                    out_probs && workspace,
+                "null pointer");
+    NRK_REQUIRE(n_ctx == 0 || ctx_idx, "ctx_idx null");
+    NRK_REQUIRE(n_seg < (1ll << 31) && batch < (1ll << 40), "too many samples");
+    const DinWs w = din_ws_layout(workspace, batch, S, seq_len, n_user, n_item, n_ctx, h1, h2);
+    NRK_REQUIRE(workspace_bytes >= w.bytes, "workspace too small");
+    hipStream_t s = as_stream(stream);
+    const int T = seq_len;
+    const int IN = (n_user + n_ctx + 2 * n_item) * DIN_E;
+    const int G = din_att_groups(batch, S);
+    const int64_t nb_att = n_seg * G;
+    NRK_REQUIRE(nb_att < (1ll << 31), "too many segments");
+    const float* pf = reinterpret_cast<const float*>(prep);
+#define NRK_ATT_H(TT, NI)                                                                              \
+    do {                                                                                               \
+        if (T <= 64)                                                                                   \
+            din_att_h_kernel<TT, NI, 1><<<(unsigned)nb_att, 256, 0, s>>>(                              \
+                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G, \
+                T, pf, att_b0, w.h, w.hpart);                                                          \
+        else                                                                                           \
+            din_att_h_kernel<TT, NI, 2><<<(unsigned)nb_att, 256, 0, s>>>(                              \
+                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G, \
+                T, pf, att_b0, w.h, w.hpart);                                                          \
+    } while (0)
+    if (table_dtype == 0) {
+        if (n_item == 4) NRK_ATT_H(float, 4); else if (n_item == 2) NRK_ATT_H(float, 2); else NRK_ATT_H(float, 1);
+    } else {
+        if (n_item == 4) NRK_ATT_H(uint16_t, 4); else if (n_item == 2) NRK_ATT_H(uint16_t, 2); else NRK_ATT_H(uint16_t, 1);
+    }
+#undef NRK_ATT_H
+    const int ncol_att = T * DIN_H;
+    const unsigned gs = (unsigned)n_seg;
+    col_stats_kernel<<<dim3(gs, (ncol_att + 3) / 4), 256, 0, s>>>(w.hpart, G, (int)nb_att, ncol_att,
+                                                                   batch, S, w.hstats);
+    const int64_t gb = (batch + 3) / 4;
+    const int go = (int)(batch < 8192 ? batch : 8192);
+    if (table_dtype == 0)
+        din_att_out_kernel<float><<<go, 256, 0, s>>>(
+            reinterpret_cast<const float*>(table), row_base, n_user, n_item, n_ctx, user_idx,
+            item_idx, hist_idx, ctx_idx, mask, batch, S, T, w.h, w.hstats, att_w1, att_b1, w.mlp_in);
+    else
+        din_att_out_kernel<uint16_t><<<go, 256, 0, s>>>(
+            reinterpret_cast<const uint16_t*>(table), row_base, n_user, n_item, n_ctx, user_idx,
+            item_idx, hist_idx, ctx_idx, mask, batch, S, T, w.h, w.hstats, att_w1, att_b1, w.mlp_in);
+    const int64_t nb_m = (batch + 63) / 64;
+    const int bps = n_seg == 1 ? (int)nb_m : (int)(S / 64);  // 64-row GEMM blocks per segment
+    din_gemm_kernel<false><<<dim3((unsigned)nb_m, (h1 + 63) / 64), 512, 0, s>>>(
+        w.mlp_in, nullptr, mlp_w0, mlp_b0, batch, S, h1, IN, w.z1, w.z1part);
+    col_stats_kernel<<<dim3(gs, (h1 + 3) / 4), 256, 0, s>>>(w.z1part, bps, (int)nb_m, h1, batch, S,
+                                                            w.z1stats);
+    din_gemm_kernel<true><<<dim3((unsigned)nb_m, (h2 + 63) / 64), 512, 0, s>>>(
+        w.z1, w.z1stats, mlp_w1, mlp_b1, batch, S, h2, h1, w.z2, w.z2part);
+    col_stats_kernel<<<dim3(gs, (h2 + 3) / 4), 256, 0, s>>>(w.z2part, bps, (int)nb_m, h2, batch, S,
+                                                            w.z2stats);
+    din_head_kernel<<<(unsigned)gb, 256, 0, s>>>(w.z2, w.z2stats, batch, S, h2, mlp_w2, mlp_b2,
+                                                 out_probs, out_logits);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
 }
 
 int nrk_din_forward(const void* table, int table_dtype, const int64_t* row_base, int n_user,
@@ -628,65 +744,15 @@ int nrk_din_forward(const void* table, int table_dtype, const int64_t* row_base,
                     int h2, const float* mlp_w2, const float* mlp_b2, float* out_probs,
                     float* out_logits, void* workspace, size_t workspace_bytes,
                     nrk_stream_t stream) {
-    clear_error();
-    NRK_REQUIRE(table_dtype == 0 || table_dtype == 1, "table_dtype must be 0 (f32) or 1 (bf16)");
-    NRK_REQUIRE(batch >= 2, "batch must be >= 2 (Dice uses the batch std; B = 1 is NaN in the reference)");
-    NRK_REQUIRE(seq_len >= 1 && seq_len <= 128, "seq_len must be in [1, 128]");
-    NRK_REQUIRE(n_user >= 1 && n_ctx >= 0 && n_item >= 1, "bad feature counts");
-    if (n_item != 4 && n_item != 2 && n_item != 1) NRK_UNSUPPORTED("n_item must be 1, 2 or 4");
-    NRK_REQUIRE(h1 >= 1 && h1 <= 1024 && h2 >= 1 && h2 <= 1024, "hidden sizes out of range");
-    NRK_REQUIRE(table && row_base && user_idx && item_idx && hist_idx && mask && prep && att_b0 &&
-                    att_w1 && att_b1 && mlp_w0 && mlp_b0 && mlp_w1 && mlp_b1 && mlp_w2 && mlp_b2 &&
-                    out_probs && workspace,
-                "null pointer");
-    NRK_REQUIRE(n_ctx == 0 || ctx_idx, "ctx_idx null");
-    const DinWs w = din_ws_layout(workspace, batch, seq_len, n_user, n_item, n_ctx, h1, h2);
-    NRK_REQUIRE(workspace_bytes >= w.bytes, "workspace too small");
-    hipStream_t s = as_stream(stream);
-    const int T = seq_len;
-    const int IN = (n_user + n_ctx + 2 * n_item) * DIN_E;
-    const int nb_att = (int)(batch < DIN_ATT_GRID ? batch : DIN_ATT_GRID);
-    const float* pf = reinterpret_cast<const float*>(prep);
-#define NRK_ATT_H(TT, NI)                                                                           \
-    do {                                                                                            \
-        if (T <= 64)                                                                                \
-            din_att_h_kernel<TT, NI, 1><<<nb_att, 256, 0, s>>>(                                     \
-                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, T, \
-                pf, att_b0, w.h, w.hpart);                                                          \
-        else                                                                                        \
-            din_att_h_kernel<TT, NI, 2><<<nb_att, 256, 0, s>>>(                                     \
-                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, T, \
-                pf, att_b0, w.h, w.hpart);                                                          \
-    } while (0)
-    if (table_dtype == 0) {
-        if (n_item == 4) NRK_ATT_H(float, 4); else if (n_item == 2) NRK_ATT_H(float, 2); else NRK_ATT_H(float, 1);
-    } else {
-        if (n_item == 4) NRK_ATT_H(uint16_t, 4); else if (n_item == 2) NRK_ATT_H(uint16_t, 2); else NRK_ATT_H(uint16_t, 1);
+    if (batch < 2) {
+        clear_error();
+        NRK_REQUIRE(batch >= 2, "batch must be >= 2 (Dice uses the batch std; B = 1 is NaN in the reference)");
     }
-#undef NRK_ATT_H
-    const int ncol_att = T * DIN_H;
-    col_stats_kernel<<<(ncol_att + 3) / 4, 256, 0, s>>>(w.hpart, nb_att, ncol_att, batch, w.hstats);
-    const int gb = (int)((batch + 3) / 4);
-    const int go = (int)(batch < 4096 ? batch : 4096);
-    if (table_dtype == 0)
-        din_att_out_kernel<float><<<go, 256, 0, s>>>(
-            reinterpret_cast<const float*>(table), row_base, n_user, n_item, n_ctx, user_idx,
-            item_idx, hist_idx, ctx_idx, mask, batch, T, w.h, w.hstats, att_w1, att_b1, w.mlp_in);
-    else
-        din_att_out_kernel<uint16_t><<<go, 256, 0, s>>>(
-            reinterpret_cast<const uint16_t*>(table), row_base, n_user, n_item, n_ctx, user_idx,
-            item_idx, hist_idx, ctx_idx, mask, batch, T, w.h, w.hstats, att_w1, att_b1, w.mlp_in);
-    const int nb_m = (int)((batch + 63) / 64);
-    din_gemm_kernel<false><<<dim3(nb_m, (h1 + 63) / 64), 512, 0, s>>>(
-        w.mlp_in, nullptr, mlp_w0, mlp_b0, batch, h1, IN, w.z1, w.z1part);
-    col_stats_kernel<<<(h1 + 3) / 4, 256, 0, s>>>(w.z1part, nb_m, h1, batch, w.z1stats);
-    din_gemm_kernel<true><<<dim3(nb_m, (h2 + 63) / 64), 512, 0, s>>>(
-        w.z1, w.z1stats, mlp_w1, mlp_b1, batch, h2, h1, w.z2, w.z2part);
-    col_stats_kernel<<<(h2 + 3) / 4, 256, 0, s>>>(w.z2part, nb_m, h2, batch, w.z2stats);
-    din_head_kernel<<<gb, 256, 0, s>>>(w.z2, w.z2stats, batch, h2, mlp_w2, mlp_b2, out_probs,
-                                       out_logits);
-    NRK_CHECK_LAUNCH();
-    return NRK_OK;
+    return nrk_din_forward_segments(table, table_dtype, row_base, n_user, n_item, n_ctx, user_idx,
+                                    item_idx, hist_idx, ctx_idx, mask, batch, batch, seq_len, prep,
+                                    att_b0, att_w1, att_b1, mlp_w0, mlp_b0, h1, mlp_w1, mlp_b1, h2,
+                                    mlp_w2, mlp_b2, out_probs, out_logits, workspace,
+                                    workspace_bytes, stream);
 }
 
 }  // extern "C"

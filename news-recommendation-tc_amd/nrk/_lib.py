@@ -45,6 +45,9 @@ SIGNATURES = {
     "nrk_din_workspace_bytes": (SZ, [I64, INT, INT, INT, INT, INT, INT]),
     "nrk_din_forward": (INT, [P, INT, P, INT, INT, INT, P, P, P, P, P, I64, INT, P, P, P, P,
                               P, P, INT, P, P, INT, P, P, P, P, P, SZ, P]),
+    "nrk_din_segments_workspace_bytes": (SZ, [I64, I64, INT, INT, INT, INT, INT, INT]),
+    "nrk_din_forward_segments": (INT, [P, INT, P, INT, INT, INT, P, P, P, P, P, I64, I64, INT, P, P,
+                                       P, P, P, P, INT, P, P, INT, P, P, P, P, P, SZ, P]),
 }
 
 _lib = None

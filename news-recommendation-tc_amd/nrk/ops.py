@@ -233,14 +233,29 @@ def din_validate(p: DinParams, user, item, hist, ctx):
             raise ValueError("history index out of its embedding table")
 
 
+def _din_seg(B, batch_size):
+    S = B if batch_size is None or batch_size >= B else int(batch_size)
+    if S < B and S % 64:
+        raise ValueError("batch_size must be a multiple of 64 when the samples span several batches")
+    if S == B and B < 2:
+        raise ValueError("batch must be >= 2 (Dice uses the batch std; B = 1 is NaN in the reference)")
+    return S
+
+
 def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspace=None,
-                out=None, validate=True):
-    """One DIN batch (B >= 2): int32 index tensors user [B,Fu], item [B,Fi],
+                out=None, validate=True, batch_size=None):
+    """DIN scores of B samples: int32 index tensors user [B,Fu], item [B,Fi],
     hist [B,T,Fi], ctx [B,Fc], mask [B,T] f32 -> probs [B] (+ logits).
+    ``batch_size=None``: the B samples are one Dice batch (B >= 2).
+    Otherwise they are scored as consecutive batches of ``batch_size`` (a
+    multiple of 64), each with its own Dice statistics -- DINRanker.predict's
+    loop (DIN.py:1245-1283) in one call; a trailing batch of one row is NaN
+    as in the reference.
     ``validate=False`` skips the host-side index range check (one device sync)
     for callers that validated the resident index tensors once up front."""
     _dev(user, item, hist, ctx, mask)
     B, T = mask.shape
+    S = _din_seg(B, batch_size)
     _need(user, torch.int32, (B, p.n_user), "user")
     _need(item, torch.int32, (B, p.n_item), "item")
     _need(hist, torch.int32, (B, T, p.n_item), "hist")
@@ -254,19 +269,24 @@ def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspa
     else:
         probs = torch.empty(B, dtype=torch.float32, device=mask.device)
     lg = torch.empty(B, dtype=torch.float32, device=mask.device) if logits else None
-    nb = _lib.lib().nrk_din_workspace_bytes(B, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
+    nb = _lib.lib().nrk_din_segments_workspace_bytes(B, S, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
     if workspace is None or workspace.numel() < nb:
         workspace = torch.empty(nb, dtype=torch.uint8, device=mask.device)
-    _lib.call("nrk_din_forward", _ptr(p.table), p.table_code, _ptr(p.row_base), p.n_user, p.n_item,
-              p.n_ctx, _ptr(user), _ptr(item), _ptr(hist), _ptr(ctx), _ptr(mask), B, T,
+    _lib.call("nrk_din_forward_segments", _ptr(p.table), p.table_code, _ptr(p.row_base), p.n_user,
+              p.n_item, p.n_ctx, _ptr(user), _ptr(item), _ptr(hist), _ptr(ctx), _ptr(mask), B, S, T,
               _ptr(p.prep), _ptr(p.att_b0), _ptr(p.att_w1), _ptr(p.att_b1), _ptr(p.mlp_w0),
               _ptr(p.mlp_b0), p.h1, _ptr(p.mlp_w1), _ptr(p.mlp_b1), p.h2, _ptr(p.mlp_w2),
               _ptr(p.mlp_b2), _ptr(probs), _ptr(lg), _ptr(workspace), workspace.numel(), _stream())
+    if S < B and B % S == 1:  # trailing batch of one row: std undefined -> NaN (reference)
+        probs[B - 1] = float("nan")
+        if lg is not None:
+            lg[B - 1] = float("nan")
     return (probs, lg) if logits else probs
 
 
-def din_workspace(p: DinParams, B, T, device):
-    nb = _lib.lib().nrk_din_workspace_bytes(B, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
+def din_workspace(p: DinParams, B, T, device, batch_size=None):
+    S = _din_seg(B, batch_size)
+    nb = _lib.lib().nrk_din_segments_workspace_bytes(B, S, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
     return torch.empty(nb, dtype=torch.uint8, device=device)
 
 

@@ -132,8 +132,18 @@ class DINScorer:
                                logits=logits)
 
     def predict(self, enc, batch_size):
-        """All rows in order, reference batching (DIN.py:1245-1283)."""
+        """All rows in order, reference batching (DIN.py:1245-1283).  With a
+        batch size that is a multiple of 64 every batch is scored in one
+        nrk_din_forward_segments call (each batch keeps its own Dice
+        statistics); otherwise one call per batch."""
         n = enc["mask"].shape[0]
+        if n >= 2 and (batch_size % 64 == 0 or n <= batch_size):
+            d = self.device
+            t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a)).to(d, dt).contiguous()  # noqa: E731
+            p = ops.din_forward(self.params, t(enc["user"], torch.int32), t(enc["item"], torch.int32),
+                                t(enc["hist"], torch.int32), t(enc["ctx"], torch.int32),
+                                t(enc["mask"], torch.float32), batch_size=batch_size)
+            return p.cpu().numpy()
         out = np.empty(n, np.float32)
         for s in range(0, n, batch_size):
             e = min(n, s + batch_size)

@@ -163,6 +163,48 @@ def test_din_config3_batch():
     np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
 
 
+@pytest.mark.parametrize("N,S,table_dtype", [(1000, 128, "bf16"), (257, 64, "fp32"), (2 * 4096 + 77, 4096, "bf16")])
+def test_din_segments_vs_per_batch_oracle(N, S, table_dtype):
+    """nrk_din_forward_segments: N samples as consecutive Dice batches of S in
+    one call == the oracle run batch by batch (DINRanker.predict's loop);
+    a trailing one-row batch is NaN."""
+    from nrk import ops
+
+    rng = np.random.default_rng(N + S)
+    vu, vi, vc = [50, 300, 7, 2000, 90], [60, 900, 5000, 70], [12] * 16
+    sd, feats = synth_model(rng, vu, vi, vc)
+    b = synth_batch(rng, N, 50, vu, vi, vc)
+    p = ops.DinParams(sd, *feats, table_dtype=table_dtype, device="cuda")
+    d = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to("cuda", dt)  # noqa: E731
+    probs, lg = ops.din_forward(p, d(b["user"], torch.int32), d(b["item"], torch.int32),
+                                d(b["hist"], torch.int32), d(b["ctx"], torch.int32),
+                                d(b["mask"], torch.float32), logits=True, batch_size=S)
+    probs, lg = probs.cpu().numpy(), lg.cpu().numpy()
+    for s in range(0, N, S):
+        e = min(N, s + S)
+        if e - s == 1:
+            assert np.isnan(probs[s]) and np.isnan(lg[s])
+            continue
+        po, lo, _ = oracle.din_forward(sd, *(b[k][s:e] for k in ("user", "item", "hist", "ctx", "mask")),
+                                       feats, round_bf16=table_dtype == "bf16")
+        np.testing.assert_allclose(probs[s:e], po, atol=TOL, rtol=0)
+        np.testing.assert_allclose(lg[s:e], lo, atol=TOL, rtol=TOL)
+
+
+def test_din_segments_errors():
+    from nrk import ops
+
+    rng = np.random.default_rng(2)
+    vu, vi, vc = [50], [60, 900, 5000, 70], [12]
+    sd, feats = synth_model(rng, vu, vi, vc)
+    b = synth_batch(rng, 300, 10, vu, vi, vc)
+    p = ops.DinParams(sd, *feats, device="cuda")
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in b.items()}
+    with pytest.raises(ValueError):  # several batches need a multiple-of-64 batch size
+        ops.din_forward(p, t["user"].int(), t["item"].int(), t["hist"].int(), t["ctx"].int(),
+                        t["mask"].float(), batch_size=100)
+
+
 def test_din_ranker_predict_batches(golden):
     """DINRanker.predict batching: short last batch scored with its own
     statistics; a trailing batch of one row is NaN as in the reference."""
@@ -179,3 +221,11 @@ def test_din_ranker_predict_batches(golden):
         np.testing.assert_allclose(out[s:e], po, atol=TOL, rtol=0)
     out2 = sc.predict({k: v[:201] for k, v in b.items()}, 100)
     assert np.isnan(out2[200]) and not np.isnan(out2[:200]).any()
+    # multiple-of-64 batch size: the one-call segmented path
+    out3 = sc.predict(b, 128)
+    for s in range(0, 512, 128):
+        po, _, _ = oracle.din_forward(sd, *(b[k][s:s + 128] for k in ("user", "item", "hist", "ctx", "mask")),
+                                      feats)
+        np.testing.assert_allclose(out3[s:s + 128], po, atol=TOL, rtol=0)
+    out4 = sc.predict({k: v[:129] for k, v in b.items()}, 128)
+    assert np.isnan(out4[128]) and not np.isnan(out4[:128]).any()
