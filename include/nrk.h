@@ -109,6 +109,19 @@ int nrk_topk_merge(const double* in_exact, const int32_t* in_rows, int n_lists,
                    int32_t* out_rows, double* out_exact, nrk_stream_t stream);
 
 /* ---------------------------------------------------------------------- */
+/* Embedding similarity (the second Faiss site)                           */
+/* ---------------------------------------------------------------------- */
+
+/* out[r] = x[r] / ||x[r]||, bit-identical to numpy's float32
+ *   item_emb_np / np.linalg.norm(item_emb_np, axis=1, keepdims=True)
+ * (src/similarity/embedding.py:41; pairwise float32 sum of squares, correctly
+ * rounded sqrt and division).  norms (nullable) receives ||x[r]||.  The
+ * self-search that follows (embedding.py:46-50) is nrk_ip_topk with
+ * users == items == out.  dim <= 256; out may not alias x. */
+int nrk_row_normalize(const float* x, int64_t n, int dim, float* out, float* norms,
+                      nrk_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
 /* ItemCF co-occurrence similarity                                        */
 /* ---------------------------------------------------------------------- */
 

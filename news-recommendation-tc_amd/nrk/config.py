@@ -14,6 +14,7 @@ class RecallConfig:
     itemcf_recall_num: int = 20
     itemcf_hot_topk: int = 20
     embedding_topk: int = 20
+    embedding_dim: int = 64
     youtubednn_seq_max_len: int = 30
     youtubednn_embedding_dim: int = 16
     youtubednn_hidden_units: List[int] = field(default_factory=lambda: [64, 16])

@@ -164,6 +164,19 @@ def ip_topk_finish(users, catalog: Catalog, k: int, workspace, out_scores, out_r
               workspace.numel(), _stream())
 
 
+def row_normalize(x, norms=False):
+    """x / ||x|| per row, bit-identical to numpy float32 (similarity/embedding.py:41)."""
+    _dev(x)
+    _need(x, torch.float32, name="x")
+    if x.dim() != 2 or not (1 <= x.shape[1] <= 256):
+        raise ValueError("x must be [n, d] with 1 <= d <= 256")
+    n, d = x.shape
+    out = torch.empty_like(x)
+    nr = torch.empty(n, dtype=torch.float32, device=x.device) if norms else None
+    _lib.call("nrk_row_normalize", _ptr(x), n, d, _ptr(out), _ptr(nr), _stream())
+    return (out, nr) if norms else out
+
+
 # -------------------------------------------------------------------- DIN --
 class DinParams:
     """Device-resident DIN weights in kernel layout (DINModel state_dict,

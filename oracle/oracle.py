@@ -9,6 +9,8 @@ Each function restates the reference (file:line cited) in numpy / C:
 
 * ``ip_topk``            -- faiss.IndexFlatIP contract, youtubednn_recaller.py:493-494, :520
 * ``youtubednn_recall``  -- YoutubeDNNRecaller.recall, youtubednn_recaller.py:497-535
+* ``embedding_similarity`` / ``embedding_sim_dict``
+                         -- EmbeddingSimilarity.calculate, similarity/embedding.py:35-62
 * ``tower_user``         -- YoutubeDNN.forward + _extract_embeddings re-norm, :129-178, :467-470
 * ``tower_item``         -- get_item_embedding + re-norm, :184-188, :485-489
 * ``itemcf_sim``         -- ItemCFSimilarity.calculate, item_cf.py:17-89
@@ -99,6 +101,28 @@ def youtubednn_recall(scores, rows, user_rawid_2_index, item_index_2_rawid, user
             if len(res) >= topk:
                 break
         out[u] = res
+    return out
+
+
+def embedding_similarity(emb, topk, nthreads=0):
+    """EmbeddingSimilarity.calculate's arithmetic (similarity/embedding.py:35-50):
+    numpy float32 row normalisation (:41) then the IndexFlatIP self-search for
+    topk+1 neighbours (:46-50).  Returns (normalised rows, scores, rows)."""
+    x = np.ascontiguousarray(emb, dtype=np.float32)
+    xn = np.ascontiguousarray(x / np.linalg.norm(x, axis=1, keepdims=True))
+    s, r = ip_topk(xn, xn, topk + 1, nthreads=nthreads)
+    return xn, s, r
+
+
+def embedding_sim_dict(ids, scores, rows):
+    """The dict build of embedding.py:52-62: row -> raw id, column 0 dropped
+    (whatever row it holds), later duplicate keys overwrite."""
+    i2r = {n: int(x) for n, x in enumerate(ids)}
+    out = {}
+    for t in range(scores.shape[0]):
+        d = out.setdefault(i2r[t], {})
+        for r, v in zip(rows[t, 1:].tolist(), scores[t, 1:].tolist()):
+            d[i2r[r]] = float(v)
     return out
 
 

@@ -323,6 +323,41 @@ def gen_topk(tmp):
 
 
 # --------------------------------------------------------------------------
+# EmbeddingSimilarity (similarity/embedding.py:15-67), the 2nd Faiss site
+# --------------------------------------------------------------------------
+def gen_embsim(tmp):
+    import pandas as pd
+    from src.utils.config import RecallConfig
+    from src.similarity.embedding import EmbeddingSimilarity
+
+    rng = np.random.default_rng(11)
+    n_items, d = 1500, 250  # Tianchi articles_emb is 250-d
+    emb = rng.standard_normal((n_items, d)).astype(np.float32)
+    emb *= rng.uniform(0.2, 5.0, (n_items, 1)).astype(np.float32)
+    # exact duplicates (up to scale): "self" is not always column 0 (lower row wins)
+    src = rng.integers(0, n_items, 40)
+    emb[n_items - 40:] = emb[src] * np.float32(2.0)
+    ids = (rng.permutation(n_items).astype(np.int64) * 3 + 5)
+    df = pd.DataFrame(emb, columns=[f"emb_{n}" for n in range(d)])
+    df.insert(0, "article_id", ids)
+    df.index = rng.permutation(n_items) + 10  # reset_index(drop=True) discards this
+    cfg = RecallConfig(_project_root=tmp)
+    sim = EmbeddingSimilarity(cfg).calculate(df)
+    si, sj, sv = [], [], []
+    for i, dd in sim.items():
+        for j, v in dd.items():
+            si.append(i)
+            sj.append(j)
+            sv.append(v)
+    np.savez_compressed(
+        os.path.join(HERE, "embsim_small.npz"),
+        ids=ids, emb=emb, topk=np.int64(cfg.embedding_topk),
+        sim_i=np.array(si, np.int64), sim_j=np.array(sj, np.int64), sim_v=np.array(sv, np.float64),
+    )
+    print(f"embsim_small: {n_items} items x {d}, {len(si)} entries")
+
+
+# --------------------------------------------------------------------------
 # DIN (DIN.py:29-286, 289-520)
 # --------------------------------------------------------------------------
 USER_FEATS = ["user_click_count", "user_avg_time_gap", "device_group", "avg_click_time", "avg_word_count"]

@@ -123,6 +123,26 @@ def test_ip_topk_padding(golden):
     assert np.array_equal(s, g["small_D"])
 
 
+def _embsim_golden_dict(g):
+    out = {}
+    for i, j, v in zip(g["sim_i"].tolist(), g["sim_j"].tolist(), g["sim_v"].tolist()):
+        out.setdefault(i, {})[j] = v
+    return out
+
+
+def test_embedding_similarity_matches_reference(golden):
+    g = golden("embsim_small")
+    _, s, r = oracle.embedding_similarity(g["emb"], int(g["topk"]))
+    got = oracle.embedding_sim_dict(g["ids"], s, r)
+    ref = _embsim_golden_dict(g)
+    assert list(got) == list(ref)
+    for i in ref:
+        assert list(got[i].items()) == list(ref[i].items())
+    # the duplicated rows make "self" land off column 0 for some items
+    n = len(g["ids"])
+    assert (r[:, 0] != np.arange(n)).any()
+
+
 # ------------------------------------------------------------------- DIN --
 def _din_sd(g):
     return {k[4:]: g[k] for k in g.files if k.startswith("sd::")}
