@@ -391,6 +391,329 @@ __global__ __launch_bounds__(256) void din_att_out_kernel(
     }
 }
 
+// ----------------------------------------------------- 3'. att wh (fast) --
+// Fast path (T <= 64, h1 <= 256): only the weighted history sum wh [B, ID]
+// is materialised -- GEMM1 (din_mlp1_kernel) gathers the user / context /
+// candidate embeddings itself.  One wave per sample: lane t < T reduces its
+// Dice row of h (w_t = (sum_j w1_j Dice(h_tj) + b1) * mask_t, DIN.py:117-124)
+// and holds the table rows of history slot t; lane l then forms wh[o] for
+// o = l, l + 64 (< ID) over t ascending (:276), w_t and the rows broadcast by
+// readlane.  Slots after the last nonzero weight add exactly +0 and are
+// skipped.  Dice here uses the hardware exp / reciprocal (~1 ulp each; the
+// parity bar is 1e-5).  Each wave owns a contiguous run of samples and
+// publishes max |wh| per Dice batch (atomicMax on the float bits) for
+// GEMM1's fp16 scale.
+__device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
+    const float p = __builtin_amdgcn_rcpf(1.0f + __expf((mean - x) * inv));
+    return p * x + ((1.0f - p) * 0.01f) * x;
+}
+
+template <typename TT, int NI>
+__global__ __launch_bounds__(256) void din_wh_kernel(
+    const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
+    const int32_t* __restrict__ hist_idx, const float* __restrict__ mask, int64_t B, int64_t S,
+    int T, int64_t per_wave, const float* __restrict__ h, const float2* __restrict__ hstats_all,
+    const float* __restrict__ att_w1, const float* __restrict__ att_b1, float* __restrict__ wh,
+    unsigned int* __restrict__ segmax) {
+    constexpr int ID = NI * DIN_E;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t b0 = wave * per_wave;
+    const int64_t b1e = b0 + per_wave < B ? b0 + per_wave : B;
+    const float ab1 = att_b1[0];
+    int64_t cur = -1;
+    float mx = 0.0f;
+    auto flush = [&]() {
+        float m = mx;
+#pragma unroll
+        for (int k = 32; k > 0; k >>= 1) m = fmaxf(m, __shfl_xor(m, k, WAVE));
+        if (lane == 0 && cur >= 0) atomicMax(segmax + cur, __float_as_uint(m));
+    };
+    for (int64_t b = b0; b < b1e; ++b) {
+        const int64_t seg = b / S;
+        if (seg != cur) {
+            flush();
+            cur = seg;
+            mx = 0.0f;
+        }
+        float w = 0.0f;
+        int32_t rr[NI];
+#pragma unroll
+        for (int f = 0; f < NI; ++f) rr[f] = 0;
+        if (lane < T) {
+            const float4* hr = reinterpret_cast<const float4*>(h + ((size_t)b * T + lane) * DIN_H);
+            const float4* st = reinterpret_cast<const float4*>(hstats_all + ((size_t)seg * T + lane) * DIN_H);
+            float s = 0.0f;
+#pragma unroll
+            for (int c = 0; c < DIN_H / 4; ++c) {
+                const float4 x = hr[c];
+                const float4 s0 = st[2 * c], s1 = st[2 * c + 1];
+                const float xs[4] = {x.x, x.y, x.z, x.w};
+                const float ms[4] = {s0.x, s0.z, s1.x, s1.z};
+                const float sd[4] = {s0.y, s0.w, s1.y, s1.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    s += att_w1[4 * c + e] * dice_fast(xs[e], ms[e], __builtin_amdgcn_rcpf(sd[e] + 1e-8f));
+            }
+            w = (s + ab1) * mask[b * T + lane];
+#pragma unroll
+            for (int f = 0; f < NI; ++f)
+                rr[f] = (int32_t)(row_base[n_user + f] + hist_idx[((size_t)b * T + lane) * NI + f]);
+        }
+        const uint64_t nz = __builtin_amdgcn_ballot_w64(w != 0.0f);
+        const int te = nz ? 64 - __builtin_clzll(nz) : 0;
+        const int e = lane & 31, fo = lane >> 5;  // o1 = lane -> feature fo, o2 = lane + 64 -> 2 + fo
+        float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll 4
+        for (int t = 0; t < te; ++t) {
+            const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
+            int32_t r[NI];
+#pragma unroll
+            for (int f = 0; f < NI; ++f) r[f] = __builtin_amdgcn_readlane(rr[f], t);
+            if constexpr (NI == 1) {
+                if (lane < 32) s1 += wt * tload(table + (int64_t)r[0] * DIN_E + e);
+            } else {
+                const int32_t ra = fo ? r[1] : r[0];
+                s1 += wt * tload(table + (int64_t)ra * DIN_E + e);
+                if constexpr (NI == 4) {
+                    const int32_t rb = fo ? r[3] : r[2];
+                    s2 += wt * tload(table + (int64_t)rb * DIN_E + e);
+                }
+            }
+        }
+        float* o = wh + (size_t)b * ID;
+        if (lane < ID) o[lane] = s1;
+        if (lane + 64 < ID) o[lane + 64] = s2;
+        mx = fmaxf(mx, fmaxf(lane < ID ? fabsf(s1) : 0.0f, lane + 64 < ID ? fabsf(s2) : 0.0f));
+    }
+    flush();
+}
+
+// ----------------------------------------------------- 4'. mlp1 (fast) --
+// z1 = [user | ctx | cand | wh] W0^T + b0 (DIN.py:279-282, Linear(IN -> h1))
+// without materialising the MLP input: every 32-wide feature is one k-step
+// of v_mfma_f32_16x16x32_f16, its A fragment gathered straight from the
+// embedding table (or read from wh).  Exact-f32-class split product, the
+// din_att_h scheme:
+//   * W0 = W_hi + W_lo (fp16 at scale s_w, packed per call in fragment order
+//     by din_w1_pack_kernel);
+//   * bf16 table rows are exact in fp16 at scale s_k -> 2 MFMAs per fragment;
+//     fp32 rows and wh (scale s_h, per Dice batch) are split too -> 3.
+// The embedding k-steps accumulate at scale s_k s_w; the accumulator is then
+// rescaled exactly (powers of two) to s_h s_w for the wh k-steps.
+// Workgroup = 4 waves x 32 rows (two 16-row A tiles, all NT column tiles per
+// wave) = 128 rows.  The W0 slice of k-step s+1 is loaded into registers
+// during step s and stored to the other LDS buffer after it (one barrier per
+// step); the A rows of step s+1 and the indices of step s+2 are in flight
+// during step s.  Per 64-row half: fp64 column sums for the next Dice.
+constexpr int MLP1_ROWS = 128;
+
+template <int NT>
+__global__ void din_w1_pack_kernel(const float* __restrict__ W, int N, int K,
+                                   const unsigned int* __restrict__ wmax, din_half8* __restrict__ out) {
+    // out[s][j][v][lane] = 8 halves of (W * s_w) (v = 0: hi, 1: lo) for column
+    // n = 16 j + (lane & 15), k = 32 s + 8 (lane >> 4) + [0, 8)
+    const float s_w = pow2_scale(__uint_as_float(*wmax));
+    const int KS = K / DIN_E;
+    const int64_t total = (int64_t)KS * NT * 64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(i % 64), j = (int)((i / 64) % NT), s = (int)(i / (64 * NT));
+        const int n = 16 * j + (lane & 15), k = DIN_E * s + 8 * (lane >> 4);
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = n < N ? W[(size_t)n * K + k + e] : 0.0f;
+        din_half8 hi, lo;
+        split8(x, s_w, hi, lo);
+        out[((int64_t)s * NT + j) * 128 + lane] = hi;
+        out[((int64_t)s * NT + j) * 128 + 64 + lane] = lo;
+    }
+}
+
+// W0 slice staging: every thread moves CPT 16-B chunks (clamped, so the
+// loads are unconditional; the stores past the slice are skipped)
+typedef uint32_t din_u4 __attribute__((ext_vector_type(4)));  // native vector: promotable to VGPRs
+
+template <int CPT, int CH>
+__device__ __forceinline__ void stage_load(din_u4 (&stg)[CPT], const din_u4* __restrict__ src, int tid) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) stg[i] = src[min(tid + 256 * i, CH - 1)];
+}
+template <int CPT, int CH>
+__device__ __forceinline__ void stage_store(const din_u4 (&stg)[CPT], din_u4* dst, int tid) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i)
+        if (tid + 256 * i < CH) dst[tid + 256 * i] = stg[i];
+}
+
+template <typename TT, int NT>
+__global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
+    const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user, int n_item,
+    int n_ctx, const int32_t* __restrict__ user_idx, const int32_t* __restrict__ item_idx,
+    const int32_t* __restrict__ ctx_idx, const float* __restrict__ wh,
+    const unsigned int* __restrict__ wh_segmax, const float* __restrict__ prep,
+    const unsigned int* __restrict__ w1max, const din_u4* __restrict__ w1pack,
+    const float* __restrict__ bias, int64_t M, int64_t S, int N, float* __restrict__ C,
+    double* __restrict__ partial) {
+    constexpr bool F32 = sizeof(TT) == 4;
+    constexpr int CH = NT * 128;               // 16-B chunks per k-step slice
+    constexpr int CPT = (CH + 255) / 256;      // chunks per thread
+    __shared__ __attribute__((aligned(16))) din_u4 wr[2][CH];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4;
+    const int ID = n_item * DIN_E;
+    const int KE = n_user + n_ctx + n_item;  // embedding k-steps
+    const int KS = KE + n_item;              // + the wh k-steps
+    const int64_t m0 = (int64_t)blockIdx.x * MLP1_ROWS + wv * 32;
+    int64_t mrow[2];
+    bool mok[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        mrow[a] = m0 + 16 * a + (lane & 15);
+        mok[a] = mrow[a] < M;
+    }
+    const int64_t seg = (m0 < M ? m0 : M - 1) / S;  // a wave's 32 rows lie in one Dice batch
+    const float s_k = reinterpret_cast<const DinScales*>(prep + 3 * DIN_H * ID)->s_k;
+    const float s_w = pow2_scale(__uint_as_float(*w1max));
+    const float s_h = pow2_scale(__uint_as_float(wh_segmax[seg]));
+
+    auto idx_load = [&](int s, int a) -> int32_t {
+        if (!mok[a] || s >= KE) return 0;
+        const int64_t m = mrow[a];
+        if (s < n_user) return user_idx[m * n_user + s];
+        if (s < n_user + n_ctx) return ctx_idx[m * n_ctx + (s - n_user)];
+        return item_idx[m * n_item + (s - n_user - n_ctx)];
+    };
+    auto data_load = [&](int s, int a, int32_t idx, uint32_t (&raw)[8]) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) raw[e] = 0u;
+        if (!mok[a]) return;
+        if (s >= KE) {
+            const uint4* p = reinterpret_cast<const uint4*>(wh + mrow[a] * ID + (s - KE) * DIN_E + 8 * q);
+            const uint4 x = p[0], y = p[1];
+            raw[0] = x.x; raw[1] = x.y; raw[2] = x.z; raw[3] = x.w;
+            raw[4] = y.x; raw[5] = y.y; raw[6] = y.z; raw[7] = y.w;
+            return;
+        }
+        const int64_t base = s < n_user ? row_base[s]
+                             : s < n_user + n_ctx ? row_base[n_user + n_item + (s - n_user)]
+                                                  : row_base[n_user + (s - n_user - n_ctx)];
+        const uint4* p = reinterpret_cast<const uint4*>(table + (base + idx) * DIN_E + 8 * q);
+        const uint4 x = p[0];
+        raw[0] = x.x; raw[1] = x.y; raw[2] = x.z; raw[3] = x.w;
+        if (F32) {
+            const uint4 y = p[1];
+            raw[4] = y.x; raw[5] = y.y; raw[6] = y.z; raw[7] = y.w;
+        }
+    };
+    din_u4 stg[CPT];
+    din_f4 acc[2][NT];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[a][j] = din_f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    uint32_t raw[2][8], nraw[2][8];
+    int32_t idx1[2], idx2[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        idx1[a] = idx_load(0, a);
+        data_load(0, a, idx1[a], raw[a]);
+        idx1[a] = idx_load(1, a);
+        idx2[a] = idx_load(2, a);
+    }
+    stage_load<CPT, CH>(stg, w1pack, tid);
+    stage_store<CPT, CH>(stg, wr[0], tid);
+    __syncthreads();
+    for (int s = 0; s < KS; ++s) {
+        if (s + 1 < KS) stage_load<CPT, CH>(stg, w1pack + (size_t)(s + 1) * CH, tid);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            if (s + 1 < KS) data_load(s + 1, a, idx1[a], nraw[a]);
+            idx1[a] = idx2[a];
+            idx2[a] = s + 3 < KS ? idx_load(s + 3, a) : 0;
+        }
+        if (s == KE) {
+            const float r = s_h / s_k;  // exact: both are powers of two
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[a][j] *= r;
+        }
+        const bool split = F32 || s >= KE;
+        const float sc = s >= KE ? s_h : s_k;
+        din_half8 ahi[2], alo[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            float v[8];
+            if (F32 || s >= KE) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(raw[a][e]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    v[2 * i] = __uint_as_float(raw[a][i] << 16);
+                    v[2 * i + 1] = __uint_as_float(raw[a][i] & 0xFFFF0000u);
+                }
+            }
+            split8(v, sc, ahi[a], alo[a]);
+        }
+        const din_half8* wb = reinterpret_cast<const din_half8*>(wr[s & 1]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const din_half8 bh = wb[(2 * j) * 64 + lane];
+            const din_half8 bl = wb[(2 * j + 1) * 64 + lane];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[a], bh, acc[a][j], 0, 0, 0);
+                acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[a], bl, acc[a][j], 0, 0, 0);
+                if (split) acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[a], bh, acc[a][j], 0, 0, 0);
+            }
+        }
+        if (s + 1 < KS) stage_store<CPT, CH>(stg, wr[(s + 1) & 1], tid);
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) raw[a][e] = nraw[a][e];
+    }
+    // epilogue: scale, bias, store, per-64-row-half fp64 column sums
+    const float inv = 1.0f / (s_h * s_w);
+    double2* cs = reinterpret_cast<double2*>(&wr[0][0]);  // [4 waves][NT * 16]
+    static_assert(sizeof(wr) >= 4 * NT * 16 * sizeof(double2), "LDS reuse");
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int n = 16 * j + (lane & 15);
+        const float bn = n < N ? bias[n] : 0.0f;
+        double su = 0.0, sq = 0.0;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t m = m0 + 16 * a + 4 * q + r;
+                const float v = acc[a][j][r] * inv + bn;
+                if (n < N && m < M) {
+                    C[m * N + n] = v;
+                    su += (double)v;
+                    sq += (double)v * (double)v;
+                }
+            }
+        su += __shfl_xor(su, 16, WAVE);
+        sq += __shfl_xor(sq, 16, WAVE);
+        su += __shfl_xor(su, 32, WAVE);
+        sq += __shfl_xor(sq, 32, WAVE);
+        if (lane < 16) cs[wv * NT * 16 + n] = make_double2(su, sq);
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * N; e += 256) {
+        const int hf = e / N, n = e % N;
+        const int64_t blk = (int64_t)blockIdx.x * 2 + hf;
+        if (blk * 64 < M) {
+            const double2 x = cs[(2 * hf) * NT * 16 + n], y = cs[(2 * hf + 1) * NT * 16 + n];
+            partial[((size_t)blk * N + n) * 2] = x.x + y.x;
+            partial[((size_t)blk * N + n) * 2 + 1] = x.y + y.y;
+        }
+    }
+}
+
 // ---------------------------------------------------------- 4/6. gemm --
 // C[M][N] = f(A)[M][K] W[N][K]^T + bias on the f32-input MFMA
 // (v_mfma_f32_32x32x2_f32, exact f32 fma chains), f = Dice with per-column
@@ -568,7 +891,10 @@ struct DinWs {
     float* h;
     double* hpart;
     float2* hstats;
-    float* mlp_in;
+    float* mlp_in;   // general path only
+    float* wh;       // fast path only: [N, ID]
+    unsigned int* whmax;  // fast path: per-segment max |wh| (float bits), then max |W0|
+    din_half8* w1pack;    // fast path: packed W0 fragments
     float* z1;
     double* z1part;
     float2* z1stats;
@@ -580,6 +906,13 @@ struct DinWs {
 
 static inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// fast path: wave-per-sample wh + gather-on-load split-fp16 GEMM1
+static inline bool din_fast(int T, int h1) { return T <= 64 && h1 <= 256; }
+static inline int din_mlp1_nt(int h1) {
+    const int nt = (h1 + 15) / 16;
+    return nt <= 4 ? 4 : nt <= 8 ? 8 : nt <= 13 ? 13 : 16;
+}
+
 // N samples in Dice batches (segments) of S
 static DinWs din_ws_layout(void* base, int64_t N, int64_t S, int T, int n_user, int n_item, int n_ctx,
                            int h1, int h2) {
@@ -590,11 +923,15 @@ static DinWs din_ws_layout(void* base, int64_t N, int64_t S, int T, int n_user, 
     const int64_t nb_att = n_seg * din_att_groups(N, S);
     const int64_t nb_m = (N + 63) / 64;
     const int IN = (n_user + n_ctx + 2 * n_item) * DIN_E;
+    const bool fast = din_fast(T, h1);
     auto take = [&](size_t bytes) { uint8_t* r = p + o; o += al(bytes); return r; };
     w.h = (float*)take((size_t)N * T * DIN_H * 4);
     w.hpart = (double*)take((size_t)nb_att * T * DIN_H * 16);
     w.hstats = (float2*)take((size_t)n_seg * T * DIN_H * 8);
-    w.mlp_in = (float*)take((size_t)N * IN * 4);
+    w.mlp_in = fast ? nullptr : (float*)take((size_t)N * IN * 4);
+    w.wh = fast ? (float*)take((size_t)N * n_item * DIN_E * 4) : nullptr;
+    w.whmax = fast ? (unsigned int*)take((size_t)(n_seg + 1) * 4) : nullptr;
+    w.w1pack = fast ? (din_half8*)take((size_t)(IN / DIN_E) * din_mlp1_nt(h1) * 2048) : nullptr;
     w.z1 = (float*)take((size_t)N * h1 * 4);
     w.z1part = (double*)take((size_t)nb_m * h1 * 16);
     w.z1stats = (float2*)take((size_t)n_seg * h1 * 8);
@@ -710,6 +1047,53 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     col_stats_kernel<<<dim3(gs, (ncol_att + 3) / 4), 256, 0, s>>>(w.hpart, G, (int)nb_att, ncol_att,
                                                                    batch, S, w.hstats);
     const int64_t gb = (batch + 3) / 4;
+    const int64_t nb_m = (batch + 63) / 64;
+    const int bps = n_seg == 1 ? (int)nb_m : (int)(S / 64);  // 64-row GEMM blocks per segment
+    if (din_fast(T, h1)) {
+        // max |W0| -> packed split-fp16 W0; per-segment max |wh| (zeroed here)
+        unsigned int* w1max = w.whmax + n_seg;
+        if (hipMemsetAsync(w.whmax, 0, (size_t)(n_seg + 1) * 4, s) != hipSuccess) {
+            set_error("nrk_din_forward: hipMemsetAsync failed");
+            return NRK_EHIP;
+        }
+        const int64_t nw = (int64_t)h1 * IN;
+        din_absmax_kernel<<<(int)std::min<int64_t>((nw + 255) / 256, 1024), 256, 0, s>>>(mlp_w0, 0, nw, w1max);
+        const int NT = din_mlp1_nt(h1);
+        const int64_t npk = (int64_t)(IN / DIN_E) * NT * 64;
+        const int gp = (int)std::min<int64_t>((npk + 255) / 256, 2048);
+#define NRK_PACK(NTV) din_w1_pack_kernel<NTV><<<gp, 256, 0, s>>>(mlp_w0, h1, IN, w1max, w.w1pack)
+        if (NT == 4) NRK_PACK(4); else if (NT == 8) NRK_PACK(8); else if (NT == 13) NRK_PACK(13); else NRK_PACK(16);
+#undef NRK_PACK
+        // wh: one wave per sample, contiguous runs of samples per wave
+        const int64_t waves = std::min<int64_t>(batch, 32768);
+        const int64_t per_wave = (batch + waves - 1) / waves;
+        const unsigned gw = (unsigned)((((batch + per_wave - 1) / per_wave) + 3) / 4);
+#define NRK_WH(TT, NI)                                                                                  \
+    din_wh_kernel<TT, NI><<<gw, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,      \
+                                             hist_idx, mask, batch, S, T, per_wave, w.h, w.hstats,    \
+                                             att_w1, att_b1, w.wh, w.whmax)
+        if (table_dtype == 0) {
+            if (n_item == 4) NRK_WH(float, 4); else if (n_item == 2) NRK_WH(float, 2); else NRK_WH(float, 1);
+        } else {
+            if (n_item == 4) NRK_WH(uint16_t, 4); else if (n_item == 2) NRK_WH(uint16_t, 2); else NRK_WH(uint16_t, 1);
+        }
+#undef NRK_WH
+        const unsigned gm = (unsigned)((batch + MLP1_ROWS - 1) / MLP1_ROWS);
+#define NRK_MLP1(TT, NTV)                                                                                 \
+    din_mlp1_kernel<TT, NTV><<<gm, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,     \
+                                                n_item, n_ctx, user_idx, item_idx, ctx_idx, w.wh, w.whmax, \
+                                                pf, w1max,                                                 \
+                                                reinterpret_cast<const din_u4*>(w.w1pack), mlp_b0, batch,   \
+                                                S, h1, w.z1, w.z1part)
+        if (table_dtype == 0) {
+            if (NT == 4) NRK_MLP1(float, 4); else if (NT == 8) NRK_MLP1(float, 8);
+            else if (NT == 13) NRK_MLP1(float, 13); else NRK_MLP1(float, 16);
+        } else {
+            if (NT == 4) NRK_MLP1(uint16_t, 4); else if (NT == 8) NRK_MLP1(uint16_t, 8);
+            else if (NT == 13) NRK_MLP1(uint16_t, 13); else NRK_MLP1(uint16_t, 16);
+        }
+#undef NRK_MLP1
+    } else {
     const int go = (int)(batch < 8192 ? batch : 8192);
     if (table_dtype == 0)
         din_att_out_kernel<float><<<go, 256, 0, s>>>(
@@ -719,10 +1103,9 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         din_att_out_kernel<uint16_t><<<go, 256, 0, s>>>(
             reinterpret_cast<const uint16_t*>(table), row_base, n_user, n_item, n_ctx, user_idx,
             item_idx, hist_idx, ctx_idx, mask, batch, S, T, w.h, w.hstats, att_w1, att_b1, w.mlp_in);
-    const int64_t nb_m = (batch + 63) / 64;
-    const int bps = n_seg == 1 ? (int)nb_m : (int)(S / 64);  // 64-row GEMM blocks per segment
     din_gemm_kernel<false><<<dim3((unsigned)nb_m, (h1 + 63) / 64), 512, 0, s>>>(
         w.mlp_in, nullptr, mlp_w0, mlp_b0, batch, S, h1, IN, w.z1, w.z1part);
+    }
     col_stats_kernel<<<dim3(gs, (h1 + 3) / 4), 256, 0, s>>>(w.z1part, bps, (int)nb_m, h1, batch, S,
                                                             w.z1stats);
     din_gemm_kernel<true><<<dim3((unsigned)nb_m, (h2 + 63) / 64), 512, 0, s>>>(
