@@ -97,6 +97,16 @@ __device__ __forceinline__ void split8(const float (&x)[8], float s, din_half8& 
     }
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic
+// (lgkmcnt) but not for its outstanding global loads, which __syncthreads()
+// (a workgroup release fence: vmcnt(0) on gfx9) would drain -- prefetched
+// gathers stay in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // Segments: the N samples are scored as consecutive Dice batches of S
 // (DINRanker.predict's DataLoader batches, DIN.py:1245-1283); workgroup
 // blockIdx.x = seg * G + g strides over segment seg's samples, so partial row
@@ -152,29 +162,83 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
 
     const int64_t seg = blockIdx.x / G;
     const int64_t b_end = (seg + 1) * S < N ? (seg + 1) * S : N;
-    for (int64_t b = seg * S + blockIdx.x % G; b < b_end; b += G) {
-        // (1) this wave's k rows -> A fragments (issued first: latency overlaps (2)-(4))
-        din_half8 ahi[NTW][NI], alo[NTW][NI];
+    // software pipeline over this workgroup's samples b, b + G, ...: the
+    // history / candidate indices are loaded two samples ahead and the table
+    // rows (k rows, q) one sample ahead, so each sample's gathers overlap the
+    // previous sample's M_b build, MFMAs and epilogue
+    constexpr int RW = F32 ? 2 : 1;  // 16-B pieces per lane per k row
+    typedef uint32_t u4n __attribute__((ext_vector_type(4)));
+    auto idx_of = [&](int64_t bb, int32_t (&hi)[NTW][NI], int32_t& qi) {
 #pragma unroll
         for (int a = 0; a < NTW; ++a) {
             const int t = 16 * (wv + 4 * a) + (lane & 15);
 #pragma unroll
+            for (int s = 0; s < NI; ++s) hi[a][s] = (bb < b_end && t < T) ? hist_idx[(bb * T + t) * NI + s] : -1;
+        }
+        qi = (bb < b_end && tid < ID) ? item_idx[bb * NI + tid / DIN_E] : -1;
+    };
+    auto rows_of = [&](const int32_t (&hi)[NTW][NI], int32_t qi, u4n (&raw)[NTW][NI][RW], float& qv) {
+#pragma unroll
+        for (int a = 0; a < NTW; ++a)
+#pragma unroll
             for (int s = 0; s < NI; ++s) {
-                float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (t < T) {
-                    const int64_t r = row_base[n_user + s] + hist_idx[(b * T + t) * NI + s];
-                    load8<TT>(table + r * DIN_E + 8 * (lane >> 4), v);
+#pragma unroll
+                for (int w = 0; w < RW; ++w) raw[a][s][w] = u4n{0u, 0u, 0u, 0u};
+                if (hi[a][s] >= 0) {
+                    const u4n* p = reinterpret_cast<const u4n*>(
+                        table + (row_base[n_user + s] + hi[a][s]) * DIN_E + 8 * (lane >> 4));
+#pragma unroll
+                    for (int w = 0; w < RW; ++w) raw[a][s][w] = p[w];
+                }
+            }
+        qv = qi >= 0 ? tload(table + (row_base[n_user + tid / DIN_E] + qi) * DIN_E + tid % DIN_E) : 0.0f;
+    };
+    int32_t nidx[NTW][NI], nqi;
+    u4n raw[NTW][NI][RW];
+    float qv;
+    {
+        int32_t i0[NTW][NI], q0;
+        idx_of(seg * S + blockIdx.x % G, i0, q0);
+        rows_of(i0, q0, raw, qv);
+        idx_of(seg * S + blockIdx.x % G + G, nidx, nqi);
+    }
+    for (int64_t b = seg * S + blockIdx.x % G; b < b_end; b += G) {
+        u4n nraw[NTW][NI][RW];
+        float nqv;
+        rows_of(nidx, nqi, nraw, nqv);   // rows of sample b + G
+        idx_of(b + 2 * G, nidx, nqi);    // indices of sample b + 2G
+        // (1) this wave's k rows -> A fragments
+        din_half8 ahi[NTW][NI], alo[NTW][NI];
+#pragma unroll
+        for (int a = 0; a < NTW; ++a)
+#pragma unroll
+            for (int s = 0; s < NI; ++s) {
+                float v[8];
+                if (F32) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[e] = __uint_as_float(raw[a][s][0][e]);
+                        v[4 + e] = __uint_as_float(raw[a][s][RW - 1][e]);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        v[2 * i] = __uint_as_float(raw[a][s][0][i] << 16);
+                        v[2 * i + 1] = __uint_as_float(raw[a][s][0][i] & 0xFFFF0000u);
+                    }
                 }
                 split8(v, sc.s_k, ahi[a][s], alo[a][s]);
             }
-        }
         // (2) query embedding
-        if (tid < ID) {
-            const int s = tid / DIN_E, e = tid % DIN_E;
-            const int64_t r = row_base[n_user + s] + item_idx[b * NI + s];
-            qs[tid] = tload(table + r * DIN_E + e);
-        }
-        __syncthreads();
+        if (tid < ID) qs[tid] = qv;
+#pragma unroll
+        for (int a = 0; a < NTW; ++a)
+#pragma unroll
+            for (int s = 0; s < NI; ++s)
+#pragma unroll
+                for (int w = 0; w < RW; ++w) raw[a][s][w] = nraw[a][s][w];
+        qv = nqv;
+        lds_barrier();
         // (3) M_b fragments (hi / lo, scaled by s_m) and c_b
 #pragma unroll
         for (int m = 0; m < SPT; ++m) {
@@ -201,7 +265,7 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
             const int j = tid >> 2;
             if ((tid & 3) == 0 && j < DIN_H) cs[j] = c + att_b0[j];
         }
-        __syncthreads();
+        lds_barrier();
         // (4) MFMAs + epilogue
 #pragma unroll
         for (int a = 0; a < NTW; ++a) {
@@ -307,7 +371,8 @@ __global__ void din_scales_kernel(const float* __restrict__ prep_ap, int ID, con
 // segment has no std (NaN in the reference); the host marks its output.
 __global__ __launch_bounds__(256) void col_stats_kernel(const double* __restrict__ partial, int bps,
                                                         int nblk, int ncol, int64_t N, int64_t S,
-                                                        float2* __restrict__ stats) {
+                                                        float2* __restrict__ stats,
+                                                        float2* __restrict__ stats_inv = nullptr) {
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int64_t seg = blockIdx.x;
@@ -326,7 +391,9 @@ __global__ __launch_bounds__(256) void col_stats_kernel(const double* __restrict
         const double mean = s / (double)B;
         double var = B > 1 ? (ss - s * mean) / (double)(B - 1) : 0.0;
         if (var < 0.0) var = 0.0;
-        stats[seg * ncol + c] = make_float2((float)mean, (float)sqrt(var));
+        const float sd = (float)sqrt(var);
+        stats[seg * ncol + c] = make_float2((float)mean, sd);
+        if (stats_inv) stats_inv[seg * ncol + c] = make_float2((float)mean, 1.0f / (sd + 1e-8f));
     }
 }
 
@@ -400,7 +467,9 @@ __global__ __launch_bounds__(256) void din_att_out_kernel(
 // o = l, l + 64 (< ID) over t ascending (:276), w_t and the rows broadcast by
 // readlane.  Slots after the last nonzero weight add exactly +0 and are
 // skipped.  Dice here uses the hardware exp / reciprocal (~1 ulp each; the
-// parity bar is 1e-5).  Each wave owns a contiguous run of samples and
+// parity bar is 1e-5), with (mean, 1 / (std + 1e-8)) per column from
+// col_stats.  The next sample's h row, indices and mask are loaded while the
+// current one is reduced.  Each wave owns a contiguous run of samples and
 // publishes max |wh| per Dice batch (atomicMax on the float bits) for
 // GEMM1's fp16 scale.
 __device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
@@ -412,15 +481,17 @@ template <typename TT, int NI>
 __global__ __launch_bounds__(256) void din_wh_kernel(
     const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
     const int32_t* __restrict__ hist_idx, const float* __restrict__ mask, int64_t B, int64_t S,
-    int T, int64_t per_wave, const float* __restrict__ h, const float2* __restrict__ hstats_all,
+    int T, int64_t per_wave, const float* __restrict__ h, const float2* __restrict__ hinv_all,
     const float* __restrict__ att_w1, const float* __restrict__ att_b1, float* __restrict__ wh,
     unsigned int* __restrict__ segmax) {
     constexpr int ID = NI * DIN_E;
+    typedef float f4n __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t b0 = wave * per_wave;
     const int64_t b1e = b0 + per_wave < B ? b0 + per_wave : B;
     const float ab1 = att_b1[0];
+    const bool act = lane < T;
     int64_t cur = -1;
     float mx = 0.0f;
     auto flush = [&]() {
@@ -429,6 +500,27 @@ __global__ __launch_bounds__(256) void din_wh_kernel(
         for (int k = 32; k > 0; k >>= 1) m = fmaxf(m, __shfl_xor(m, k, WAVE));
         if (lane == 0 && cur >= 0) atomicMax(segmax + cur, __float_as_uint(m));
     };
+    // this lane's h row, history indices and mask of sample bb (prefetched one sample ahead)
+    auto fetch = [&](int64_t bb, f4n (&hv)[DIN_H / 4], int32_t (&ix)[NI], float& mk) {
+        if (act && bb < b1e) {
+            const f4n* hr = reinterpret_cast<const f4n*>(h + ((size_t)bb * T + lane) * DIN_H);
+#pragma unroll
+            for (int c = 0; c < DIN_H / 4; ++c) hv[c] = hr[c];
+#pragma unroll
+            for (int f = 0; f < NI; ++f) ix[f] = hist_idx[((size_t)bb * T + lane) * NI + f];
+            mk = mask[bb * T + lane];
+        } else {
+#pragma unroll
+            for (int c = 0; c < DIN_H / 4; ++c) hv[c] = f4n{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int f = 0; f < NI; ++f) ix[f] = 0;
+            mk = 0.0f;
+        }
+    };
+    f4n hv[DIN_H / 4];
+    int32_t ix[NI];
+    float mk;
+    fetch(b0, hv, ix, mk);
     for (int64_t b = b0; b < b1e; ++b) {
         const int64_t seg = b / S;
         if (seg != cur) {
@@ -436,55 +528,68 @@ __global__ __launch_bounds__(256) void din_wh_kernel(
             cur = seg;
             mx = 0.0f;
         }
+        f4n nhv[DIN_H / 4];
+        int32_t nix[NI];
+        float nmk;
+        fetch(b + 1, nhv, nix, nmk);
         float w = 0.0f;
         int32_t rr[NI];
 #pragma unroll
         for (int f = 0; f < NI; ++f) rr[f] = 0;
-        if (lane < T) {
-            const float4* hr = reinterpret_cast<const float4*>(h + ((size_t)b * T + lane) * DIN_H);
-            const float4* st = reinterpret_cast<const float4*>(hstats_all + ((size_t)seg * T + lane) * DIN_H);
-            float s = 0.0f;
+        if (act) {
+            const f4n* st = reinterpret_cast<const f4n*>(hinv_all + ((size_t)seg * T + lane) * DIN_H);
+            float sacc = 0.0f;
 #pragma unroll
             for (int c = 0; c < DIN_H / 4; ++c) {
-                const float4 x = hr[c];
-                const float4 s0 = st[2 * c], s1 = st[2 * c + 1];
-                const float xs[4] = {x.x, x.y, x.z, x.w};
+                const f4n s0 = st[2 * c], s1 = st[2 * c + 1];
                 const float ms[4] = {s0.x, s0.z, s1.x, s1.z};
-                const float sd[4] = {s0.y, s0.w, s1.y, s1.w};
+                const float iv[4] = {s0.y, s0.w, s1.y, s1.w};
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    s += att_w1[4 * c + e] * dice_fast(xs[e], ms[e], __builtin_amdgcn_rcpf(sd[e] + 1e-8f));
+                for (int e = 0; e < 4; ++e) sacc += att_w1[4 * c + e] * dice_fast(hv[c][e], ms[e], iv[e]);
             }
-            w = (s + ab1) * mask[b * T + lane];
+            w = (sacc + ab1) * mk;
 #pragma unroll
-            for (int f = 0; f < NI; ++f)
-                rr[f] = (int32_t)(row_base[n_user + f] + hist_idx[((size_t)b * T + lane) * NI + f]);
+            for (int f = 0; f < NI; ++f) rr[f] = (int32_t)(row_base[n_user + f] + ix[f]);
         }
         const uint64_t nz = __builtin_amdgcn_ballot_w64(w != 0.0f);
         const int te = nz ? 64 - __builtin_clzll(nz) : 0;
         const int e = lane & 31, fo = lane >> 5;  // o1 = lane -> feature fo, o2 = lane + 64 -> 2 + fo
         float s1 = 0.0f, s2 = 0.0f;
-#pragma unroll 4
-        for (int t = 0; t < te; ++t) {
-            const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
-            int32_t r[NI];
+        // 8 slots per round: all 16 gathers issued before the (in-order) adds;
+        // slots >= te carry weight +0 on row of lane 63's slot (adds exactly +0)
+        for (int t0 = 0; t0 < te; t0 += 8) {
+            float wt[8], v1[8], v2[8];
 #pragma unroll
-            for (int f = 0; f < NI; ++f) r[f] = __builtin_amdgcn_readlane(rr[f], t);
-            if constexpr (NI == 1) {
-                if (lane < 32) s1 += wt * tload(table + (int64_t)r[0] * DIN_E + e);
-            } else {
-                const int32_t ra = fo ? r[1] : r[0];
-                s1 += wt * tload(table + (int64_t)ra * DIN_E + e);
-                if constexpr (NI == 4) {
-                    const int32_t rb = fo ? r[3] : r[2];
-                    s2 += wt * tload(table + (int64_t)rb * DIN_E + e);
+            for (int u = 0; u < 8; ++u) {
+                const int t = (t0 + u) & 63;
+                wt[u] = t0 + u < te ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t)) : 0.0f;
+                int32_t r[NI];
+#pragma unroll
+                for (int f = 0; f < NI; ++f) r[f] = __builtin_amdgcn_readlane(rr[f], t);
+                if constexpr (NI == 1) {
+                    v1[u] = tload(table + (int64_t)r[0] * DIN_E + e);
+                    v2[u] = 0.0f;
+                } else {
+                    v1[u] = tload(table + (int64_t)(fo ? r[1] : r[0]) * DIN_E + e);
+                    v2[u] = NI == 4 ? tload(table + (int64_t)(fo ? r[NI - 1] : r[NI / 2]) * DIN_E + e) : 0.0f;
                 }
             }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s1 += wt[u] * v1[u];
+                s2 += wt[u] * v2[u];
+            }
         }
+        if (NI == 1 && lane >= 32) s1 = 0.0f;
         float* o = wh + (size_t)b * ID;
         if (lane < ID) o[lane] = s1;
         if (lane + 64 < ID) o[lane + 64] = s2;
         mx = fmaxf(mx, fmaxf(lane < ID ? fabsf(s1) : 0.0f, lane + 64 < ID ? fabsf(s2) : 0.0f));
+#pragma unroll
+        for (int c = 0; c < DIN_H / 4; ++c) hv[c] = nhv[c];
+#pragma unroll
+        for (int f = 0; f < NI; ++f) ix[f] = nix[f];
+        mk = nmk;
     }
     flush();
 }
@@ -622,7 +727,7 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
     }
     stage_load<CPT, CH>(stg, w1pack, tid);
     stage_store<CPT, CH>(stg, wr[0], tid);
-    __syncthreads();
+    lds_barrier();
     for (int s = 0; s < KS; ++s) {
         if (s + 1 < KS) stage_load<CPT, CH>(stg, w1pack + (size_t)(s + 1) * CH, tid);
 #pragma unroll
@@ -669,7 +774,7 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
             }
         }
         if (s + 1 < KS) stage_store<CPT, CH>(stg, wr[(s + 1) & 1], tid);
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -893,6 +998,7 @@ struct DinWs {
     float2* hstats;
     float* mlp_in;   // general path only
     float* wh;       // fast path only: [N, ID]
+    float2* hinv;    // fast path only: per-segment (mean, 1 / (std + 1e-8)) of h
     unsigned int* whmax;  // fast path: per-segment max |wh| (float bits), then max |W0|
     din_half8* w1pack;    // fast path: packed W0 fragments
     float* z1;
@@ -930,6 +1036,7 @@ static DinWs din_ws_layout(void* base, int64_t N, int64_t S, int T, int n_user, 
     w.hstats = (float2*)take((size_t)n_seg * T * DIN_H * 8);
     w.mlp_in = fast ? nullptr : (float*)take((size_t)N * IN * 4);
     w.wh = fast ? (float*)take((size_t)N * n_item * DIN_E * 4) : nullptr;
+    w.hinv = fast ? (float2*)take((size_t)n_seg * T * DIN_H * 8) : nullptr;
     w.whmax = fast ? (unsigned int*)take((size_t)(n_seg + 1) * 4) : nullptr;
     w.w1pack = fast ? (din_half8*)take((size_t)(IN / DIN_E) * din_mlp1_nt(h1) * 2048) : nullptr;
     w.z1 = (float*)take((size_t)N * h1 * 4);
@@ -1045,7 +1152,7 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     const int ncol_att = T * DIN_H;
     const unsigned gs = (unsigned)n_seg;
     col_stats_kernel<<<dim3(gs, (ncol_att + 3) / 4), 256, 0, s>>>(w.hpart, G, (int)nb_att, ncol_att,
-                                                                   batch, S, w.hstats);
+                                                                   batch, S, w.hstats, w.hinv);
     const int64_t gb = (batch + 3) / 4;
     const int64_t nb_m = (batch + 63) / 64;
     const int bps = n_seg == 1 ? (int)nb_m : (int)(S / 64);  // 64-row GEMM blocks per segment
@@ -1070,7 +1177,7 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         const unsigned gw = (unsigned)((((batch + per_wave - 1) / per_wave) + 3) / 4);
 #define NRK_WH(TT, NI)                                                                                  \
     din_wh_kernel<TT, NI><<<gw, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,      \
-                                             hist_idx, mask, batch, S, T, per_wave, w.h, w.hstats,    \
+                                             hist_idx, mask, batch, S, T, per_wave, w.h, w.hinv,      \
                                              att_w1, att_b1, w.wh, w.whmax)
         if (table_dtype == 0) {
             if (n_item == 4) NRK_WH(float, 4); else if (n_item == 2) NRK_WH(float, 2); else NRK_WH(float, 1);
