@@ -392,7 +392,7 @@ __global__ __launch_bounds__(256) void col_stats_kernel(const double* __restrict
         double var = B > 1 ? (ss - s * mean) / (double)(B - 1) : 0.0;
         if (var < 0.0) var = 0.0;
         const float sd = (float)sqrt(var);
-        stats[seg * ncol + c] = make_float2((float)mean, sd);
+        if (stats) stats[seg * ncol + c] = make_float2((float)mean, sd);
         if (stats_inv) stats_inv[seg * ncol + c] = make_float2((float)mean, 1.0f / (sd + 1e-8f));
     }
 }
@@ -617,21 +617,74 @@ template <int NT>
 __global__ void din_w1_pack_kernel(const float* __restrict__ W, int N, int K,
                                    const unsigned int* __restrict__ wmax, din_half8* __restrict__ out) {
     // out[s][j][v][lane] = 8 halves of (W * s_w) (v = 0: hi, 1: lo) for column
-    // n = 16 j + (lane & 15), k = 32 s + 8 (lane >> 4) + [0, 8)
+    // n = 16 j + (lane & 15), k = 32 s + 8 (lane >> 4) + [0, 8); zero past N, K
     const float s_w = pow2_scale(__uint_as_float(*wmax));
-    const int KS = K / DIN_E;
+    const int KS = (K + DIN_E - 1) / DIN_E;
     const int64_t total = (int64_t)KS * NT * 64;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const int lane = (int)(i % 64), j = (int)((i / 64) % NT), s = (int)(i / (64 * NT));
         const int n = 16 * j + (lane & 15), k = DIN_E * s + 8 * (lane >> 4);
         float x[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = n < N ? W[(size_t)n * K + k + e] : 0.0f;
+        for (int e = 0; e < 8; ++e) x[e] = (n < N && k + e < K) ? W[(size_t)n * K + k + e] : 0.0f;
         din_half8 hi, lo;
         split8(x, s_w, hi, lo);
         out[((int64_t)s * NT + j) * 128 + lane] = hi;
         out[((int64_t)s * NT + j) * 128 + 64 + lane] = lo;
     }
+}
+
+// Shared GEMM epilogue of din_mlp1 / din_mlp2 (one 128-row block, 4 waves x
+// 32 rows): C = acc * inv + bias, fp64 (sum, sumsq) per column over each
+// 64-row half -> partial rows blk0, blk0 + 1 (fixed order: waves 2h, 2h+1),
+// and optionally max |C| per Dice batch (atomicMax on the float bits).
+template <int NT>
+__device__ __forceinline__ void mlp_epilogue(const din_f4 (&acc)[2][NT], float inv, const float* __restrict__ bias,
+                                             int N, int64_t M, int64_t m0, int64_t blk0, int64_t S,
+                                             double2* cs, float* __restrict__ C, double* __restrict__ partial,
+                                             unsigned int* __restrict__ zmax) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4;
+    float mx = 0.0f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int n = 16 * j + (lane & 15);
+        const float bn = n < N ? bias[n] : 0.0f;
+        double su = 0.0, sq = 0.0;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t m = m0 + 16 * a + 4 * q + r;
+                const float v = acc[a][j][r] * inv + bn;
+                if (n < N && m < M) {
+                    C[m * N + n] = v;
+                    su += (double)v;
+                    sq += (double)v * (double)v;
+                    mx = fmaxf(mx, fabsf(v));
+                }
+            }
+        su += __shfl_xor(su, 16, WAVE);
+        sq += __shfl_xor(sq, 16, WAVE);
+        su += __shfl_xor(su, 32, WAVE);
+        sq += __shfl_xor(sq, 32, WAVE);
+        if (lane < 16) cs[wv * NT * 16 + n] = make_double2(su, sq);
+    }
+    if (zmax != nullptr && m0 < M) {
+#pragma unroll
+        for (int k = 32; k > 0; k >>= 1) mx = fmaxf(mx, __shfl_xor(mx, k, WAVE));
+        if (lane == 0) atomicMax(zmax + m0 / S, __float_as_uint(mx));
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * N; e += 256) {
+        const int hf = e / N, n = e % N;
+        const int64_t blk = blk0 + hf;
+        if (blk * 64 < M) {
+            const double2 x = cs[(2 * hf) * NT * 16 + n], y = cs[(2 * hf + 1) * NT * 16 + n];
+            partial[((size_t)blk * N + n) * 2] = x.x + y.x;
+            partial[((size_t)blk * N + n) * 2 + 1] = x.y + y.y;
+        }
+    }
+    __syncthreads();
 }
 
 // W0 slice staging: every thread moves CPT 16-B chunks (clamped, so the
@@ -658,7 +711,7 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
     const unsigned int* __restrict__ wh_segmax, const float* __restrict__ prep,
     const unsigned int* __restrict__ w1max, const din_u4* __restrict__ w1pack,
     const float* __restrict__ bias, int64_t M, int64_t S, int N, float* __restrict__ C,
-    double* __restrict__ partial) {
+    double* __restrict__ partial, unsigned int* __restrict__ zmax) {
     constexpr bool F32 = sizeof(TT) == 4;
     constexpr int CH = NT * 128;               // 16-B chunks per k-step slice
     constexpr int CPT = (CH + 255) / 256;      // chunks per thread
@@ -780,42 +833,109 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) raw[a][e] = nraw[a][e];
     }
-    // epilogue: scale, bias, store, per-64-row-half fp64 column sums
-    const float inv = 1.0f / (s_h * s_w);
+    // epilogue: scale, bias, store, per-64-row-half fp64 column sums, max |z1|
+    lds_barrier();  // (every wave is past its last read of wr)
     double2* cs = reinterpret_cast<double2*>(&wr[0][0]);  // [4 waves][NT * 16]
     static_assert(sizeof(wr) >= 4 * NT * 16 * sizeof(double2), "LDS reuse");
+    mlp_epilogue<NT>(acc, 1.0f / (s_h * s_w), bias, N, M, m0, (int64_t)blockIdx.x * 2, S, cs, C, partial, zmax);
+}
+
+// ----------------------------------------------------- 6'. mlp2 (fast) --
+// z2 = Dice(z1) W1^T + b1 (DIN.py:282-283) on the same split-fp16 MFMA: A =
+// Dice-on-load of z1 (batch (mean, 1 / (std + 1e-8)) per column) at scale s_a
+// from max |z1| of the Dice batch (|Dice(x)| <= |x|), split hi / lo -> 3 MFMAs
+// per fragment.  The whole packed W1 (KS x NT x 2 KB) stays in LDS; each
+// workgroup walks 128-row blocks (4 waves x 32 rows), loading the next
+// k-step's A while the current one runs.
+template <int NT>
+__global__ __launch_bounds__(256, 2) void din_mlp2_kernel(
+    const float* __restrict__ A, const float2* __restrict__ astats_all,
+    const unsigned int* __restrict__ amax, const unsigned int* __restrict__ wmax,
+    const din_u4* __restrict__ wpack, const float* __restrict__ bias, int64_t M, int64_t S, int K, int N,
+    float* __restrict__ C, double* __restrict__ partial) {
+    extern __shared__ __attribute__((aligned(16))) din_u4 wl[];
+    const int KS = (K + DIN_E - 1) / DIN_E;
+    const int CH = KS * NT * 128;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4;
+    for (int c = tid; c < CH; c += 256) wl[c] = wpack[c];
+    double2* cs = reinterpret_cast<double2*>(wl + CH);
+    __syncthreads();
+    const din_half8* wb = reinterpret_cast<const din_half8*>(wl);
+    const float s_w = pow2_scale(__uint_as_float(*wmax));
+    const int64_t nrb = (M + MLP1_ROWS - 1) / MLP1_ROWS;
+    typedef float f4n __attribute__((ext_vector_type(4)));
+    for (int64_t rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+        const int64_t m0 = rb * MLP1_ROWS + wv * 32;
+        const int64_t seg = (m0 < M ? m0 : M - 1) / S;
+        const float s_a = pow2_scale(__uint_as_float(amax[seg]));
+        const float2* st = astats_all + seg * K;
+        int64_t mrow[2];
+        bool mok[2];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        const int n = 16 * j + (lane & 15);
-        const float bn = n < N ? bias[n] : 0.0f;
-        double su = 0.0, sq = 0.0;
+        for (int a = 0; a < 2; ++a) {
+            mrow[a] = m0 + 16 * a + (lane & 15);
+            mok[a] = mrow[a] < M;
+        }
+        auto load = [&](int s, int a, f4n (&x)[2]) {
+            const int k = DIN_E * s + 8 * q;
+            x[0] = x[1] = f4n{0.0f, 0.0f, 0.0f, 0.0f};
+            if (!mok[a]) return;
+            const float* p = A + mrow[a] * K + k;
+            if (k + 8 <= K && (K & 3) == 0) {
+                x[0] = *reinterpret_cast<const f4n*>(p);
+                x[1] = *reinterpret_cast<const f4n*>(p + 4);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (k + e < K) x[e >> 2][e & 3] = p[e];
+            }
+        };
+        din_f4 acc[2][NT];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t m = m0 + 16 * a + 4 * q + r;
-                const float v = acc[a][j][r] * inv + bn;
-                if (n < N && m < M) {
-                    C[m * N + n] = v;
-                    su += (double)v;
-                    sq += (double)v * (double)v;
+            for (int j = 0; j < NT; ++j) acc[a][j] = din_f4{0.0f, 0.0f, 0.0f, 0.0f};
+        f4n cur[2][2], nxt[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) load(0, a, cur[a]);
+        for (int s = 0; s < KS; ++s) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                if (s + 1 < KS) load(s + 1, a, nxt[a]);
+            const int k = DIN_E * s + 8 * q;
+            float mu[8], iv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float2 t = k + e < K ? st[k + e] : make_float2(0.0f, 0.0f);
+                mu[e] = t.x;
+                iv[e] = t.y;
+            }
+            din_half8 ahi[2], alo[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = k + e < K ? dice_fast(cur[a][e >> 2][e & 3], mu[e], iv[e]) : 0.0f;
+                split8(v, s_a, ahi[a], alo[a]);
+            }
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const din_half8 bh = wb[((s * NT + j) * 2) * 64 + lane];
+                const din_half8 bl = wb[((s * NT + j) * 2 + 1) * 64 + lane];
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[a], bh, acc[a][j], 0, 0, 0);
+                    acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[a], bl, acc[a][j], 0, 0, 0);
+                    acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[a], bh, acc[a][j], 0, 0, 0);
                 }
             }
-        su += __shfl_xor(su, 16, WAVE);
-        sq += __shfl_xor(sq, 16, WAVE);
-        su += __shfl_xor(su, 32, WAVE);
-        sq += __shfl_xor(sq, 32, WAVE);
-        if (lane < 16) cs[wv * NT * 16 + n] = make_double2(su, sq);
-    }
-    __syncthreads();
-    for (int e = tid; e < 2 * N; e += 256) {
-        const int hf = e / N, n = e % N;
-        const int64_t blk = (int64_t)blockIdx.x * 2 + hf;
-        if (blk * 64 < M) {
-            const double2 x = cs[(2 * hf) * NT * 16 + n], y = cs[(2 * hf + 1) * NT * 16 + n];
-            partial[((size_t)blk * N + n) * 2] = x.x + y.x;
-            partial[((size_t)blk * N + n) * 2 + 1] = x.y + y.y;
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                cur[a][0] = nxt[a][0];
+                cur[a][1] = nxt[a][1];
+            }
         }
+        mlp_epilogue<NT>(acc, 1.0f / (s_a * s_w), bias, N, M, m0, rb * 2, S, cs, C, partial, nullptr);
     }
 }
 
@@ -869,8 +989,8 @@ __device__ __forceinline__ void gemm_load(const float* __restrict__ A, const flo
 #pragma unroll
         for (int e = 0; e < 8; ++e)
             if (k + e < K) {
-                const float2 st = astats[k + e];
-                a[e] = dice(a[e], st.x, st.y);
+                const float2 st = astats[k + e];  // (mean, 1 / (std + 1e-8))
+                a[e] = dice_fast(a[e], st.x, st.y);
             }
     }
 }
@@ -958,7 +1078,7 @@ __global__ void din_head_kernel(const float* __restrict__ Z, const float2* __res
     float s = 0.0f;
     for (int j = lane; j < H; j += 64) {
         const float2 st = zstats[j];
-        s += w[j] * dice(Z[b * H + j], st.x, st.y);
+        s += w[j] * dice_fast(Z[b * H + j], st.x, st.y);  // st = (mean, 1 / (std + 1e-8))
     }
     s = wave_sum_f32(s);
     if (lane == 0) {
@@ -1001,6 +1121,7 @@ struct DinWs {
     float2* hinv;    // fast path only: per-segment (mean, 1 / (std + 1e-8)) of h
     unsigned int* whmax;  // fast path: per-segment max |wh| (float bits), then max |W0|
     din_half8* w1pack;    // fast path: packed W0 fragments
+    din_half8* w2pack;    // fast path, h2 <= 128: packed W1 fragments
     float* z1;
     double* z1part;
     float2* z1stats;
@@ -1014,6 +1135,11 @@ static inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // fast path: wave-per-sample wh + gather-on-load split-fp16 GEMM1
 static inline bool din_fast(int T, int h1) { return T <= 64 && h1 <= 256; }
+static inline bool din_fast2(int T, int h1, int h2) { return din_fast(T, h1) && h2 <= 128; }
+static inline int din_mlp2_nt(int h2) {
+    const int nt = (h2 + 15) / 16;
+    return nt <= 2 ? 2 : nt <= 4 ? 4 : nt <= 5 ? 5 : 8;
+}
 static inline int din_mlp1_nt(int h1) {
     const int nt = (h1 + 15) / 16;
     return nt <= 4 ? 4 : nt <= 8 ? 8 : nt <= 13 ? 13 : 16;
@@ -1037,7 +1163,11 @@ static DinWs din_ws_layout(void* base, int64_t N, int64_t S, int T, int n_user, 
     w.mlp_in = fast ? nullptr : (float*)take((size_t)N * IN * 4);
     w.wh = fast ? (float*)take((size_t)N * n_item * DIN_E * 4) : nullptr;
     w.hinv = fast ? (float2*)take((size_t)n_seg * T * DIN_H * 8) : nullptr;
-    w.whmax = fast ? (unsigned int*)take((size_t)(n_seg + 1) * 4) : nullptr;
+    // [max |wh| per segment][max |W0|][max |z1| per segment][max |W1|]
+    w.whmax = fast ? (unsigned int*)take((size_t)(2 * n_seg + 2) * 4) : nullptr;
+    w.w2pack = din_fast2(T, h1, h2)
+                   ? (din_half8*)take((size_t)((h1 + DIN_E - 1) / DIN_E) * din_mlp2_nt(h2) * 2048)
+                   : nullptr;
     w.w1pack = fast ? (din_half8*)take((size_t)(IN / DIN_E) * din_mlp1_nt(h1) * 2048) : nullptr;
     w.z1 = (float*)take((size_t)N * h1 * 4);
     w.z1part = (double*)take((size_t)nb_m * h1 * 16);
@@ -1159,7 +1289,7 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     if (din_fast(T, h1)) {
         // max |W0| -> packed split-fp16 W0; per-segment max |wh| (zeroed here)
         unsigned int* w1max = w.whmax + n_seg;
-        if (hipMemsetAsync(w.whmax, 0, (size_t)(n_seg + 1) * 4, s) != hipSuccess) {
+        if (hipMemsetAsync(w.whmax, 0, (size_t)(2 * n_seg + 2) * 4, s) != hipSuccess) {
             set_error("nrk_din_forward: hipMemsetAsync failed");
             return NRK_EHIP;
         }
@@ -1191,7 +1321,7 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
                                                 n_item, n_ctx, user_idx, item_idx, ctx_idx, w.wh, w.whmax, \
                                                 pf, w1max,                                                 \
                                                 reinterpret_cast<const din_u4*>(w.w1pack), mlp_b0, batch,   \
-                                                S, h1, w.z1, w.z1part)
+                                                S, h1, w.z1, w.z1part, w.whmax + n_seg + 1)
         if (table_dtype == 0) {
             if (NT == 4) NRK_MLP1(float, 4); else if (NT == 8) NRK_MLP1(float, 8);
             else if (NT == 13) NRK_MLP1(float, 13); else NRK_MLP1(float, 16);
@@ -1214,11 +1344,34 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         w.mlp_in, nullptr, mlp_w0, mlp_b0, batch, S, h1, IN, w.z1, w.z1part);
     }
     col_stats_kernel<<<dim3(gs, (h1 + 3) / 4), 256, 0, s>>>(w.z1part, bps, (int)nb_m, h1, batch, S,
-                                                            w.z1stats);
-    din_gemm_kernel<true><<<dim3((unsigned)nb_m, (h2 + 63) / 64), 512, 0, s>>>(
-        w.z1, w.z1stats, mlp_w1, mlp_b1, batch, S, h2, h1, w.z2, w.z2part);
+                                                            nullptr, w.z1stats);
+    if (din_fast2(T, h1, h2)) {
+        unsigned int* z1max = w.whmax + n_seg + 1;
+        unsigned int* w2max = z1max + n_seg;
+        const int64_t nw = (int64_t)h2 * h1;
+        din_absmax_kernel<<<(int)std::min<int64_t>((nw + 255) / 256, 256), 256, 0, s>>>(mlp_w1, 0, nw, w2max);
+        const int NT2 = din_mlp2_nt(h2);
+        const int KS2 = (h1 + DIN_E - 1) / DIN_E;
+        const int gp = (int)std::min<int64_t>(((int64_t)KS2 * NT2 * 64 + 255) / 256, 512);
+        const size_t lds = (size_t)KS2 * NT2 * 2048 + (size_t)4 * NT2 * 16 * 16;
+        const unsigned g2 = (unsigned)std::min<int64_t>((batch + MLP1_ROWS - 1) / MLP1_ROWS, 512);
+#define NRK_MLP2(NTV)                                                                                   \
+    do {                                                                                                \
+        din_w1_pack_kernel<NTV><<<gp, 256, 0, s>>>(mlp_w1, h2, h1, w2max, w.w2pack);                     \
+        (void)hipFuncSetAttribute((const void*)din_mlp2_kernel<NTV>,                                     \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
+        din_mlp2_kernel<NTV><<<g2, 256, lds, s>>>(w.z1, w.z1stats, z1max, w2max,                         \
+                                                  reinterpret_cast<const din_u4*>(w.w2pack), mlp_b1,     \
+                                                  batch, S, h1, h2, w.z2, w.z2part);                     \
+    } while (0)
+        if (NT2 == 2) NRK_MLP2(2); else if (NT2 == 4) NRK_MLP2(4); else if (NT2 == 5) NRK_MLP2(5); else NRK_MLP2(8);
+#undef NRK_MLP2
+    } else {
+        din_gemm_kernel<true><<<dim3((unsigned)nb_m, (h2 + 63) / 64), 512, 0, s>>>(
+            w.z1, w.z1stats, mlp_w1, mlp_b1, batch, S, h2, h1, w.z2, w.z2part);
+    }
     col_stats_kernel<<<dim3(gs, (h2 + 3) / 4), 256, 0, s>>>(w.z2part, bps, (int)nb_m, h2, batch, S,
-                                                            w.z2stats);
+                                                            nullptr, w.z2stats);
     din_head_kernel<<<(unsigned)gb, 256, 0, s>>>(w.z2, w.z2stats, batch, S, h2, mlp_w2, mlp_b2,
                                                  out_probs, out_logits);
     NRK_CHECK_LAUNCH();
