@@ -48,20 +48,34 @@ PEAK_HBM_GBS = 8000.0
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
 
 
+def _traffic_file():
+    return json.load(open(TRAFFIC_FILE)) if os.path.exists(TRAFFIC_FILE) else None
+
+
 def pmc_traffic(kernels, default_config):
     """HBM-side bytes per launch of ``kernels`` (summed) from the committed
     rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench at its default
     config (tools/pmc_traffic.py applies the gfx950 corrections); None when
     the run is not at that config or the file is absent."""
-    if not default_config or not os.path.exists(TRAFFIC_FILE):
+    tf = _traffic_file()
+    if not default_config or tf is None:
         return None
-    ks = json.load(open(TRAFFIC_FILE))["kernels"]
+    ks = tf["kernels"]
     tot = 0.0
     for k in kernels:
         if k not in ks:
             return None
         tot += ks[k]["traffic_bytes_per_launch"]
     return tot
+
+
+def pmc_din_pass(default_config):
+    """HBM-side bytes of one whole DIN config-3 pass (every launch of one
+    nrk_din_forward_segments call), from the committed PMC passes."""
+    tf = _traffic_file()
+    if not default_config or tf is None or "din_pass" not in tf:
+        return None
+    return tf["din_pass"]["traffic_bytes"]
 
 
 def log(*a):
@@ -190,18 +204,14 @@ def run_din(args, device, rank, world):
     pass_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     value = n / dt
     achieved = DIN_BYTES_PER_PAIR * n / (pass_ms * 1e-3) / 1e9
-    t = pmc_traffic(["nrk::din_att_h_kernel<unsigned short, 4, 1>", "nrk::col_stats_kernel",
-                     "nrk::din_att_out_kernel<unsigned short>", "nrk::din_gemm_kernel<false>",
-                     "nrk::din_gemm_kernel<true>", "nrk::din_head_kernel"], n == DIN_SAMPLES)
-    if t is not None:
-        t += 2 * pmc_traffic(["nrk::col_stats_kernel"], True)  # three col_stats launches per pass
+    t = pmc_din_pass(n == DIN_SAMPLES)
     din_traffic = round(t) if t else None
     out = {"value": round(value * world, 1), "unit": "DIN scored pairs/s", "ms_per_pass": round(dt * 1e3, 3),
            "samples": n, "batch": B, "seq_len": T, "dtype": "fp32 math, bf16 tables",
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": din_traffic,
-                        "traffic_unit": "bytes per pass, all 8 launches (profiles/r01_traffic.json)",
-                        "kernel": f"nrk_din_forward_segments ({n} samples in Dice batches of {B}, 8 launches)",
+                        "traffic_unit": "bytes per pass, every launch of one nrk_din_forward_segments call (profiles/r01_traffic.json din_pass)",
+                        "kernel": f"nrk_din_forward_segments ({n} samples in Dice batches of {B}, one call)",
                         "kernel_ms": round(pass_ms, 4),
                         "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * n}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -352,7 +362,7 @@ def main():
     flops = 2.0 * U * cat.n * D
     achieved = flops / (screen_ms * 1e-3) / 1e12
     default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and not catalog_mode
-    traffic = pmc_traffic(["nrk::ip_screen_kernel<32>"], default_cfg)
+    traffic = pmc_traffic(["nrk::ip_screen_kernel<32, 8>"], default_cfg)
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                 "traffic": round(traffic) if traffic else None,
