@@ -157,6 +157,32 @@ int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
                     const double* vals, const int64_t* first, int topn, int32_t* out_cols,
                     double* out_vals, int32_t* out_cnt, nrk_stream_t stream);
 
+/* ItemCFRecaller.recall for a batch of query users (replaces the per-user
+ * host loop of src/recall/itemcf_recaller.py:56-129).  Dense item ids; the
+ * user click lists in CSR (offsets, items; the history order of
+ * user_item_time_dict); q_slot[q] = the query's row in that CSR or -1 for an
+ * unknown user (cold start, :68-70).  nbr_*: per item its top-n neighbours
+ * [n_items, topn] from nrk_itemcf_topn (A9).  emb_* (ke = 0: none): per item
+ * up to ke embedding neighbours (EmbeddingSimilarity, the content weight of
+ * :98-103).  hot: item_topk_click (dense), the fill order of :116-122.
+ * Pass 1 (nrk_itemcf_recall_offsets): cand_off[q] = exclusive prefix of the
+ * candidate counts, cand_off[n_query] = n_cand (read it to size the
+ * workspace).  Pass 2: per query up to topk (item, score) sorted like
+ * sorted(item_rank.items(), key=score, reverse=True)[:topk] -- ties in dict
+ * insertion order; out_src = 0 scored candidate, 1 hot fill (-x - 100),
+ * 2 cold start (-x), -1 padding.  topk <= 64. */
+int nrk_itemcf_recall_offsets(const int64_t* q_slot, int64_t n_query, const int64_t* offsets,
+                              const int32_t* items, const int32_t* nbr_cnt, int64_t* cand_off,
+                              nrk_stream_t stream);
+size_t nrk_itemcf_recall_workspace_bytes(int64_t n_cand);
+int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* offsets, const int32_t* items,
+                      const int32_t* nbr_cols, const double* nbr_vals, const int32_t* nbr_cnt, int topn,
+                      const double* created, int32_t n_items, const int32_t* hot, int n_hot,
+                      const int32_t* emb_cols, const double* emb_vals, const int32_t* emb_cnt, int ke,
+                      double loc_beta, double created_alpha, const int64_t* cand_off, int64_t n_cand,
+                      int topk, int32_t* out_items, double* out_scores, int32_t* out_src,
+                      int32_t* out_cnt, void* workspace, size_t workspace_bytes, nrk_stream_t stream);
+
 /* ---------------------------------------------------------------------- */
 /* DIN attention-over-history scorer                                      */
 /* ---------------------------------------------------------------------- */

@@ -297,11 +297,11 @@ __global__ __launch_bounds__(RS_THREADS) void cf_emit(
         double s = 0.0;
         for (int64_t q = e; q < n && keys[q] == k; ++q) s += w[vals[q]];
         const int32_t i = (int32_t)(k >> bj), j = (int32_t)(k & jmask);
-        const unsigned long long ci = cnt[i], cj = cnt[j];
+        const unsigned long long ci = cnt ? cnt[i] : 1ull, cj = cnt ? cnt[j] : 1ull;
         // wij / math.sqrt(item_cnt[i] * item_cnt[j])  (item_cf.py:81-84)
         out_i[idx] = i;
         out_j[idx] = j;
-        out_v[idx] = s / sqrt((double)(ci * cj));
+        out_v[idx] = cnt ? s / sqrt((double)(ci * cj)) : s;
         out_first[idx] = vals[e];
         ++idx;
     }
@@ -391,6 +391,254 @@ __global__ __launch_bounds__(256) void cf_topn_kernel(const int64_t* __restrict_
     }
 }
 
+// ------------------------------------------------------------- recall --
+// ItemCFRecaller.recall (itemcf_recaller.py:56-129) for a batch of query
+// users.  The reference accumulates item_rank[j] += w over (loc, x) -- the
+// history position and the rank in item i's top-n list -- and breaks score
+// ties by dict insertion order.  Every candidate (q, loc, x) gets a global
+// sequence number c = cand_off[q] + (position in that walk), so the same
+// stable (key, c) radix sort + ordered segment sums as the similarity pass
+// reproduce the reference's sums and first-encounter order exactly:
+//   rc_count / rc_scan   C_q = sum_loc nbr_cnt[items[loc]], exclusive offsets;
+//   rc_cand              one wave per query: key (q << bj | j) (sentinel for
+//                        j in the history), c, and the contribution
+//                        exp(alpha^|ct_i - ct_j|) * beta^(L - loc) * content * w_ij;
+//   radix sort + cf_emit (q, j, score, first c) per distinct key;
+//   rc_topk              one wave per query: hot-item fill while fewer than
+//                        topk entries (:116-122), then the top-k by
+//                        (score desc, insertion order asc), as sorted(...)[:topk].
+__global__ __launch_bounds__(256) void rc_count_kernel(const int64_t* __restrict__ q_slot, int64_t nq,
+                                                       const int64_t* __restrict__ offsets,
+                                                       const int32_t* __restrict__ items,
+                                                       const int32_t* __restrict__ nbr_cnt,
+                                                       int64_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); q < nq; q += nw) {
+        const int64_t sl = q_slot[q];
+        int64_t c = 0;
+        if (sl >= 0)
+            for (int64_t l = offsets[sl] + lane; l < offsets[sl + 1]; l += 64) c += nbr_cnt[items[l]];
+#pragma unroll
+        for (int k = 32; k > 0; k >>= 1) c += __shfl_xor(c, k, WAVE);
+        if (lane == 0) cnt[q] = c;
+    }
+}
+
+// exclusive scan of n int64 counts -> off[0..n], one workgroup
+__global__ __launch_bounds__(1024) void rc_scan_kernel(const int64_t* __restrict__ cnt, int64_t n,
+                                                      int64_t* __restrict__ off) {
+    __shared__ int64_t part[1024];
+    const int tid = threadIdx.x;
+    const int64_t chunk = (n + 1023) / 1024;
+    const int64_t a = tid * chunk, e = a + chunk < n ? a + chunk : n;
+    int64_t s = 0;
+    for (int64_t u = a; u < e; ++u) s += cnt[u];
+    part[tid] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int64_t v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int64_t run = part[tid] - s;
+    for (int64_t u = a; u < e; ++u) {  // (in place: cnt may alias off)
+        const int64_t c = cnt[u];
+        off[u] = run;
+        run += c;
+    }
+    if (tid == 1023) off[n] = part[1023];
+}
+
+struct RcParams {
+    double loc_beta, created_alpha;
+    int topn, ke, bj;
+};
+
+__device__ __forceinline__ bool rc_find(const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                        int n, int32_t key, double& v) {
+    for (int x = 0; x < n; ++x)
+        if (cols[x] == key) {
+            v = vals[x];
+            return true;
+        }
+    return false;
+}
+
+__global__ __launch_bounds__(256) void rc_cand_kernel(
+    const int64_t* __restrict__ q_slot, int64_t nq, const int64_t* __restrict__ offsets,
+    const int32_t* __restrict__ items, const int32_t* __restrict__ nbr_cols,
+    const double* __restrict__ nbr_vals, const int32_t* __restrict__ nbr_cnt,
+    const double* __restrict__ created, const int32_t* __restrict__ emb_cols,
+    const double* __restrict__ emb_vals, const int32_t* __restrict__ emb_cnt, RcParams prm,
+    const int64_t* __restrict__ cand_off, uint64_t sentinel, uint64_t* __restrict__ keys,
+    int32_t* __restrict__ vals, double* __restrict__ contrib) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); q < nq; q += nw) {
+        const int64_t sl = q_slot[q];
+        if (sl < 0) continue;
+        const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
+        int64_t c = cand_off[q];
+        for (int64_t loc = 0; loc < L; ++loc) {
+            const int32_t i = items[b + loc];
+            const int n = nbr_cnt[i];
+            // position_weight(len(hist) - loc) (:92-95)
+            const double lw = pow(prm.loc_beta, (double)(L - loc));
+            for (int x = lane; x < n; x += 64) {
+                const int32_t j = nbr_cols[(int64_t)i * prm.topn + x];
+                const double wij = nbr_vals[(int64_t)i * prm.topn + x];
+                bool inh = false;
+                for (int64_t l = 0; l < L && !inh; ++l) inh = items[b + l] == j;
+                uint64_t key = sentinel;
+                double v = 0.0;
+                if (!inh) {
+                    // time_decay_weight(created_i, created_j) (:86-90)
+                    const double cw = exp(pow(prm.created_alpha, fabs(created[i] - created[j])));
+                    double content = 1.0;  // (:98-103)
+                    if (prm.ke > 0) {
+                        double e;
+                        if (rc_find(emb_cols + (int64_t)i * prm.ke, emb_vals + (int64_t)i * prm.ke, emb_cnt[i], j, e))
+                            content += e;
+                        if (rc_find(emb_cols + (int64_t)j * prm.ke, emb_vals + (int64_t)j * prm.ke, emb_cnt[j], i, e))
+                            content += e;
+                    }
+                    v = cw * lw * content * wij;
+                    key = ((uint64_t)q << prm.bj) | (uint32_t)j;
+                }
+                keys[c + x] = key;
+                vals[c + x] = (int32_t)(c + x);
+                contrib[c + x] = v;
+            }
+            c += n;
+        }
+    }
+}
+
+// lower bound of q in the emitted (q, j) run (sorted by q)
+__device__ __forceinline__ int64_t rc_lower(const int32_t* __restrict__ oq, int64_t n, int64_t q) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)oq[mid] < q) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void rc_topk_kernel(
+    const int64_t* __restrict__ q_slot, int64_t nq, const int64_t* __restrict__ offsets,
+    const int32_t* __restrict__ items, const int32_t* __restrict__ hot, int n_hot,
+    const int32_t* __restrict__ eq, const int32_t* __restrict__ ej, const double* __restrict__ ev,
+    const int64_t* __restrict__ ef, const int64_t* __restrict__ n_emit, int topk,
+    int32_t* __restrict__ out_items, double* __restrict__ out_scores, int32_t* __restrict__ out_src,
+    int32_t* __restrict__ out_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int64_t ne = *n_emit;
+    const int64_t HOT_FIRST = (int64_t)1 << 62;  // after every candidate (insertion order)
+    for (int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); q < nq; q += nw) {
+        const int64_t sl = q_slot[q];
+        int32_t* oi = out_items + q * topk;
+        double* os = out_scores + q * topk;
+        int32_t* osrc = out_src + q * topk;
+        if (sl < 0) {  // cold start: [(hot[i], -i) for i < topk] (:68-70)
+            const int m = n_hot < topk ? n_hot : topk;
+            if (lane < topk) {
+                oi[lane] = lane < m ? hot[lane] : -1;
+                os[lane] = lane < m ? -(double)lane : 0.0;
+                osrc[lane] = lane < m ? 2 : -1;
+            }
+            if (lane == 0) out_cnt[q] = m;
+            continue;
+        }
+        const int64_t a = rc_lower(eq, ne, q), e = rc_lower(eq, ne, q + 1), n = e - a;
+        CfEnt cur{-INFINITY, INT64_MAX, -1};
+        auto merge = [&](CfEnt x, bool first_chunk) {
+            cf_sort64(x);
+            if (first_chunk) {
+                cur = x;
+                return;
+            }
+            const double ys = __shfl(x.s, 63 - lane, WAVE);
+            const int64_t yf = __shfl(x.f, 63 - lane, WAVE);
+            const int32_t yc = __shfl(x.c, 63 - lane, WAVE);
+            if (cf_better(ys, yf, cur.s, cur.f)) {
+                cur.s = ys;
+                cur.f = yf;
+                cur.c = yc;
+            }
+#pragma unroll
+            for (int j = 32; j > 0; j >>= 1) cf_cmpx(cur, j, (lane & j) == 0);
+        };
+        for (int64_t c0 = 0; c0 < n; c0 += 64) {
+            CfEnt x{-INFINITY, INT64_MAX, -1};
+            if (c0 + lane < n) {
+                x.s = ev[a + c0 + lane];
+                x.f = ef[a + c0 + lane];
+                x.c = ej[a + c0 + lane];
+            }
+            merge(x, c0 == 0);
+        }
+        int64_t total = n;
+        if (n < topk) {
+            // fill with popular items not yet ranked and not in the history,
+            // scored -x - 100, until topk entries (:116-122)
+            const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
+            int need = (int)(topk - n);
+            CfEnt hx{-INFINITY, INT64_MAX, -1};
+            int got = 0;
+            for (int x0 = 0; x0 < n_hot && need > 0; x0 += 64) {
+                const int x = x0 + lane;
+                bool ok = false;
+                int32_t h = -1;
+                if (x < n_hot) {
+                    h = hot[x];
+                    ok = true;
+                    for (int64_t l = 0; l < L && ok; ++l) ok = items[b + l] != h;
+                    if (ok && n > 0) {  // binary search in the query's candidate js (sorted)
+                        int64_t lo = a, hi = e;
+                        while (lo < hi) {
+                            const int64_t mid = (lo + hi) >> 1;
+                            if (ej[mid] < h) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        ok = !(lo < e && ej[lo] == h);
+                    }
+                }
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(ok);
+                const int take = __builtin_popcountll(bal) < need ? __builtin_popcountll(bal) : need;
+                // the first `take` accepted entries, in hot order, into hx lanes got ..
+                for (int t = 0; t < take; ++t) {
+                    // lane holding the t-th set bit of bal
+                    uint64_t bb = bal;
+                    for (int z = 0; z < t; ++z) bb &= bb - 1ull;
+                    const int src = __builtin_ctzll(bb);
+                    const int32_t hv = __shfl(h, src, WAVE);
+                    if (lane == got + t) {
+                        hx.s = (double)(-(x0 + src) - 100);
+                        hx.f = HOT_FIRST + x0 + src;
+                        hx.c = hv;
+                    }
+                }
+                got += take;
+                need -= take;
+            }
+            total += got;
+            if (got > 0) merge(hx, n == 0);
+        }
+        const int64_t m = total < topk ? total : topk;
+        if (lane < topk) {
+            const bool ok = lane < m;
+            oi[lane] = ok ? cur.c : -1;
+            os[lane] = ok ? cur.s : 0.0;
+            osrc[lane] = ok ? (cur.f >= HOT_FIRST ? 1 : 0) : -1;
+        }
+        if (lane == 0) out_cnt[q] = (int32_t)m;
+    }
+}
+
 // ---------------------------------------------------------- workspace --
 struct CfWs {
     uint64_t *ka, *kb;
@@ -418,6 +666,30 @@ static CfWs cf_ws_layout(void* base, int64_t P) {
     w.totals = (uint32_t*)take(256 * 4);
     w.blkcnt = (uint32_t*)take(nblk * 4);
     w.blkoff = (uint32_t*)take(nblk * 4);
+    w.bytes = o;
+    return w;
+}
+
+struct RcWs {
+    CfWs sort;
+    int32_t *eq, *ej;
+    double* ev;
+    int64_t *ef, *n_emit;
+    size_t bytes;
+};
+
+static RcWs rc_ws_layout(void* base, int64_t n_cand) {
+    RcWs w;
+    w.sort = cf_ws_layout(base, n_cand);
+    uint8_t* p = reinterpret_cast<uint8_t*>(base);
+    size_t o = w.sort.bytes;
+    const size_t n = (size_t)(n_cand > 0 ? n_cand : 1);
+    auto take = [&](size_t b) { uint8_t* r = p + o; o += cf_al(b); return r; };
+    w.eq = (int32_t*)take(n * 4);
+    w.ej = (int32_t*)take(n * 4);
+    w.ev = (double*)take(n * 8);
+    w.ef = (int64_t*)take(n * 8);
+    w.n_emit = (int64_t*)take(8);
     w.bytes = o;
     return w;
 }
@@ -511,10 +783,95 @@ int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
     if (topn > 64) NRK_UNSUPPORTED("topn must be <= 64");
     NRK_REQUIRE(n_rows >= 0, "n_rows < 0");
     if (n_rows == 0) return NRK_OK;
-    NRK_REQUIRE(row_off && cols && vals && first && out_cols && out_vals && out_cnt, "null pointer");
+    // cols / vals / first may be null when the CSR has no entries (empty torch tensors)
+    NRK_REQUIRE(row_off && out_cols && out_vals && out_cnt, "null pointer");
     const int64_t g = (n_rows + 3) / 4;
     cf_topn_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, as_stream(stream)>>>(
         row_off, n_rows, cols, vals, first, topn, out_cols, out_vals, out_cnt);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_itemcf_recall_offsets(const int64_t* q_slot, int64_t n_query, const int64_t* offsets,
+                              const int32_t* items, const int32_t* nbr_cnt, int64_t* cand_off,
+                              nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_query >= 0, "n_query < 0");
+    NRK_REQUIRE(cand_off, "null pointer");
+    hipStream_t s = as_stream(stream);
+    if (n_query > 0) {
+        NRK_REQUIRE(q_slot && offsets && items && nbr_cnt, "null pointer");
+        const int64_t g = (n_query + 3) / 4;
+        rc_count_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, s>>>(q_slot, n_query, offsets, items, nbr_cnt,
+                                                                     cand_off);
+    }
+    rc_scan_kernel<<<1, 1024, 0, s>>>(cand_off, n_query, cand_off);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+size_t nrk_itemcf_recall_workspace_bytes(int64_t n_cand) {
+    if (n_cand < 0) return 0;
+    return rc_ws_layout(nullptr, n_cand).bytes;
+}
+
+int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* offsets, const int32_t* items,
+                      const int32_t* nbr_cols, const double* nbr_vals, const int32_t* nbr_cnt, int topn,
+                      const double* created, int32_t n_items, const int32_t* hot, int n_hot,
+                      const int32_t* emb_cols, const double* emb_vals, const int32_t* emb_cnt, int ke,
+                      double loc_beta, double created_alpha, const int64_t* cand_off, int64_t n_cand,
+                      int topk, int32_t* out_items, double* out_scores, int32_t* out_src,
+                      int32_t* out_cnt, void* workspace, size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_query >= 0 && n_cand >= 0 && n_hot >= 0, "negative size");
+    NRK_REQUIRE(topk >= 1, "topk must be >= 1");
+    if (topk > 64) NRK_UNSUPPORTED("topk must be <= 64");
+    NRK_REQUIRE(topn >= 1 && n_items >= 1 && ke >= 0, "bad sizes");
+    NRK_REQUIRE(n_cand < (int64_t(1) << 31) - RS_TILE, "n_cand must be < 2^31");
+    if (n_query == 0) return NRK_OK;
+    NRK_REQUIRE(q_slot && offsets && items && nbr_cols && nbr_vals && nbr_cnt && created && cand_off &&
+                    out_items && out_scores && out_src && out_cnt && workspace,
+                "null pointer");
+    NRK_REQUIRE(n_hot == 0 || hot, "hot is null");
+    NRK_REQUIRE(ke == 0 || (emb_cols && emb_vals && emb_cnt), "emb arrays null");
+    const RcWs w = rc_ws_layout(workspace, n_cand);
+    NRK_REQUIRE(workspace_bytes >= w.bytes, "workspace too small");
+    hipStream_t s = as_stream(stream);
+    const int bj = bits_for(n_items);
+    const int bq = bits_for(n_query);
+    const int nbits = bj + bq;
+    if (nbits > 64) NRK_UNSUPPORTED("n_query * n_items too large for 64-bit keys");
+    const uint64_t sentinel = (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
+    const int64_t g = (n_query + 3) / 4;
+    const int gq = (int)(g < 65536 ? g : 65536);
+    const int64_t n = n_cand;
+    const int nblk = (int)((n + RS_TILE - 1) / RS_TILE);
+    if (n > 0) {
+        const RcParams prm{loc_beta, created_alpha, topn, ke, bj};
+        rc_cand_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created,
+                                          emb_cols, emb_vals, emb_cnt, prm, cand_off, sentinel, w.sort.ka,
+                                          w.sort.va, w.sort.w);
+        uint64_t* kin = w.sort.ka;
+        uint64_t* kout = w.sort.kb;
+        int32_t* vin = w.sort.va;
+        int32_t* vout = w.sort.vb;
+        for (int shift = 0; shift < nbits; shift += 8) {
+            rs_upsweep<<<nblk, RS_THREADS, 0, s>>>(kin, n, shift, nblk, w.sort.counts);
+            rs_scan_rows<<<256, 256, 0, s>>>(w.sort.counts, nblk, w.sort.totals);
+            rs_downsweep<<<nblk, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n, shift, nblk, w.sort.counts,
+                                                     w.sort.totals);
+            uint64_t* tk = kin; kin = kout; kout = tk;
+            int32_t* tv = vin; vin = vout; vout = tv;
+        }
+        cf_head_count<<<nblk, RS_THREADS, 0, s>>>(kin, n, sentinel, w.sort.blkcnt);
+        cf_head_scan<<<1, 1024, 0, s>>>(w.sort.blkcnt, nblk, w.sort.blkoff, w.n_emit);
+        cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, w.sort.w, n, sentinel, w.sort.blkoff, nullptr, bj, w.eq,
+                                             w.ej, w.ev, w.ef);
+    } else {
+        (void)hipMemsetAsync(w.n_emit, 0, sizeof(int64_t), s);
+    }
+    rc_topk_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, hot, n_hot, w.eq, w.ej, w.ev, w.ef,
+                                      w.n_emit, topk, out_items, out_scores, out_src, out_cnt);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

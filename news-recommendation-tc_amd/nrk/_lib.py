@@ -36,11 +36,15 @@ SIGNATURES = {
     "nrk_ip_topk_finish": (INT, [P, I64, P, P, I64, INT, INT, I64, P, P, P, P, SZ, P]),
     "nrk_topk_merge": (INT, [P, P, INT, I64, I64, INT, INT, P, P, P, P]),
     "nrk_row_normalize": (INT, [P, I64, INT, P, P, P]),
-    "nrk_itemcf_pair_offsets":(INT, [P, I64, P, P]),
+    "nrk_itemcf_pair_offsets": (INT, [P, I64, P, P]),
     "nrk_itemcf_workspace_bytes": (SZ, [I64, I32]),
     "nrk_itemcf_sim": (INT, [P, I64, P, P, P, I32, P, I64, F64, F64, F64, F64, F64,
                              P, P, P, P, P, P, P, SZ, P]),
     "nrk_itemcf_topn": (INT, [P, I64, P, P, P, INT, P, P, P, P]),
+    "nrk_itemcf_recall_offsets": (INT, [P, I64, P, P, P, P, P]),
+    "nrk_itemcf_recall_workspace_bytes": (SZ, [I64]),
+    "nrk_itemcf_recall": (INT, [P, I64, P, P, P, P, P, INT, P, I32, P, INT, P, P, P, INT, F64, F64, P, I64,
+                                INT, P, P, P, P, P, SZ, P]),
     "nrk_din_prep_bytes": (SZ, [INT]),
     "nrk_din_prepare": (INT, [P, INT, P, INT, I64, P, P]),
     "nrk_din_workspace_bytes": (SZ, [I64, INT, INT, INT, INT, INT, INT]),

@@ -377,3 +377,49 @@ def itemcf_topn(row_off, cols, vals, first, topn=20):
     _lib.call("nrk_itemcf_topn", _ptr(row_off), n_rows, _ptr(cols), _ptr(vals), _ptr(first), int(topn),
               _ptr(oc), _ptr(ov), _ptr(cnt), _stream())
     return oc, ov, cnt
+
+
+def itemcf_recall(q_slot, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created, hot, topk,
+                  loc_beta=0.9, created_alpha=0.8, emb_cols=None, emb_vals=None, emb_cnt=None):
+    """ItemCFRecaller.recall (itemcf_recaller.py:56-129) for every query user at
+    once.  Dense ids: q_slot [Q] int64 (CSR row or -1 = unknown user),
+    offsets/items = the user_item_time_dict CSR, nbr_* = per-item top-n
+    neighbours [I, topn] (itemcf_topn), created [I] f64, hot [H] int32,
+    optional emb_* [I, ke] content-weight neighbours.  Returns (items [Q, topk]
+    int32 -1 padded, scores [Q, topk] f64, src [Q, topk] int32 (0 candidate,
+    1 hot fill, 2 cold start), cnt [Q] int32)."""
+    _dev(q_slot, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created, hot, emb_cols, emb_vals, emb_cnt)
+    _need(q_slot, torch.int64, name="q_slot")
+    _need(offsets, torch.int64, name="offsets")
+    _need(items, torch.int32, name="items")
+    n_items, topn = nbr_cols.shape
+    _need(nbr_cols, torch.int32, name="nbr_cols")
+    _need(nbr_vals, torch.float64, (n_items, topn), "nbr_vals")
+    _need(nbr_cnt, torch.int32, (n_items,), "nbr_cnt")
+    _need(created, torch.float64, (n_items,), "created")
+    _need(hot, torch.int32, name="hot")
+    ke = 0
+    if emb_cols is not None:
+        ke = emb_cols.shape[1]
+        _need(emb_cols, torch.int32, (n_items, ke), "emb_cols")
+        _need(emb_vals, torch.float64, (n_items, ke), "emb_vals")
+        _need(emb_cnt, torch.int32, (n_items,), "emb_cnt")
+    if not (1 <= topk <= 64):
+        raise NotImplementedError("topk must be in [1, 64]")
+    nq = q_slot.numel()
+    dev = q_slot.device
+    cand_off = torch.empty(nq + 1, dtype=torch.int64, device=dev)
+    _lib.call("nrk_itemcf_recall_offsets", _ptr(q_slot), nq, _ptr(offsets), _ptr(items), _ptr(nbr_cnt),
+              _ptr(cand_off), _stream())
+    n_cand = int(cand_off[nq].item())
+    ws = torch.empty(_lib.lib().nrk_itemcf_recall_workspace_bytes(n_cand), dtype=torch.uint8, device=dev)
+    oi = torch.empty((nq, topk), dtype=torch.int32, device=dev)
+    osc = torch.empty((nq, topk), dtype=torch.float64, device=dev)
+    osrc = torch.empty((nq, topk), dtype=torch.int32, device=dev)
+    ocnt = torch.empty(nq, dtype=torch.int32, device=dev)
+    _lib.call("nrk_itemcf_recall", _ptr(q_slot), nq, _ptr(offsets), _ptr(items), _ptr(nbr_cols),
+              _ptr(nbr_vals), _ptr(nbr_cnt), topn, _ptr(created), n_items, _ptr(hot), hot.numel(),
+              _ptr(emb_cols), _ptr(emb_vals), _ptr(emb_cnt), ke, float(loc_beta), float(created_alpha),
+              _ptr(cand_off), n_cand, int(topk), _ptr(oi), _ptr(osc), _ptr(osrc), _ptr(ocnt), _ptr(ws),
+              ws.numel(), _stream())
+    return oi, osc, osrc, ocnt

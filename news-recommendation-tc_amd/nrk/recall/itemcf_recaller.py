@@ -2,9 +2,12 @@
 
 ``_precompute_topk_similar_items`` (A9, :41-54) runs on the GPU
 (nrk_itemcf_topn: per item, stable top-``itemcf_sim_item_topk`` by score,
-ties in dict insertion order).  ``recall`` (A10, :56-129) is the
-reference's per-user host loop over the precomputed neighbour lists (the GPU
-version of A10 is the next row).
+ties in dict insertion order).  ``recall`` / ``batch_recall`` (A10,
+:56-129) run on the GPU too (nrk_itemcf_recall: every query user of a batch
+in one call -- candidate weights, ordered per-(user, item) sums through a
+stable radix sort, hot-item fill and the stable top-k).  The neighbour
+lists, the user histories and the embedding content weights are laid out
+once, at construction, over one dense id space.
 """
 from __future__ import annotations
 
@@ -52,6 +55,7 @@ class ItemCFRecaller(BaseRecaller):
             for row in r.row_order.tolist():
                 m = int(cnt[row])
                 self.topk_sim_items[int(ids[row])] = list(zip(ids[oc[row, :m]].tolist(), ov[row, :m].tolist()))
+            self._build_device(np.asarray(ids, np.int64), np.asarray(ids, np.int64)[np.maximum(oc, 0)], ov, cnt)
             return
         rows = list(self.i2i_sim.keys())
         lens = np.array([len(self.i2i_sim[i]) for i in rows], np.int64)
@@ -77,39 +81,89 @@ class ItemCFRecaller(BaseRecaller):
             m = int(cnt[r])
             sel = oc[r, :m]
             self.topk_sim_items[i] = list(zip(js[sel].tolist(), vs[sel].tolist()))
+        sel = np.maximum(oc, 0)
+        self._build_device(np.asarray(rows, np.int64).reshape(-1), js[sel] if n else np.zeros(oc.shape, np.int64),
+                           vs[sel] if n else np.zeros(oc.shape), cnt)
+
+    # ----------------------------------------------------------- device --
+    def _build_device(self, rows_raw, cols_raw, vals, cnt):
+        """Dense id space over every item the recall can touch (neighbour rows
+        and columns, histories, hot items) and the device arrays of A10."""
+        d = self.device
+        users = list(self.user_item_time_dict.keys())
+        lens = np.fromiter((len(self.user_item_time_dict[u]) for u in users), np.int64, len(users))
+        offs = np.zeros(len(users) + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+        hist = np.fromiter((it for u in users for it, _ in self.user_item_time_dict[u]), np.int64, int(offs[-1]))
+        hot = np.asarray(list(self.item_topk_click), np.int64)
+        valid = np.arange(cols_raw.shape[1])[None, :] < cnt[:, None]
+        ids = np.unique(np.concatenate([rows_raw, cols_raw[valid], hist, hot]))
+        n = max(len(ids), 1)
+        topn = max(cols_raw.shape[1], 1)
+        nb_cols = np.full((n, topn), -1, np.int32)
+        nb_vals = np.zeros((n, topn), np.float64)
+        nb_cnt = np.zeros(n, np.int32)
+        if len(rows_raw):
+            rp = np.searchsorted(ids, rows_raw)
+            cc = np.where(valid, np.searchsorted(ids, np.where(valid, cols_raw, ids[0])), -1)
+            nb_cols[rp, :cols_raw.shape[1]] = cc
+            nb_vals[rp, :cols_raw.shape[1]] = np.where(valid, vals, 0.0)
+            nb_cnt[rp] = cnt
+        ct = self.item_created_time_dict
+        created = np.fromiter((float(ct.get(int(x), 0.0)) for x in ids), np.float64, len(ids))
+        self._ids = ids
+        self._slot = {u: k for k, u in enumerate(users)}
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(d)  # noqa: E731
+        self._dev = {
+            "offsets": t(offs), "items": t(np.searchsorted(ids, hist).astype(np.int32)),
+            "nbr_cols": t(nb_cols), "nbr_vals": t(nb_vals), "nbr_cnt": t(nb_cnt),
+            "created": t(created if len(ids) else np.zeros(1)), "hot": t(np.searchsorted(ids, hot).astype(np.int32)),
+        }
+        self._emb = None
+        if self.emb_i2i_sim:
+            pos = {int(x): k for k, x in enumerate(ids)}
+            rows = {}
+            for i, dd in self.emb_i2i_sim.items():
+                pi = pos.get(i)
+                if pi is None:
+                    continue
+                rows[pi] = [(pos[j], v) for j, v in dd.items() if j in pos]
+            ke = max([len(r) for r in rows.values()] + [1])
+            if ke > 64:
+                raise NotImplementedError("more than 64 embedding neighbours per item")
+            ec = np.full((n, ke), -1, np.int32)
+            ev = np.zeros((n, ke), np.float64)
+            en = np.zeros(n, np.int32)
+            for pi, r in rows.items():
+                en[pi] = len(r)
+                if r:
+                    ec[pi, :len(r)] = [a for a, _ in r]
+                    ev[pi, :len(r)] = [b for _, b in r]
+            self._emb = (t(ec), t(ev), t(en))
+
+    def batch_recall(self, user_ids: List[int], topk: int = 10) -> Dict[int, List[Tuple[int, float]]]:
+        """Every user of the batch in one nrk_itemcf_recall call (recall/base.py:24-40)."""
+        user_ids = list(user_ids)
+        if not user_ids:
+            return {}
+        dv = self._dev
+        q = torch.tensor([self._slot.get(u, -1) for u in user_ids], dtype=torch.int64, device=self.device)
+        e = self._emb or (None, None, None)
+        oi, osc, osrc, ocnt = ops.itemcf_recall(q, dv["offsets"], dv["items"], dv["nbr_cols"], dv["nbr_vals"],
+                                                dv["nbr_cnt"], dv["created"], dv["hot"], topk,
+                                                self.config.loc_beta, self.config.created_time_alpha, *e)
+        oi, osc, osrc, ocnt = (x.cpu().numpy() for x in (oi, osc, osrc, ocnt))
+        ids = self._ids
+        out = {}
+        for n, u in enumerate(user_ids):
+            m = int(ocnt[n])
+            raw = ids[oi[n, :m]].tolist()
+            sc = osc[n, :m].tolist()
+            src = osrc[n, :m].tolist()
+            # hot-fill / cold-start scores are Python ints in the reference (:70, :120)
+            out[u] = [(it, float(v) if k == 0 else int(v)) for it, v, k in zip(raw, sc, src)]
+        return out
 
     def recall(self, user_id: int, topk: int = 10) -> List[Tuple[int, float]]:
-        """itemcf_recaller.py:56-129, same arithmetic order."""
-        if user_id not in self.user_item_time_dict:
-            return [(item, -i) for i, item in enumerate(self.item_topk_click[:topk])]
-        hist = self.user_item_time_dict[user_id]
-        hist_set = {it for it, _ in hist}
-        beta = self.config.loc_beta
-        calpha = self.config.created_time_alpha
-        ct = self.item_created_time_dict
-        item_rank: Dict[int, float] = {}
-        for loc, (i, _) in enumerate(hist):
-            sims = self.topk_sim_items.get(i)
-            if sims is None:
-                continue
-            for j, wij in sims:
-                if j in hist_set:
-                    continue
-                created_w = np.exp(calpha ** np.abs(ct[i] - ct[j]))
-                loc_w = beta ** (len(hist) - loc)
-                content = 1.0
-                if self.emb_i2i_sim:
-                    if i in self.emb_i2i_sim and j in self.emb_i2i_sim[i]:
-                        content += self.emb_i2i_sim[i][j]
-                    if j in self.emb_i2i_sim and i in self.emb_i2i_sim[j]:
-                        content += self.emb_i2i_sim[j][i]
-                item_rank.setdefault(j, 0)
-                item_rank[j] += created_w * loc_w * content * wij
-        if len(item_rank) < topk:
-            for i, item in enumerate(self.item_topk_click):
-                if item in item_rank or item in hist_set:
-                    continue
-                item_rank[item] = -i - 100
-                if len(item_rank) == topk:
-                    break
-        return sorted(item_rank.items(), key=lambda x: x[1], reverse=True)[:topk]
+        """itemcf_recaller.py:56-129 on the GPU (a batch of one)."""
+        return self.batch_recall([user_id], topk)[user_id]

@@ -144,6 +144,29 @@ def gen_itemcf(tmp):
             rs.append(sc)
         ru.append(u)
         roff.append(len(ri))
+    # the same recall with the content weight of EmbeddingSimilarity (itemcf_recaller.py:98-103)
+    from src.similarity.embedding import EmbeddingSimilarity
+
+    erng = np.random.default_rng(17)
+    art_ids = articles_df["click_article_id"].to_numpy(np.int64)
+    eemb = erng.standard_normal((len(art_ids), 16)).astype(np.float32)
+    edf = pd.DataFrame(eemb, columns=[f"emb_{n}" for n in range(16)])
+    edf.insert(0, "article_id", art_ids)
+    esim = EmbeddingSimilarity(RecallConfig(_project_root=tmp)).calculate(edf)
+    ei, ej, ev = [], [], []
+    for a, dd in esim.items():
+        for b, v in dd.items():
+            ei.append(a)
+            ej.append(b)
+            ev.append(v)
+    erec = ItemCFRecaller(RecallConfig(_project_root=tmp), sim, created, uit, hot, emb_similarity_matrix=esim)
+    eres = erec.batch_recall(users, topk=30)
+    eri, ers, eroff = [], [], [0]
+    for u in users:
+        for it, sc in eres[u]:
+            eri.append(it)
+            ers.append(sc)
+        eroff.append(len(eri))
     # user_item_time_dict as CSR (checks the host-side list builder)
     uu, uoff, uitems, uts = [], [0], [], []
     for u, lst in uit.items():
@@ -175,6 +198,12 @@ def gen_itemcf(tmp):
         recall_scores=np.array(rs, dtype=np.float64),
         topk=np.int64(30),
         sim_item_topk=np.int64(cfg30.itemcf_sim_item_topk),
+        emb_i=np.array(ei, dtype=np.int64),
+        emb_j=np.array(ej, dtype=np.int64),
+        emb_v=np.array(ev, dtype=np.float64),
+        emb_recall_offsets=np.array(eroff, dtype=np.int64),
+        emb_recall_items=np.array(eri, dtype=np.int64),
+        emb_recall_scores=np.array(ers, dtype=np.float64),
     )
     print(f"itemcf_small: {len(si)} sim pairs, {len(users)} users recalled")
 

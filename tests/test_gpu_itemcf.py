@@ -166,3 +166,103 @@ def test_itemcf_full_size():
     same = gc.cpu().numpy() == oc
     # identical except where device/libm last-ulp differences reorder near-ties
     assert same.mean() > 0.9999
+
+
+# ------------------------------------------------------------ A10 recall --
+def _emb_dict(g):
+    out = {}
+    for i, j, v in zip(g["emb_i"].tolist(), g["emb_j"].tolist(), g["emb_v"].tolist()):
+        out.setdefault(i, {})[j] = v
+    return out
+
+
+def test_itemcf_recall_with_embedding_content_weight_matches_reference(golden):
+    """ItemCFRecaller with the EmbeddingSimilarity content weight (itemcf_recaller.py:98-103)
+    against the reference's own output on the same inputs."""
+    from nrk.config import RecallConfig
+    from nrk.data.extractors import csr_to_dict
+    from nrk.recall.itemcf_recaller import ItemCFRecaller
+    from nrk.similarity.item_cf import ItemCFSimilarity
+
+    g = golden("itemcf_small")
+    cfg = RecallConfig(itemcf_sim_item_topk=int(g["sim_item_topk"]))
+    log = synth.ClickLog(g["click_user"], g["click_item"], g["click_ts"])
+    users, offs, items, ts = synth.user_lists(log)
+    created = dict(zip(g["created_ids"].tolist(), g["created_vals"].tolist()))
+    res = ItemCFSimilarity(cfg).compute(users, offs, items, ts, created)
+    uit = csr_to_dict(users, offs, items, ts)
+    rec = ItemCFRecaller.from_result(cfg, res, created, uit, g["hot"].tolist(), emb_similarity_matrix=_emb_dict(g))
+    out = rec.batch_recall([int(u) for u in g["recall_users"]], topk=int(g["topk"]))
+    ro = g["emb_recall_offsets"]
+    for n, u in enumerate(g["recall_users"]):
+        got = out[int(u)]
+        assert [a for a, _ in got] == g["emb_recall_items"][ro[n]:ro[n + 1]].tolist(), n
+        np.testing.assert_allclose([b for _, b in got], g["emb_recall_scores"][ro[n]:ro[n + 1]], rtol=RTOL)
+    # single-user recall() is the same kernel (a batch of one); unknown user -> hot items, int scores
+    u0 = int(g["recall_users"][0])
+    assert rec.recall(u0, topk=30) == out[u0]
+    cold = rec.recall(-5, topk=7)
+    assert cold == [(int(h), -x) for x, h in enumerate(g["hot"][:7].tolist())]
+    assert all(isinstance(s, int) for _, s in cold)
+
+
+def _recall_case(rng, n_users, n_items, max_len, topn, n_hot):
+    from nrk import ops
+
+    offs, items, ts, created = _random_lists(rng, n_users, n_items, max_len)
+    sim = _gpu_sim(offs, items, ts, created, n_items)
+    nc, nv, nn = ops.itemcf_topn(sim.row_offsets(), sim.j, sim.v, sim.first, topn)
+    hot = rng.permutation(n_items)[:n_hot].astype(np.int32)
+    return offs, items, created, nc, nv, nn, hot
+
+
+@pytest.mark.parametrize("n_users,n_items,max_len,topn,topk,n_hot",
+                         [(1, 3, 1, 20, 5, 2), (40, 30, 12, 5, 64, 100), (500, 400, 40, 20, 30, 50),
+                          (3000, 20000, 25, 20, 30, 50), (60, 5000, 250, 64, 64, 64)])
+def test_itemcf_recall_vs_oracle(n_users, n_items, max_len, topn, topk, n_hot):
+    """nrk_itemcf_recall vs the C restatement of ItemCFRecaller.recall
+    (oracle_itemcf_recall): candidate sums in (loc, x) order, hot fill,
+    stable (score desc, insertion order) top-k, unknown users."""
+    from nrk import ops
+
+    rng = np.random.default_rng(n_users * 7 + topk)
+    offs, items, created, nc, nv, nn, hot = _recall_case(rng, n_users, n_items, max_len, topn, n_hot)
+    q = np.concatenate([rng.permutation(n_users), [-1, -1]]).astype(np.int64)  # + two cold-start queries
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    gi, gs, gsrc, gn = ops.itemcf_recall(d(q), d(offs), d(items), nc, nv, nn, d(created), d(hot), topk)
+    oi, os_, on = oracle.itemcf_recall(q, offs, items, nc.cpu().numpy(), nv.cpu().numpy(), nn.cpu().numpy(),
+                                       created, hot, topk, n_items)
+    gi, gs, gsrc, gn = (t.cpu().numpy() for t in (gi, gs, gsrc, gn))
+    assert np.array_equal(gn, on)
+    for r in range(len(q)):
+        m = on[r]
+        assert np.array_equal(gi[r, :m], oi[r, :m]), r
+        np.testing.assert_allclose(gs[r, :m], os_[r, :m], rtol=RTOL, atol=0)
+        assert (gsrc[r, :m] == 2).all() if q[r] < 0 else (gsrc[r, :m] < 2).all()
+
+
+def test_itemcf_recall_full_size():
+    """All 250k users of the synthetic Tianchi log (BASELINE sizes) recalled in
+    one call; every list against the C oracle (identical except where the
+    device and libm exp/pow differ in the last ulp of near-tied scores)."""
+    from nrk import ops
+
+    log = synth.make_click_log(n_users=250_000, n_items=364_047, seed=23)
+    users, offs, items_raw, ts = synth.user_lists(log)
+    ids, dense = np.unique(items_raw, return_inverse=True)
+    dense = dense.astype(np.int32)
+    created = np.random.default_rng(1).random(len(ids))
+    sim = _gpu_sim(offs, dense, ts, created, len(ids))
+    nc, nv, nn = ops.itemcf_topn(sim.row_offsets(), sim.j, sim.v, sim.first, 20)
+    hot = np.argsort(-np.bincount(dense, minlength=len(ids)), kind="stable")[:50].astype(np.int32)
+    q = np.arange(len(users), dtype=np.int64)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    gi, gs, _, gn = ops.itemcf_recall(d(q), d(offs), d(dense), nc, nv, nn, d(created), d(hot), 30)
+    oi, os_, on = oracle.itemcf_recall(q, offs, dense, nc.cpu().numpy(), nv.cpu().numpy(), nn.cpu().numpy(),
+                                       created, hot, 30, len(ids))
+    assert np.array_equal(gn.cpu().numpy(), on)
+    gi = gi.cpu().numpy()
+    valid = np.arange(30)[None, :] < on[:, None]
+    same = (gi == oi) | ~valid
+    assert same.all(axis=1).mean() > 0.9999
+    np.testing.assert_allclose(np.sort(gs.cpu().numpy()[valid]), np.sort(os_[valid]), rtol=1e-11)
