@@ -127,6 +127,76 @@ def cpu_baseline_recall(users_np, items_np, k, sample, threads, seconds):
     return done * (k - 1) / dt, dt, done
 
 
+def run_itemcf(args, device):
+    """Informational ItemCF leg: the whole similarity
+    (nrk_itemcf_sim, item_cf.py:17-89), per-item top-20 (A9) and the recall of
+    every user, top-30 (nrk_itemcf_recall, A10), over the same 250k-user
+    synthetic click log as the recall bench; timed end to end (including the
+    host reads that size the outputs), inputs resident in HBM."""
+    from nrk import ops
+    from nrk.data import synth
+
+    clog = synth.make_click_log(n_users=args.users, n_items=args.items, seed=23)
+    users, offs, items_raw, ts = synth.user_lists(clog)
+    ids, dense = np.unique(items_raw, return_inverse=True)
+    created = np.random.default_rng(1).random(len(ids))
+    hot = np.argsort(-np.bincount(dense, minlength=len(ids)), kind="stable")[:50].astype(np.int32)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+    t_off, t_items, t_ts, t_cr, t_hot = d(offs), d(dense.astype(np.int32)), d(ts), d(created), d(hot)
+    q = torch.arange(len(users), dtype=torch.int64, device=device)
+    n_pairs = int(((offs[1:] - offs[:-1]) ** 2).sum())
+
+    def one():
+        sim = ops.itemcf_sim(t_off, t_items, t_ts, t_cr, len(ids))
+        t1 = time.perf_counter()
+        nc, nv, nn = ops.itemcf_topn(sim.row_offsets(), sim.j, sim.v, sim.first, 20)
+        oi, osc, _, ocnt = ops.itemcf_recall(q, t_off, t_items, nc, nv, nn, t_cr, t_hot, 30)
+        torch.cuda.synchronize()
+        return t1, oi, ocnt
+
+    one()
+    torch.cuda.synchronize()
+    reps = 3
+    t_sim = t_rec = 0.0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        t1, oi, ocnt = one()
+        t2 = time.perf_counter()
+        t_sim += t1 - t0
+        t_rec += t2 - t1
+    t_sim /= reps
+    t_rec /= reps
+    recalled = int(ocnt.sum())
+    out = {"unit": "ordered pairs/s (similarity), recalled pairs/s (recall)",
+           "users": len(users), "items": len(ids), "ordered_pairs": n_pairs,
+           "sim_ms": round(t_sim * 1e3, 3), "sim_pairs_per_s": round(n_pairs / t_sim, 1),
+           "sim_roofline": {"bound": "hbm", "bytes_per_pair": 32,
+                            "achieved": round(32 * n_pairs / t_sim / 1e9, 1), "peak": PEAK_HBM_GBS,
+                            "unit": "GB/s", "frac": round(32 * n_pairs / t_sim / 1e9 / PEAK_HBM_GBS, 4)},
+           "recall_ms": round(t_rec * 1e3, 3), "recall_pairs_per_s": round(recalled / t_rec, 1),
+           "workload": "250k-user synthetic Tianchi log: ItemCF similarity + top-20 per item + top-30 "
+                       "recall of every user"}
+    if not args.no_cpu_baseline:
+        from oracle import oracle
+
+        # the C restatement (single thread) on a bounded prefix of the same
+        # users, grown 4x until one timed run takes >= 2 s (or covers them all)
+        nu = 1000
+        while True:
+            nu = min(nu, len(users))
+            t0 = time.perf_counter()
+            oracle.itemcf_sim(offs[:nu + 1], dense[:offs[nu]].astype(np.int32), ts[:offs[nu]], created, len(ids))
+            dt = time.perf_counter() - t0
+            if dt >= 2.0 or nu == len(users):
+                break
+            nu *= 4
+        sp = int(((offs[1:nu + 1] - offs[:nu]) ** 2).sum())
+        out["cpu_baseline"] = {"value": round(sp / dt, 1), "unit": "ordered pairs/s (similarity)", "cores": 1,
+                               "kind": "port",
+                               "sample": f"first {nu} users, oracle/nrk_oracle.c oracle_itemcf_sim ({dt:.1f}s)"}
+    return out
+
+
 DIN_SAMPLES = 675_653  # README.md:28 (BASELINE config 3)
 DIN_VOCAB_U = [200, 5000, 6, 200000, 3000]
 DIN_VOCAB_I = [462, 3000, 300000, 1500]
@@ -196,11 +266,23 @@ def run_din(args, device, rank, world):
     torch.cuda.synchronize()
     steps = args.din_steps
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
         one_pass(evs[i])
     torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     dt = (time.perf_counter() - t0) / steps
+    if dist is not None:  # whole-job rate: every rank's pass / the slowest rank's time
+        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
     pass_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     value = n / dt
     achieved = DIN_BYTES_PER_PAIR * n / (pass_ms * 1e-3) / 1e9
@@ -253,6 +335,7 @@ def main():
                     help="CPU work timed for each cpu_baseline leg (chunks of --cpu-sample users / batches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-din", action="store_true")
+    ap.add_argument("--no-itemcf", action="store_true", help="skip the informational ItemCF leg")
     ap.add_argument("--shard", choices=["users", "catalog"], default="users",
                     help="N>1 layout: users-sharded (weak scaling, no collective) or "
                          "catalog-sharded (BASELINE config 4: all_to_all of shard top-k + merge)")
@@ -392,6 +475,11 @@ def main():
         din = run_din(args, device, rank, world)
         log(f"DIN: {din['value']:.0f} pairs/s, {din['ms_per_pass']:.1f} ms/pass, device {din['roofline']['kernel_ms']:.3f} ms")
 
+    itemcf = None
+    if world == 1 and not args.no_itemcf:
+        itemcf = run_itemcf(args, device)
+        log(f"ItemCF: sim {itemcf['sim_ms']:.1f} ms, recall {itemcf['recall_ms']:.1f} ms")
+
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "recalled pairs/s",
@@ -407,7 +495,7 @@ def main():
                                        else f"users-sharded x{world}" if world > 1 else "single")},
             "phase_ms": {"tower": round(tower_ms, 4), "screen": round(screen_ms, 4),
                          "finish": round(finish_ms, 4)},
-            "roofline": roofline, "cpu_baseline": cpu, "din": din,
+            "roofline": roofline, "cpu_baseline": cpu, "din": din, "itemcf": itemcf,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
