@@ -229,3 +229,53 @@ def test_din_ranker_predict_batches(golden):
         np.testing.assert_allclose(out3[s:s + 128], po, atol=TOL, rtol=0)
     out4 = sc.predict({k: v[:129] for k, v in b.items()}, 128)
     assert np.isnan(out4[128]) and not np.isnan(out4[:128]).any()
+
+
+def _reference_rank_and_recommend(main_df, probs, top_k):
+    """rank_pipeline.py:162-172, executed with pandas exactly as written there."""
+    df = main_df.copy()
+    df["rank_score"] = probs
+    rec = {}
+    for user_id, group in df.groupby("user_id"):
+        top_items = group.nlargest(top_k, "rank_score")[["item_id", "rank_score"]]
+        rec[str(user_id)] = [(str(row["item_id"]), float(row["rank_score"])) for _, row in top_items.iterrows()]
+    return rec
+
+
+@pytest.mark.parametrize("n_rows,n_users,top_k", [(1, 1, 10), (5000, 700, 10), (20000, 300, 64), (3000, 2999, 3)])
+def test_rank_and_recommend_matches_reference(n_rows, n_users, top_k, tmp_path):
+    """RankPipeline.rank_and_recommend (rank_pipeline.py:143-191): per-user
+    nlargest with first-occurrence ties, NaN after numbers, float-formatted item ids."""
+    import pickle
+
+    import pandas as pd
+
+    from nrk.rank.recommend import rank_and_recommend
+
+    rng = np.random.default_rng(n_rows + top_k)
+    main_df = pd.DataFrame({"user_id": rng.integers(0, n_users, n_rows) * 3 + 1,
+                            "item_id": rng.integers(0, 10**6, n_rows)})
+    probs = (np.round(rng.random(n_rows) * 40) / 40).astype(np.float32)  # many exact ties
+    probs[rng.random(n_rows) < 0.01] = np.nan
+    probs[main_df["user_id"].to_numpy() == main_df["user_id"].iloc[0]] = np.nan  # a user with only NaN scores
+    ref = _reference_rank_and_recommend(main_df, probs, top_k)
+    path = str(tmp_path / "rec.pkl")
+    got = rank_and_recommend(main_df, torch.from_numpy(probs).cuda(), top_k, save_path=path)
+    assert list(got) == list(ref)
+    sizes = main_df.groupby("user_id").size()
+
+    def same(a, b, n_rows):
+        if not np.array_equal([y for _, y in a], [y for _, y in b], equal_nan=True):
+            return False
+        if n_rows > top_k:  # nlargest's selection path: mergesort, ties in row order
+            return a == b or [x for x, _ in a] == [x for x, _ in b]
+        # n >= len(group): nlargest falls back to sort_values(kind="quicksort"), whose
+        # numpy SIMD argsort orders exact ties hardware-dependently -> equal sets per score
+        key = lambda lst: sorted((str(y), x) for x, y in lst)  # noqa: E731
+        return key(a) == key(b)
+
+    for u in ref:
+        assert same(got[u], ref[u], int(sizes[int(u)])), u
+    with open(path, "rb") as f:
+        saved = pickle.load(f)
+    assert all(same(saved[u], ref[u], int(sizes[int(u)])) for u in ref)
