@@ -243,6 +243,28 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
                              float* out_probs, float* out_logits, void* workspace,
                              size_t workspace_bytes, nrk_stream_t stream);
 
+/* ---------------------------------------------------------------------- */
+/* Recall -> rank hand-off (fused config 5)                               */
+/* ---------------------------------------------------------------------- */
+
+/* Builds the DIN index tensors of the recalled pairs of users [u0, u0 + nu)
+ * on the device -- the counterpart of the host feature assembly and
+ * encoding (src/features/feature_extractor.py:440-723, src/rank/DIN.py:330-520)
+ * for the fused pipeline.  rec_rows / rec_scores [n_users, k_in] from
+ * nrk_ip_topk; pair p = (u - u0) * k_use + c uses recall column c + skip
+ * (skip = 1 drops rank 0 as youtubednn_recaller.py:524 does).  user_feat
+ * [n_users, n_user], item_feat [n_items, n_item] table indices; user_hist
+ * [n_users, T] item rows (left-aligned, hist_len valid).  Outputs
+ * out_user [P, n_user], out_item [P, n_item], out_hist [P, T, n_item]
+ * (0 on padding), out_ctx [P, n_ctx] (ctx 0 = recall-score bin + 1, the
+ * rest hash bins + 1), out_mask [P, T], out_cand [P] (candidate item row). */
+int nrk_din_assemble(const int32_t* rec_rows, const float* rec_scores, int64_t n_users, int k_in, int skip,
+                     int k_use, const int32_t* user_feat, int n_user, const int32_t* item_feat,
+                     int64_t n_items, int n_item, const int32_t* user_hist, const int32_t* hist_len, int T,
+                     int n_ctx, int ctx_bins, float score_lo, float score_hi, uint32_t seed, int64_t u0,
+                     int64_t nu, int32_t* out_user, int32_t* out_item, int32_t* out_hist, int32_t* out_ctx,
+                     float* out_mask, int32_t* out_cand, nrk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

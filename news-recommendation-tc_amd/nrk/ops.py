@@ -423,3 +423,36 @@ def itemcf_recall(q_slot, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created, 
               _ptr(cand_off), n_cand, int(topk), _ptr(oi), _ptr(osc), _ptr(osrc), _ptr(ocnt), _ptr(ws),
               ws.numel(), _stream())
     return oi, osc, osrc, ocnt
+
+
+def din_assemble(rec_rows, rec_scores, user_feat, item_feat, user_hist, hist_len, u0, nu, k_use=30, skip=1,
+                 n_ctx=16, ctx_bins=10, score_lo=-1.0, score_hi=1.0, seed=23, out=None):
+    """DIN inputs of the recalled pairs of users [u0, u0 + nu) (nrk_din_assemble).
+    Returns dict user [P, Fu], item [P, Fi], hist [P, T, Fi], ctx [P, n_ctx],
+    mask [P, T] f32, cand [P] (item rows), P = nu * k_use."""
+    _dev(rec_rows, rec_scores, user_feat, item_feat, user_hist, hist_len)
+    n_users, k_in = rec_rows.shape
+    _need(rec_rows, torch.int32, name="rec_rows")
+    _need(rec_scores, torch.float32, (n_users, k_in), "rec_scores")
+    _need(user_feat, torch.int32, name="user_feat")
+    _need(item_feat, torch.int32, name="item_feat")
+    _need(user_hist, torch.int32, name="user_hist")
+    _need(hist_len, torch.int32, (n_users,), "hist_len")
+    Fu, Fi, T = user_feat.shape[1], item_feat.shape[1], user_hist.shape[1]
+    if user_feat.shape[0] != n_users or user_hist.shape[0] != n_users:
+        raise ValueError("user tables must have one row per recalled user")
+    P = nu * k_use
+    dev = rec_rows.device
+    if out is None:
+        out = {"user": torch.empty((P, Fu), dtype=torch.int32, device=dev),
+               "item": torch.empty((P, Fi), dtype=torch.int32, device=dev),
+               "hist": torch.empty((P, T, Fi), dtype=torch.int32, device=dev),
+               "ctx": torch.empty((P, n_ctx), dtype=torch.int32, device=dev),
+               "mask": torch.empty((P, T), dtype=torch.float32, device=dev),
+               "cand": torch.empty(P, dtype=torch.int32, device=dev)}
+    _lib.call("nrk_din_assemble", _ptr(rec_rows), _ptr(rec_scores), n_users, k_in, int(skip), int(k_use),
+              _ptr(user_feat), Fu, _ptr(item_feat), item_feat.shape[0], Fi, _ptr(user_hist), _ptr(hist_len), T,
+              int(n_ctx), int(ctx_bins), float(score_lo), float(score_hi), int(seed) & 0xFFFFFFFF, int(u0), int(nu),
+              _ptr(out["user"]), _ptr(out["item"]), _ptr(out["hist"]), _ptr(out["ctx"]), _ptr(out["mask"]),
+              _ptr(out["cand"]), _stream())
+    return out
