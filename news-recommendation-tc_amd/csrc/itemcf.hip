@@ -15,10 +15,12 @@
 //   2. LSD radix sort  of (key, slot) -- stable, so equal keys keep slot
 //                      order (rs_upsweep / rs_scan_rows / rs_downsweep,
 //                      8 bits per pass, 2b bits total).
-//   3. cf_emit         one entry per distinct key: sequential fp64 sum of
-//                      w[slot] in slot order, / sqrt(cnt_i * cnt_j), and the
-//                      first slot (= dict insertion order, the reference's
-//                      stable-sort tie-break).
+//   3. cf_tile_reduce / cf_carry_scan / cf_emit
+//                      one entry per distinct key: fp64 sum of w[slot] over
+//                      the key's run (slot order within a thread chunk, fixed
+//                      segmented-scan association across chunks and tiles),
+//                      / sqrt(cnt_i * cnt_j), and the first slot (= dict
+//                      insertion order, the reference's stable-sort tie-break).
 // Memory-bound integer/byte work: no MFMA; tiles of 4096 keys per 256-thread
 // workgroup, coalesced 16-element strips.
 #include "nrk_common.h"
@@ -228,20 +230,95 @@ __device__ __forceinline__ bool cf_head(const uint64_t* keys, int64_t e, uint64_
     return k != sentinel && (e == 0 || keys[e - 1] != k);
 }
 
-__global__ __launch_bounds__(RS_THREADS) void cf_head_count(const uint64_t* __restrict__ keys, int64_t n,
-                                                          uint64_t sentinel, uint32_t* __restrict__ blkcnt) {
+// Per-key sums in sorted order as a deterministic segmented reduction (a
+// popular pair's run can be thousands of keys long, far too long for one
+// lane): every key change starts a segment, and fp64 sums are formed per
+// thread chunk (sequential), then combined across the threads of a tile and
+// across tiles by segmented scans with the fixed combine
+//   (f1, v1) . (f2, v2) = (f1 | f2, f2 ? v2 : v1 + v2).
+// The association differs from the reference's strictly sequential
+// S[i][j] += w only in rounding order (values agree to rtol 1e-12, the ItemCF
+// bar), and is the same on every run.
+struct SegSum {
+    double v;
+    int f;
+};
+__device__ __forceinline__ SegSum seg_combine(SegSum a, SegSum b) {
+    return SegSum{b.f ? b.v : a.v + b.v, a.f | b.f};
+}
+
+__device__ __forceinline__ bool cf_brk(const uint64_t* keys, int64_t e) {
+    return e == 0 || keys[e - 1] != keys[e];
+}
+
+// 1. per tile: emitted-head count, the tile's segmented aggregate, and the
+//    gathered weights w[vals[e]] in sorted order (ws)
+__global__ __launch_bounds__(RS_THREADS) void cf_tile_reduce(
+    const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, const double* __restrict__ w,
+    int64_t n, uint64_t sentinel, uint32_t* __restrict__ blkcnt, double* __restrict__ tail,
+    int32_t* __restrict__ brk, double* __restrict__ ws) {
+    __shared__ double tv[RS_THREADS];
+    __shared__ int tf[RS_THREADS];
     __shared__ uint32_t c;
-    if (threadIdx.x == 0) c = 0;
-    __syncthreads();
-    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    const int tid = threadIdx.x;
+    if (tid == 0) c = 0;
+    const int64_t a = (int64_t)blockIdx.x * RS_TILE + (int64_t)tid * RS_ITEMS;
+    SegSum agg{0.0, 0};
     uint32_t my = 0;
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const int64_t e = t0 + r * RS_THREADS + threadIdx.x;
-        if (e < n && cf_head(keys, e, sentinel)) ++my;
+        const int64_t e = a + r;
+        if (e >= n) break;
+        const double x = w[vals[e]];
+        ws[e] = x;
+        const bool b = cf_brk(keys, e);
+        if (b && keys[e] != sentinel) ++my;
+        agg = seg_combine(agg, SegSum{x, b ? 1 : 0});
     }
+    tv[tid] = agg.v;
+    tf[tid] = agg.f;
+    __syncthreads();
     atomicAdd(&c, my);
     __syncthreads();
-    if (threadIdx.x == 0) blkcnt[blockIdx.x] = c;
+    if (tid == 0) {
+        SegSum t{0.0, 0};
+        for (int i = 0; i < RS_THREADS; ++i) t = seg_combine(t, SegSum{tv[i], tf[i]});
+        tail[blockIdx.x] = t.v;
+        brk[blockIdx.x] = t.f;
+        blkcnt[blockIdx.x] = c;
+    }
+}
+
+// 2. carry into every tile: segmented exclusive scan of the tile aggregates
+__global__ __launch_bounds__(1024) void cf_carry_scan(const double* __restrict__ tail,
+                                                    const int32_t* __restrict__ brk, int nblk,
+                                                    double* __restrict__ carry) {
+    __shared__ double pv[1024];
+    __shared__ int pf[1024];
+    const int tid = threadIdx.x;
+    const int chunk = (nblk + 1023) / 1024;
+    const int a = tid * chunk, e = a + chunk < nblk ? a + chunk : nblk;
+    SegSum s{0.0, 0};
+    for (int k = a; k < e; ++k) s = seg_combine(s, SegSum{tail[k], brk[k]});
+    pv[tid] = s.v;
+    pf[tid] = s.f;
+    __syncthreads();
+    for (int dd = 1; dd < 1024; dd <<= 1) {  // inclusive Hillis-Steele, fixed order
+        SegSum o{0.0, 0};
+        const bool has = tid >= dd;
+        if (has) o = SegSum{pv[tid - dd], pf[tid - dd]};
+        __syncthreads();
+        if (has) {
+            const SegSum m = seg_combine(o, SegSum{pv[tid], pf[tid]});
+            pv[tid] = m.v;
+            pf[tid] = m.f;
+        }
+        __syncthreads();
+    }
+    SegSum run = tid > 0 ? SegSum{pv[tid - 1], pf[tid - 1]} : SegSum{0.0, 0};
+    for (int k = a; k < e; ++k) {
+        carry[k] = run.v;
+        run = seg_combine(run, SegSum{tail[k], brk[k]});
+    }
 }
 
 __global__ __launch_bounds__(1024) void cf_head_scan(const uint32_t* __restrict__ blkcnt, int nblk,
@@ -268,42 +345,71 @@ __global__ __launch_bounds__(1024) void cf_head_scan(const uint32_t* __restrict_
     if (tid == 1023) *out_n = part[1023];
 }
 
+// 3. one entry per distinct key: (i, j), the run's sum (normalised by
+//    sqrt(cnt_i cnt_j) when cnt is given, item_cf.py:81-84) and the first slot
+//    (the dict insertion order the reference's stable sorts break ties by)
 __global__ __launch_bounds__(RS_THREADS) void cf_emit(
-    const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, const double* __restrict__ w,
-    int64_t n, uint64_t sentinel, const uint32_t* __restrict__ blkoff,
+    const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, const double* __restrict__ ws,
+    int64_t n, uint64_t sentinel, const uint32_t* __restrict__ blkoff, const double* __restrict__ carry,
     const unsigned long long* __restrict__ cnt, int bj, int32_t* __restrict__ out_i,
     int32_t* __restrict__ out_j, double* __restrict__ out_v, int64_t* __restrict__ out_first) {
-    __shared__ uint32_t part[RS_THREADS];
+    __shared__ double pv[RS_THREADS];
+    __shared__ int pf[RS_THREADS];
+    __shared__ uint32_t ph[RS_THREADS];
     const int tid = threadIdx.x;
     const int64_t a = (int64_t)blockIdx.x * RS_TILE + (int64_t)tid * RS_ITEMS;
+    SegSum agg{0.0, 0};
     uint32_t my = 0;
-    for (int r = 0; r < RS_ITEMS; ++r)
-        if (a + r < n && cf_head(keys, a + r, sentinel)) ++my;
-    part[tid] = my;
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const int64_t e = a + r;
+        if (e >= n) break;
+        const bool b = cf_brk(keys, e);
+        if (b && keys[e] != sentinel) ++my;
+        agg = seg_combine(agg, SegSum{ws[e], b ? 1 : 0});
+    }
+    pv[tid] = agg.v;
+    pf[tid] = agg.f;
+    ph[tid] = my;
     __syncthreads();
-    for (int d = 1; d < RS_THREADS; d <<= 1) {
-        const uint32_t v = tid >= d ? part[tid - d] : 0;
+    for (int dd = 1; dd < RS_THREADS; dd <<= 1) {  // inclusive scans, fixed order
+        SegSum o{0.0, 0};
+        uint32_t oh = 0;
+        const bool has = tid >= dd;
+        if (has) {
+            o = SegSum{pv[tid - dd], pf[tid - dd]};
+            oh = ph[tid - dd];
+        }
         __syncthreads();
-        part[tid] += v;
+        if (has) {
+            const SegSum m = seg_combine(o, SegSum{pv[tid], pf[tid]});
+            pv[tid] = m.v;
+            pf[tid] = m.f;
+            ph[tid] += oh;
+        }
         __syncthreads();
     }
-    uint32_t idx = blkoff[blockIdx.x] + part[tid] - my;
+    SegSum run{carry[blockIdx.x], 0};
+    if (tid > 0) run = seg_combine(run, SegSum{pv[tid - 1], pf[tid - 1]});
+    uint32_t idx = blkoff[blockIdx.x] + ph[tid] - my;  // heads before this thread's chunk
     const uint64_t jmask = (1ull << bj) - 1;
     for (int r = 0; r < RS_ITEMS; ++r) {
         const int64_t e = a + r;
-        if (e >= n || !cf_head(keys, e, sentinel)) continue;
+        if (e >= n) break;
         const uint64_t k = keys[e];
-        // sum in slot order: the reference's S[i][j] += w sequence (item_cf.py:73-79)
-        double s = 0.0;
-        for (int64_t q = e; q < n && keys[q] == k; ++q) s += w[vals[q]];
+        const bool b = cf_brk(keys, e);
+        run = seg_combine(run, SegSum{ws[e], b ? 1 : 0});
+        if (k == sentinel) continue;
         const int32_t i = (int32_t)(k >> bj), j = (int32_t)(k & jmask);
-        const unsigned long long ci = cnt ? cnt[i] : 1ull, cj = cnt ? cnt[j] : 1ull;
-        // wij / math.sqrt(item_cnt[i] * item_cnt[j])  (item_cf.py:81-84)
-        out_i[idx] = i;
-        out_j[idx] = j;
-        out_v[idx] = cnt ? s / sqrt((double)(ci * cj)) : s;
-        out_first[idx] = vals[e];
-        ++idx;
+        if (b) {
+            out_i[idx] = i;
+            out_j[idx] = j;
+            out_first[idx] = vals[e];
+            ++idx;
+        }
+        if (e + 1 == n || keys[e + 1] != k) {  // last of the run: its sum
+            const unsigned long long ci = cnt ? cnt[i] : 1ull, cj = cnt ? cnt[j] : 1ull;
+            out_v[idx - 1] = cnt ? run.v / sqrt((double)(ci * cj)) : run.v;
+        }
     }
 }
 
@@ -645,6 +751,8 @@ struct CfWs {
     int32_t *va, *vb;
     double* w;
     uint32_t *counts, *totals, *blkcnt, *blkoff;
+    double *tail, *carry;
+    int32_t* brk;
     size_t bytes;
 };
 
@@ -666,6 +774,9 @@ static CfWs cf_ws_layout(void* base, int64_t P) {
     w.totals = (uint32_t*)take(256 * 4);
     w.blkcnt = (uint32_t*)take(nblk * 4);
     w.blkoff = (uint32_t*)take(nblk * 4);
+    w.tail = (double*)take(nblk * 8);
+    w.carry = (double*)take(nblk * 8);
+    w.brk = (int32_t*)take(nblk * 4);
     w.bytes = o;
     return w;
 }
@@ -763,9 +874,11 @@ int nrk_itemcf_sim(const int64_t* offsets, int64_t n_users, const int32_t* items
             uint64_t* tk = kin; kin = kout; kout = tk;
             int32_t* tv = vin; vin = vout; vout = tv;
         }
-        cf_head_count<<<nblk, RS_THREADS, 0, s>>>(kin, n, sentinel, w.blkcnt);
+        double* wsorted = reinterpret_cast<double*>(kout);  // the free ping-pong key buffer
+        cf_tile_reduce<<<nblk, RS_THREADS, 0, s>>>(kin, vin, w.w, n, sentinel, w.blkcnt, w.tail, w.brk, wsorted);
         cf_head_scan<<<1, 1024, 0, s>>>(w.blkcnt, nblk, w.blkoff, out_n);
-        cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, w.w, n, sentinel, w.blkoff,
+        cf_carry_scan<<<1, 1024, 0, s>>>(w.tail, w.brk, nblk, w.carry);
+        cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, wsorted, n, sentinel, w.blkoff, w.carry,
                                              reinterpret_cast<const unsigned long long*>(out_cnt), bj,
                                              out_i, out_j, out_v, out_first);
     } else {
@@ -863,10 +976,13 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
             uint64_t* tk = kin; kin = kout; kout = tk;
             int32_t* tv = vin; vin = vout; vout = tv;
         }
-        cf_head_count<<<nblk, RS_THREADS, 0, s>>>(kin, n, sentinel, w.sort.blkcnt);
+        double* wsorted = reinterpret_cast<double*>(kout);
+        cf_tile_reduce<<<nblk, RS_THREADS, 0, s>>>(kin, vin, w.sort.w, n, sentinel, w.sort.blkcnt, w.sort.tail,
+                                                   w.sort.brk, wsorted);
         cf_head_scan<<<1, 1024, 0, s>>>(w.sort.blkcnt, nblk, w.sort.blkoff, w.n_emit);
-        cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, w.sort.w, n, sentinel, w.sort.blkoff, nullptr, bj, w.eq,
-                                             w.ej, w.ev, w.ef);
+        cf_carry_scan<<<1, 1024, 0, s>>>(w.sort.tail, w.sort.brk, nblk, w.sort.carry);
+        cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, wsorted, n, sentinel, w.sort.blkoff, w.sort.carry, nullptr,
+                                             bj, w.eq, w.ej, w.ev, w.ef);
     } else {
         (void)hipMemsetAsync(w.n_emit, 0, sizeof(int64_t), s);
     }
