@@ -30,6 +30,7 @@ namespace nrk {
 constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys per workgroup
+constexpr int64_t CF_HEAVY = 4096;               // top-n rows longer than this get a workgroup
 
 // ------------------------------------------------------ pair offsets --
 // pair_off[u] = sum_{v<u} L_v^2 (exclusive), pair_off[n] = total.  One
@@ -462,6 +463,10 @@ __global__ __launch_bounds__(256) void cf_topn_kernel(const int64_t* __restrict_
     const int64_t nw = (int64_t)gridDim.x * 4;
     for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_rows; row += nw) {
         const int64_t a = row_off[row], n = row_off[row + 1] - a;
+        if (n > CF_HEAVY) {  // a popular item's long row: cf_topn_heavy_kernel, a workgroup per row
+            if (lane == 0) out_cnt[row] = -1;
+            continue;
+        }
         CfEnt cur{-INFINITY, INT64_MAX, -1};
         for (int64_t c0 = 0; c0 < n; c0 += 64) {
             CfEnt x{-INFINITY, INT64_MAX, -1};
@@ -745,6 +750,68 @@ __global__ __launch_bounds__(256) void rc_topk_kernel(
     }
 }
 
+// Rows longer than CF_HEAVY (flagged out_cnt = -1 by cf_topn_kernel): 16 waves
+// run the same running top-64 over interleaved 64-entry chunks, then wave 0
+// merges the 16 lists.  (score, first) is a total order, so the result does
+// not depend on the partition.
+__global__ __launch_bounds__(1024) void cf_topn_heavy_kernel(const int64_t* __restrict__ row_off, int64_t n_rows,
+                                                           const int32_t* __restrict__ cols,
+                                                           const double* __restrict__ vals,
+                                                           const int64_t* __restrict__ first, int topn,
+                                                           int32_t* __restrict__ out_cols,
+                                                           double* __restrict__ out_vals,
+                                                           int32_t* __restrict__ out_cnt) {
+    __shared__ double ls[16][64];
+    __shared__ int64_t lf[16][64];
+    __shared__ int32_t lc[16][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int64_t row = blockIdx.x; row < n_rows; row += gridDim.x) {
+        if (out_cnt[row] != -1) continue;  // uniform across the workgroup
+        const int64_t a = row_off[row], n = row_off[row + 1] - a;
+        CfEnt cur{-INFINITY, INT64_MAX, -1};
+        auto merge_in = [&](CfEnt x) {  // x sorted desc; keep the top 64 of cur + x
+            const double ys = __shfl(x.s, 63 - lane, WAVE);
+            const int64_t yf = __shfl(x.f, 63 - lane, WAVE);
+            const int32_t yc = __shfl(x.c, 63 - lane, WAVE);
+            if (cf_better(ys, yf, cur.s, cur.f)) {
+                cur.s = ys;
+                cur.f = yf;
+                cur.c = yc;
+            }
+#pragma unroll
+            for (int j = 32; j > 0; j >>= 1) cf_cmpx(cur, j, (lane & j) == 0);
+        };
+        bool started = false;
+        for (int64_t c0 = (int64_t)wv * 64; c0 < n; c0 += 16 * 64) {
+            CfEnt x{-INFINITY, INT64_MAX, -1};
+            if (c0 + lane < n) {
+                x.s = vals[a + c0 + lane];
+                x.f = first[a + c0 + lane];
+                x.c = cols[a + c0 + lane];
+            }
+            cf_sort64(x);
+            if (!started) cur = x;
+            else merge_in(x);
+            started = true;
+        }
+        ls[wv][lane] = cur.s;
+        lf[wv][lane] = cur.f;
+        lc[wv][lane] = cur.c;
+        __syncthreads();
+        if (wv == 0) {
+            for (int w = 1; w < 16; ++w) merge_in(CfEnt{ls[w][lane], lf[w][lane], lc[w][lane]});
+            const int64_t m = n < topn ? n : topn;
+            if (lane < topn) {
+                const bool ok = lane < m;
+                out_cols[row * topn + lane] = ok ? cur.c : -1;
+                out_vals[row * topn + lane] = ok ? cur.s : 0.0;
+            }
+            if (lane == 0) out_cnt[row] = (int32_t)m;
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------- workspace --
 struct CfWs {
     uint64_t *ka, *kb;
@@ -900,6 +967,8 @@ int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
     NRK_REQUIRE(row_off && out_cols && out_vals && out_cnt, "null pointer");
     const int64_t g = (n_rows + 3) / 4;
     cf_topn_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, as_stream(stream)>>>(
+        row_off, n_rows, cols, vals, first, topn, out_cols, out_vals, out_cnt);
+    cf_topn_heavy_kernel<<<(int)(n_rows < 512 ? n_rows : 512), 1024, 0, as_stream(stream)>>>(
         row_off, n_rows, cols, vals, first, topn, out_cols, out_vals, out_cnt);
     NRK_CHECK_LAUNCH();
     return NRK_OK;

@@ -134,7 +134,7 @@ def test_itemcf_topn_vs_oracle(topn):
     rng = np.random.default_rng(topn)
     n_rows = 700
     lens = rng.integers(0, 300, n_rows)
-    lens[:5] = [0, 1, 63, 64, 65]
+    lens[:9] = [0, 1, 63, 64, 65, 4096, 4097, 20000, 70000]  # + rows for the workgroup-per-row path
     off = np.zeros(n_rows + 1, np.int64)
     off[1:] = np.cumsum(lens)
     n = int(off[-1])
