@@ -157,6 +157,11 @@ int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
                     const double* vals, const int64_t* first, int topn, int32_t* out_cols,
                     double* out_vals, int32_t* out_cnt, nrk_stream_t stream);
 
+/* CSR row offsets (n_rows + 1) of nrk_itemcf_sim's entries, which are sorted
+ * by i: row_off[r] = number of entries with i < r. */
+int nrk_itemcf_row_offsets(const int32_t* ei, int64_t n, int64_t n_rows, int64_t* row_off,
+                           nrk_stream_t stream);
+
 /* ItemCFRecaller.recall for a batch of query users (replaces the per-user
  * host loop of src/recall/itemcf_recaller.py:56-129).  Dense item ids; the
  * user click lists in CSR (offsets, items; the history order of

@@ -812,6 +812,21 @@ __global__ __launch_bounds__(1024) void cf_topn_heavy_kernel(const int64_t* __re
     }
 }
 
+// CSR row offsets of the (i, j)-sorted similarity entries: off[r] = first
+// entry with i >= r (binary search per row; no atomics)
+__global__ __launch_bounds__(256) void cf_row_offsets_kernel(const int32_t* __restrict__ ei, int64_t n,
+                                                           int64_t n_rows, int64_t* __restrict__ off) {
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r <= n_rows; r += (int64_t)gridDim.x * 256) {
+        int64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)ei[mid] < r) lo = mid + 1;
+            else hi = mid;
+        }
+        off[r] = lo;
+    }
+}
+
 // ---------------------------------------------------------- workspace --
 struct CfWs {
     uint64_t *ka, *kb;
@@ -1057,6 +1072,16 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
     }
     rc_topk_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, hot, n_hot, w.eq, w.ej, w.ev, w.ef,
                                       w.n_emit, topk, out_items, out_scores, out_src, out_cnt);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_itemcf_row_offsets(const int32_t* ei, int64_t n, int64_t n_rows, int64_t* row_off, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n >= 0 && n_rows >= 0, "negative size");
+    NRK_REQUIRE(row_off && (n == 0 || ei), "null pointer");
+    const int64_t g = (n_rows + 1 + 255) / 256;
+    cf_row_offsets_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, as_stream(stream)>>>(ei, n, n_rows, row_off);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

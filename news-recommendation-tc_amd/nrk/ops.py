@@ -315,9 +315,8 @@ class ItemCFSim:
 
     def row_offsets(self):
         """CSR offsets over dense item rows (entries are sorted by i)."""
-        c = torch.bincount(self.i.long(), minlength=self.n_items)
-        off = torch.zeros(self.n_items + 1, dtype=torch.int64, device=self.i.device)
-        off[1:] = torch.cumsum(c, 0)
+        off = torch.empty(self.n_items + 1, dtype=torch.int64, device=self.i.device)
+        _lib.call("nrk_itemcf_row_offsets", _ptr(self.i), self.i.numel(), self.n_items, _ptr(off), _stream())
         return off
 
 
