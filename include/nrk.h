@@ -157,6 +157,29 @@ int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
                     const double* vals, const int64_t* first, int topn, int32_t* out_cols,
                     double* out_vals, int32_t* out_cnt, nrk_stream_t stream);
 
+/* Users-sharded ItemCF: each rank owns a contiguous user range
+ * and items are owned by contiguous id ranges; one exchange step.
+ * nrk_itemcf_pairs: the pair tuples of the rank's users -- key (i << b | j),
+ * b = smallest with 2^b > n_items (sentinel for i == j), the pair's GLOBAL
+ * slot (slot_base + local slot; the global slot order is the reference's
+ * S[i][j] += w order), weight -- as nrk_itemcf_sim computes them, and the
+ * rank's click counts (item_cnt += ; caller zeroes).  pair_off from
+ * nrk_itemcf_pair_offsets over the rank's users.
+ * nrk_itemcf_reduce: the owner's pass over the tuples it received, in global
+ * slot order (all_to_all concatenates sources in rank order): one entry per
+ * distinct key, (i, j), sum / sqrt(cnt_i cnt_j) with the all-reduced counts,
+ * first slot.  Same results as nrk_itemcf_sim on one GPU. */
+int nrk_itemcf_pairs(const int64_t* offsets, int64_t n_users, const int32_t* items, const int64_t* ts,
+                     const double* created, int32_t n_items, const int64_t* pair_off, int64_t slot_base,
+                     double loc_alpha, double loc_alpha_rev, double loc_beta, double time_alpha,
+                     double created_alpha, uint64_t* keys, int32_t* slots, double* w, int64_t* item_cnt,
+                     nrk_stream_t stream);
+size_t nrk_itemcf_reduce_workspace_bytes(int64_t n);
+int nrk_itemcf_reduce(const uint64_t* keys, const int32_t* slots, const double* w, int64_t n, int32_t n_items,
+                      const int64_t* item_cnt, int32_t* out_i, int32_t* out_j, double* out_v,
+                      int64_t* out_first, int64_t* out_n, void* workspace, size_t workspace_bytes,
+                      nrk_stream_t stream);
+
 /* CSR row offsets (n_rows + 1) of nrk_itemcf_sim's entries, which are sorted
  * by i: row_off[r] = number of entries with i < r. */
 int nrk_itemcf_row_offsets(const int32_t* ei, int64_t n, int64_t n_rows, int64_t* row_off,

@@ -71,7 +71,7 @@ struct CfParams {
 __global__ __launch_bounds__(256) void cf_pairs_kernel(
     const int64_t* __restrict__ offsets, int64_t n_users, const int32_t* __restrict__ items,
     const int64_t* __restrict__ ts, const double* __restrict__ created,
-    const int64_t* __restrict__ pair_off, CfParams prm, int bj, uint64_t sentinel,
+    const int64_t* __restrict__ pair_off, int64_t slot_base, CfParams prm, int bj, uint64_t sentinel,
     uint64_t* __restrict__ keys, int32_t* __restrict__ vals, double* __restrict__ w,
     unsigned long long* __restrict__ cnt) {
     const int lane = threadIdx.x & 63;
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void cf_pairs_kernel(
                 key = ((uint64_t)(uint32_t)i << bj) | (uint32_t)j;
             }
             keys[base + s] = key;
-            vals[base + s] = (int32_t)(base + s);
+            vals[base + s] = (int32_t)(slot_base + base + s);  // the pair's global slot
             w[base + s] = wt;
         }
     }
@@ -352,8 +352,9 @@ __global__ __launch_bounds__(1024) void cf_head_scan(const uint32_t* __restrict_
 __global__ __launch_bounds__(RS_THREADS) void cf_emit(
     const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, const double* __restrict__ ws,
     int64_t n, uint64_t sentinel, const uint32_t* __restrict__ blkoff, const double* __restrict__ carry,
-    const unsigned long long* __restrict__ cnt, int bj, int32_t* __restrict__ out_i,
-    int32_t* __restrict__ out_j, double* __restrict__ out_v, int64_t* __restrict__ out_first) {
+    const unsigned long long* __restrict__ cnt, const int32_t* __restrict__ slots, int bj,
+    int32_t* __restrict__ out_i, int32_t* __restrict__ out_j, double* __restrict__ out_v,
+    int64_t* __restrict__ out_first) {
     __shared__ double pv[RS_THREADS];
     __shared__ int pf[RS_THREADS];
     __shared__ uint32_t ph[RS_THREADS];
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(RS_THREADS) void cf_emit(
         if (b) {
             out_i[idx] = i;
             out_j[idx] = j;
-            out_first[idx] = vals[e];
+            out_first[idx] = slots ? slots[vals[e]] : vals[e];
             ++idx;
         }
         if (e + 1 == n || keys[e + 1] != k) {  // last of the run: its sum
@@ -827,6 +828,14 @@ __global__ __launch_bounds__(256) void cf_row_offsets_kernel(const int32_t* __re
     }
 }
 
+__global__ void cf_iota_copy_kernel(const uint64_t* __restrict__ kin, int64_t n, uint64_t* __restrict__ kout,
+                                    int32_t* __restrict__ v) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        kout[e] = kin[e];
+        v[e] = (int32_t)e;
+    }
+}
+
 // ---------------------------------------------------------- workspace --
 struct CfWs {
     uint64_t *ka, *kb;
@@ -939,7 +948,7 @@ int nrk_itemcf_sim(const int64_t* offsets, int64_t n_users, const int32_t* items
     const int64_t ugrid = (n_users + 3) / 4;
     if (n_users > 0)
         cf_pairs_kernel<<<(int)(ugrid < 65536 ? ugrid : 65536), 256, 0, s>>>(
-            offsets, n_users, items, ts, created, pair_off, prm, bj, sentinel, w.ka, w.va, w.w,
+            offsets, n_users, items, ts, created, pair_off, 0, prm, bj, sentinel, w.ka, w.va, w.w,
             reinterpret_cast<unsigned long long*>(out_cnt));
     const int64_t n = n_pairs;
     const int nblk = (int)((n + RS_TILE - 1) / RS_TILE);
@@ -961,8 +970,8 @@ int nrk_itemcf_sim(const int64_t* offsets, int64_t n_users, const int32_t* items
         cf_head_scan<<<1, 1024, 0, s>>>(w.blkcnt, nblk, w.blkoff, out_n);
         cf_carry_scan<<<1, 1024, 0, s>>>(w.tail, w.brk, nblk, w.carry);
         cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, wsorted, n, sentinel, w.blkoff, w.carry,
-                                             reinterpret_cast<const unsigned long long*>(out_cnt), bj,
-                                             out_i, out_j, out_v, out_first);
+                                             reinterpret_cast<const unsigned long long*>(out_cnt), nullptr,
+                                             bj, out_i, out_j, out_v, out_first);
     } else {
         (void)hipMemsetAsync(out_n, 0, sizeof(int64_t), s);
     }
@@ -1066,7 +1075,7 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
         cf_head_scan<<<1, 1024, 0, s>>>(w.sort.blkcnt, nblk, w.sort.blkoff, w.n_emit);
         cf_carry_scan<<<1, 1024, 0, s>>>(w.sort.tail, w.sort.brk, nblk, w.sort.carry);
         cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, wsorted, n, sentinel, w.sort.blkoff, w.sort.carry, nullptr,
-                                             bj, w.eq, w.ej, w.ev, w.ef);
+                                             nullptr, bj, w.eq, w.ej, w.ev, w.ef);
     } else {
         (void)hipMemsetAsync(w.n_emit, 0, sizeof(int64_t), s);
     }
@@ -1082,6 +1091,77 @@ int nrk_itemcf_row_offsets(const int32_t* ei, int64_t n, int64_t n_rows, int64_t
     NRK_REQUIRE(row_off && (n == 0 || ei), "null pointer");
     const int64_t g = (n_rows + 1 + 255) / 256;
     cf_row_offsets_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, as_stream(stream)>>>(ei, n, n_rows, row_off);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_itemcf_pairs(const int64_t* offsets, int64_t n_users, const int32_t* items, const int64_t* ts,
+                     const double* created, int32_t n_items, const int64_t* pair_off, int64_t slot_base,
+                     double loc_alpha, double loc_alpha_rev, double loc_beta, double time_alpha,
+                     double created_alpha, uint64_t* keys, int32_t* slots, double* w, int64_t* item_cnt,
+                     nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_users >= 0 && slot_base >= 0 && n_items >= 1, "bad sizes");
+    if (n_users == 0) return NRK_OK;
+    NRK_REQUIRE(offsets && items && ts && created && pair_off && keys && slots && w && item_cnt, "null pointer");
+    const int bj = bits_for(n_items);
+    const int nbits = 2 * bj;
+    const uint64_t sentinel = (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
+    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha};
+    const int64_t ugrid = (n_users + 3) / 4;
+    cf_pairs_kernel<<<(int)(ugrid < 65536 ? ugrid : 65536), 256, 0, as_stream(stream)>>>(
+        offsets, n_users, items, ts, created, pair_off, slot_base, prm, bj, sentinel, keys, slots, w,
+        reinterpret_cast<unsigned long long*>(item_cnt));
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+size_t nrk_itemcf_reduce_workspace_bytes(int64_t n) {
+    if (n < 0) return 0;
+    return cf_ws_layout(nullptr, n).bytes;
+}
+
+int nrk_itemcf_reduce(const uint64_t* keys, const int32_t* slots, const double* w, int64_t n, int32_t n_items,
+                      const int64_t* item_cnt, int32_t* out_i, int32_t* out_j, double* out_v,
+                      int64_t* out_first, int64_t* out_n, void* workspace, size_t workspace_bytes,
+                      nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n >= 0 && n_items >= 1, "bad sizes");
+    NRK_REQUIRE(n < (int64_t(1) << 31) - RS_TILE, "n must be < 2^31");
+    NRK_REQUIRE(out_n && workspace, "null pointer");
+    hipStream_t s = as_stream(stream);
+    if (n == 0) {
+        (void)hipMemsetAsync(out_n, 0, sizeof(int64_t), s);
+        NRK_CHECK_LAUNCH();
+        return NRK_OK;
+    }
+    NRK_REQUIRE(keys && slots && w && item_cnt && out_i && out_j && out_v && out_first, "null pointer");
+    const CfWs ws = cf_ws_layout(workspace, n);
+    NRK_REQUIRE(workspace_bytes >= ws.bytes, "workspace too small");
+    const int bj = bits_for(n_items);
+    const int nbits = 2 * bj;
+    const uint64_t sentinel = (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
+    const int nblk = (int)((n + RS_TILE - 1) / RS_TILE);
+    const int64_t g = (n + 255) / 256;
+    cf_iota_copy_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, s>>>(keys, n, ws.ka, ws.va);
+    uint64_t* kin = ws.ka;
+    uint64_t* kout = ws.kb;
+    int32_t* vin = ws.va;
+    int32_t* vout = ws.vb;
+    for (int shift = 0; shift < nbits; shift += 8) {
+        rs_upsweep<<<nblk, RS_THREADS, 0, s>>>(kin, n, shift, nblk, ws.counts);
+        rs_scan_rows<<<256, 256, 0, s>>>(ws.counts, nblk, ws.totals);
+        rs_downsweep<<<nblk, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n, shift, nblk, ws.counts, ws.totals);
+        uint64_t* tk = kin; kin = kout; kout = tk;
+        int32_t* tv = vin; vin = vout; vout = tv;
+    }
+    double* wsorted = reinterpret_cast<double*>(kout);
+    cf_tile_reduce<<<nblk, RS_THREADS, 0, s>>>(kin, vin, w, n, sentinel, ws.blkcnt, ws.tail, ws.brk, wsorted);
+    cf_head_scan<<<1, 1024, 0, s>>>(ws.blkcnt, nblk, ws.blkoff, out_n);
+    cf_carry_scan<<<1, 1024, 0, s>>>(ws.tail, ws.brk, nblk, ws.carry);
+    cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, wsorted, n, sentinel, ws.blkoff, ws.carry,
+                                         reinterpret_cast<const unsigned long long*>(item_cnt), slots, bj,
+                                         out_i, out_j, out_v, out_first);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

@@ -42,6 +42,9 @@ SIGNATURES = {
                              P, P, P, P, P, P, P, SZ, P]),
     "nrk_itemcf_topn": (INT, [P, I64, P, P, P, INT, P, P, P, P]),
     "nrk_itemcf_row_offsets": (INT, [P, I64, I64, P, P]),
+    "nrk_itemcf_pairs": (INT, [P, I64, P, P, P, I32, P, I64, F64, F64, F64, F64, F64, P, P, P, P, P]),
+    "nrk_itemcf_reduce_workspace_bytes": (SZ, [I64]),
+    "nrk_itemcf_reduce": (INT, [P, P, P, I64, I32, P, P, P, P, P, P, P, SZ, P]),
     "nrk_itemcf_recall_offsets": (INT, [P, I64, P, P, P, P, P]),
     "nrk_itemcf_recall_workspace_bytes": (SZ, [I64]),
     "nrk_itemcf_recall": (INT, [P, I64, P, P, P, P, P, INT, P, I32, P, INT, P, P, P, INT, F64, F64, P, I64,

@@ -455,3 +455,51 @@ def din_assemble(rec_rows, rec_scores, user_feat, item_feat, user_hist, hist_len
               _ptr(out["user"]), _ptr(out["item"]), _ptr(out["hist"]), _ptr(out["ctx"]), _ptr(out["mask"]),
               _ptr(out["cand"]), _stream())
     return out
+
+
+# ---------------------------------------------------- users-sharded ItemCF --
+def itemcf_pairs(offsets, items, ts, created, n_items, slot_base=0, loc_alpha=1.0, loc_alpha_rev=0.7,
+                 loc_beta=0.9, time_alpha=0.7, created_alpha=0.8):
+    """Pair tuples of a user range (nrk_itemcf_pairs): keys u64 (as int64),
+    global slots int32, weights f64, local click counts int64 [n_items]."""
+    _dev(offsets, items, ts, created)
+    _need(offsets, torch.int64, name="offsets")
+    _need(items, torch.int32, (items.numel(),), "items")
+    _need(ts, torch.int64, (items.numel(),), "ts")
+    _need(created, torch.float64, (n_items,), "created")
+    n_users = offsets.numel() - 1
+    dev = offsets.device
+    pair_off = torch.empty(n_users + 1, dtype=torch.int64, device=dev)
+    _lib.call("nrk_itemcf_pair_offsets", _ptr(offsets), n_users, _ptr(pair_off), _stream())
+    n = int(pair_off[-1])
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    slots = torch.empty(n, dtype=torch.int32, device=dev)
+    w = torch.empty(n, dtype=torch.float64, device=dev)
+    cnt = torch.zeros(n_items, dtype=torch.int64, device=dev)
+    _lib.call("nrk_itemcf_pairs", _ptr(offsets), n_users, _ptr(items), _ptr(ts), _ptr(created), n_items,
+              _ptr(pair_off), int(slot_base), float(loc_alpha), float(loc_alpha_rev), float(loc_beta),
+              float(time_alpha), float(created_alpha), _ptr(keys), _ptr(slots), _ptr(w), _ptr(cnt), _stream())
+    return keys, slots, w, cnt
+
+
+def itemcf_reduce(keys, slots, w, n_items, item_cnt):
+    """The owner's pass (nrk_itemcf_reduce) over tuples in global slot order ->
+    ItemCFSim of its items (entries sorted by (i, j))."""
+    _dev(keys, slots, w, item_cnt)
+    n = keys.numel()
+    _need(keys, torch.int64, name="keys")
+    _need(slots, torch.int32, (n,), "slots")
+    _need(w, torch.float64, (n,), "w")
+    _need(item_cnt, torch.int64, (n_items,), "item_cnt")
+    dev = item_cnt.device
+    cap = max(n, 1)
+    oi = torch.empty(cap, dtype=torch.int32, device=dev)
+    oj = torch.empty(cap, dtype=torch.int32, device=dev)
+    ov = torch.empty(cap, dtype=torch.float64, device=dev)
+    of = torch.empty(cap, dtype=torch.int64, device=dev)
+    on = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = torch.empty(_lib.lib().nrk_itemcf_reduce_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    _lib.call("nrk_itemcf_reduce", _ptr(keys), _ptr(slots), _ptr(w), n, n_items, _ptr(item_cnt), _ptr(oi),
+              _ptr(oj), _ptr(ov), _ptr(of), _ptr(on), _ptr(ws), ws.numel(), _stream())
+    m = int(on.item())
+    return ItemCFSim(oi[:m], oj[:m], ov[:m], of[:m], item_cnt, n_items)

@@ -97,3 +97,127 @@ def test_shard_range_covers():
             spans = [shard_range(n, w, r) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+# ------------------------------------------------ users-sharded ItemCF --
+def _np_pairs(offsets, items, ts, created, n_items, slot_base):
+    """Pair tuples of item_cf.py:36-79 (weights.py), global slots; numpy/math."""
+    import math
+
+    offs, it, t, cr = offsets.numpy(), items.numpy(), ts.numpy(), created.numpy()
+    b = 1
+    while (1 << b) <= n_items:
+        b += 1
+    sent = (1 << (2 * b)) - 1
+    keys, slots, w = [], [], []
+    cnt = np.zeros(n_items, np.int64)
+    base = slot_base
+    for u in range(len(offs) - 1):
+        a, e = offs[u], offs[u + 1]
+        L = e - a
+        pen = 1.0 / math.log(L + 1) if L else 0.0
+        for x in it[a:e]:
+            cnt[x] += 1
+        for l1 in range(L):
+            for l2 in range(L):
+                i, j = int(it[a + l1]), int(it[a + l2])
+                if i == j:
+                    keys.append(sent)
+                    w.append(0.0)
+                else:
+                    la = 1.0 if l2 > l1 else 0.7
+                    lw = la * 0.9 ** (abs(l2 - l1) - 1)
+                    cw = math.exp(0.7 ** abs(int(t[a + l1]) - int(t[a + l2])))
+                    tw = math.exp(0.8 ** abs(cr[i] - cr[j]))
+                    keys.append((i << b) | j)
+                    w.append(lw * cw * tw * pen)
+                slots.append(base + l1 * L + l2)
+        base += L * L
+    return (torch.tensor(keys, dtype=torch.int64), torch.tensor(slots, dtype=torch.int32),
+            torch.tensor(w, dtype=torch.float64), torch.from_numpy(cnt))
+
+
+class _Entries:
+    def __init__(self, i, j, v, first):
+        self.i, self.j, self.v, self.first = i, j, v, first
+
+
+def _np_reduce(keys, slots, w, n_items, cnt):
+    """The owner's reduce: sums in (global) slot order, first slot, / sqrt(cnt_i cnt_j)."""
+    import math
+
+    b = 1
+    while (1 << b) <= n_items:
+        b += 1
+    acc = {}
+    for k, s, x in zip(keys.tolist(), slots.tolist(), w.tolist()):
+        if k == (1 << (2 * b)) - 1:
+            continue
+        if k not in acc:
+            acc[k] = [0.0, s]
+        acc[k][0] += x
+    ks = sorted(acc)
+    c = cnt.numpy()
+    i = np.array([k >> b for k in ks], np.int64)
+    j = np.array([k & ((1 << b) - 1) for k in ks], np.int64)
+    v = np.array([acc[k][0] / math.sqrt(c[a] * c[bb]) for k, a, bb in zip(ks, i, j)])
+    return _Entries(i, j, v, np.array([acc[k][1] for k in ks], np.int64))
+
+
+def _cf_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nrk.dist import itemcf_sim_sharded, shard_range
+
+        rng = np.random.default_rng(11)
+        n_users, n_items = 60, 25
+        L = rng.integers(0, 9, n_users)
+        offs = np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
+        items = rng.integers(0, n_items, offs[-1]).astype(np.int32)
+        ts = (1_500_000_000_000 + np.cumsum(rng.integers(0, 3, offs[-1]))).astype(np.int64)
+        created = rng.random(n_items)
+        lo, hi = shard_range(n_users, world, rank)
+        a, e = offs[lo], offs[hi]
+        res = itemcf_sim_sharded(torch.from_numpy(offs[lo:hi + 1] - a), torch.from_numpy(items[a:e]),
+                                 torch.from_numpy(ts[a:e]), torch.from_numpy(created), n_items,
+                                 pairs=_np_pairs, reduce=_np_reduce)
+        ilo, ihi = shard_range(n_items, world, rank)
+        assert ((res.i >= ilo) & (res.i < ihi)).all()
+        q.put((rank, res.i, res.j, res.v, res.first))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_itemcf_users_sharded_gloo(world):
+    """SURVEY 8e ItemCF: users sharded, one all_to_all by item owner + an
+    all_reduce of the click counts -> the same entries, first-encounter slots
+    and values as the single-process oracle."""
+    from oracle import oracle
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_cf_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    gi = np.concatenate([g[1] for g in got])
+    gj = np.concatenate([g[2] for g in got])
+    gv = np.concatenate([g[3] for g in got])
+    gf = np.concatenate([g[4] for g in got])
+    rng = np.random.default_rng(11)
+    n_users, n_items = 60, 25
+    L = rng.integers(0, 9, n_users)
+    offs = np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
+    items = rng.integers(0, n_items, offs[-1]).astype(np.int32)
+    ts = (1_500_000_000_000 + np.cumsum(rng.integers(0, 3, offs[-1]))).astype(np.int64)
+    created = rng.random(n_items)
+    oi, oj, ov, _, _ = oracle.itemcf_sim(offs, items, ts, created, n_items)
+    order = np.argsort(gf, kind="stable")  # first-encounter order = the oracle's
+    assert np.array_equal(gi[order], oi) and np.array_equal(gj[order], oj)
+    np.testing.assert_allclose(gv[order], ov, rtol=1e-12, atol=0)

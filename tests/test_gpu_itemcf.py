@@ -266,3 +266,47 @@ def test_itemcf_recall_full_size():
     same = (gi == oi) | ~valid
     assert same.all(axis=1).mean() > 0.9999
     np.testing.assert_allclose(np.sort(gs.cpu().numpy()[valid]), np.sort(os_[valid]), rtol=1e-11)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_itemcf_users_sharded_equals_single(world):
+    """The data path of nrk.dist.itemcf_sim_sharded on one GPU: per-rank
+    nrk_itemcf_pairs (global slots), tuples bucketed by item owner in rank
+    order, summed counts, nrk_itemcf_reduce per owner == nrk_itemcf_sim."""
+    from nrk import ops
+    from nrk.dist import shard_range
+
+    rng = np.random.default_rng(world)
+    offs, items, ts, created = _random_lists(rng, 3000, 20000, 25)
+    n_items = 20000
+    full = _gpu_sim(offs, items, ts, created, n_items)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    parts, base, cnt = [], 0, torch.zeros(n_items, dtype=torch.int64, device="cuda")
+    for r in range(world):
+        lo, hi = shard_range(len(offs) - 1, world, r)
+        a, e = offs[lo], offs[hi]
+        k, s, w, c = ops.itemcf_pairs(d(offs[lo:hi + 1] - a), d(items[a:e]), d(ts[a:e]), d(created), n_items,
+                                      slot_base=base)
+        base += int(((offs[lo + 1:hi + 1] - offs[lo:hi]) ** 2).sum())
+        parts.append((k, s, w))
+        cnt += c
+    b = 1
+    while (1 << b) <= n_items:
+        b += 1
+    per = -(-n_items // world)
+    got = []
+    for o in range(world):  # owner o receives every rank's tuples for its items, in rank order
+        ks, ss, ws_ = [], [], []
+        for k, s, w in parts:
+            m = ((k >> b) // per == o) & (k != (1 << (2 * b)) - 1)
+            ks.append(k[m]), ss.append(s[m]), ws_.append(w[m])
+        res = ops.itemcf_reduce(torch.cat(ks), torch.cat(ss), torch.cat(ws_), n_items, cnt)
+        got.append(res)
+    gi = torch.cat([g.i for g in got]).cpu().numpy()
+    gj = torch.cat([g.j for g in got]).cpu().numpy()
+    gv = torch.cat([g.v for g in got]).cpu().numpy()
+    gf = torch.cat([g.first for g in got]).cpu().numpy()
+    assert np.array_equal(gi, full.i.cpu().numpy()) and np.array_equal(gj, full.j.cpu().numpy())
+    assert np.array_equal(gf, full.first.cpu().numpy())
+    np.testing.assert_allclose(gv, full.v.cpu().numpy(), rtol=1e-12, atol=0)
+    assert np.array_equal(cnt.cpu().numpy(), full.cnt.cpu().numpy())
