@@ -7,18 +7,21 @@
 //
 // Dice normalises with the BATCH mean and unbiased std of every column
 // (DIN.py:39-44), so each Dice splits the forward into phases with a
-// batch-wide reduction in between:
+// batch-wide reduction in between.  One call scores every Dice batch of a
+// pass (segments of S samples), one launch per phase:
 //   1. din_att_h      h[b,t,:] = (Wk - Wd) k_t + (Wq + Wd) q + Wp (q .* k_t) + b0
 //                     (= Linear(512->36) on [k, q, q-k, q.*k], DIN.py:105-114,
 //                     with the batch-invariant parts folded by nrk_din_prepare);
 //                     per-block fp64 column sums of h and h^2.
 //   2. col_stats      mean / unbiased std per (t, j) (deterministic, fixed order).
-//   3. din_att_out    Dice -> Linear(36->1) -> * mask (no softmax, :117-124),
-//                     weighted history sum (:276), assemble the MLP input
-//                     [user, ctx, cand, wh] (:279-281).
-//   4. din_gemm       Linear(928->h1) (+ column sums), 5. col_stats,
-//   6. din_gemm       Dice-on-load -> Linear(h1->h2) (+ column sums), 7. col_stats,
+//   3. din_wh         Dice -> Linear(36->1) -> * mask (no softmax, :117-124),
+//                     weighted history sum wh (:276).
+//   4. din_mlp1       Linear(928->h1) on [user, ctx, cand, wh] (:279-282), the
+//                     embedding parts gathered straight from the table; 5. col_stats,
+//   6. din_mlp2       Dice-on-load -> Linear(h1->h2); 7. col_stats,
 //   8. din_head       Dice -> Linear(h2->1) -> sigmoid (:282-284).
+// The general path (T > 64 or h1 > 256) assembles the MLP input with
+// din_att_out and runs the f32 MFMA din_gemm instead of 3, 4 and 6.
 #include "nrk_common.h"
 
 namespace nrk {
