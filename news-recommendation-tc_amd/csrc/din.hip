@@ -1106,11 +1106,12 @@ __global__ void din_prepare_kernel(const float* __restrict__ w0, int ID, float* 
 }
 
 // ------------------------------------------------------------- workspace --
-// din_att_h workgroups per segment: about 2048 in the whole grid (8 per CU),
-// at most 512 per segment and never more than the segment has samples
+// din_att_h workgroups per segment: about 6144 in the whole grid (24 per CU,
+// measured best of 1024...32768 at config 3), at most 512 per segment and
+// never more than the segment has samples
 static inline int din_att_groups(int64_t N, int64_t S) {
     const int64_t n_seg = (N + S - 1) / S;
-    int64_t g = (2048 + n_seg - 1) / n_seg;
+    int64_t g = (6144 + n_seg - 1) / n_seg;
     g = g < 8 ? 8 : g > 512 ? 512 : g;
     return (int)(g < S ? g : S);
 }
