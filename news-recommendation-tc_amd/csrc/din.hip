@@ -35,6 +35,10 @@ template <>
 __device__ __forceinline__ float tload<float>(const float* p) { return *p; }
 template <>
 __device__ __forceinline__ float tload<uint16_t>(const uint16_t* p) { return bf16_to_f32(*p); }
+// raw element bits (fp32 bits, or bf16 bits in the low half), for loads whose
+// conversion is deferred to the use
+__device__ __forceinline__ uint32_t table_bits(const float* p) { return __float_as_uint(*p); }
+__device__ __forceinline__ uint32_t table_bits(const uint16_t* p) { return *p; }
 
 // Dice (DIN.py:39-44), fp32 in the reference's operation order.
 __device__ __forceinline__ float dice(float x, float mean, float std) {
@@ -171,6 +175,15 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
     // previous sample's M_b build, MFMAs and epilogue
     constexpr int RW = F32 ? 2 : 1;  // 16-B pieces per lane per k row
     typedef uint32_t u4n __attribute__((ext_vector_type(4)));
+    // row bases hoisted out of the loop, and q kept as raw bits until use: a
+    // gather whose address or conversion depends on another load in flight
+    // makes the compiler wait vmcnt(0), draining the prefetched rows with it
+    int64_t rbs[NI];
+#pragma unroll
+    for (int s = 0; s < NI; ++s) rbs[s] = row_base[n_user + s];
+    const int64_t qbase = tid < ID ? row_base[n_user + tid / DIN_E] : 0;
+    const float b0j = (tid >> 2) < DIN_H ? att_b0[tid >> 2] : 0.0f;
+    auto q_of = [&](uint32_t bits) { return F32 ? __uint_as_float(bits) : __uint_as_float(bits << 16); };
     auto idx_of = [&](int64_t bb, int32_t (&hi)[NTW][NI], int32_t& qi) {
 #pragma unroll
         for (int a = 0; a < NTW; ++a) {
@@ -180,7 +193,7 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
         }
         qi = (bb < b_end && tid < ID) ? item_idx[bb * NI + tid / DIN_E] : -1;
     };
-    auto rows_of = [&](const int32_t (&hi)[NTW][NI], int32_t qi, u4n (&raw)[NTW][NI][RW], float& qv) {
+    auto rows_of = [&](const int32_t (&hi)[NTW][NI], int32_t qi, u4n (&raw)[NTW][NI][RW], uint32_t& qv) {
 #pragma unroll
         for (int a = 0; a < NTW; ++a)
 #pragma unroll
@@ -189,16 +202,16 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
                 for (int w = 0; w < RW; ++w) raw[a][s][w] = u4n{0u, 0u, 0u, 0u};
                 if (hi[a][s] >= 0) {
                     const u4n* p = reinterpret_cast<const u4n*>(
-                        table + (row_base[n_user + s] + hi[a][s]) * DIN_E + 8 * (lane >> 4));
+                        table + (rbs[s] + hi[a][s]) * DIN_E + 8 * (lane >> 4));
 #pragma unroll
                     for (int w = 0; w < RW; ++w) raw[a][s][w] = p[w];
                 }
             }
-        qv = qi >= 0 ? tload(table + (row_base[n_user + tid / DIN_E] + qi) * DIN_E + tid % DIN_E) : 0.0f;
+        qv = qi >= 0 ? (uint32_t)table_bits(table + (qbase + qi) * DIN_E + tid % DIN_E) : 0u;
     };
     int32_t nidx[NTW][NI], nqi;
     u4n raw[NTW][NI][RW];
-    float qv;
+    uint32_t qv;
     {
         int32_t i0[NTW][NI], q0;
         idx_of(seg * S + blockIdx.x % G, i0, q0);
@@ -207,7 +220,7 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
     }
     for (int64_t b = seg * S + blockIdx.x % G; b < b_end; b += G) {
         u4n nraw[NTW][NI][RW];
-        float nqv;
+        uint32_t nqv;
         rows_of(nidx, nqi, nraw, nqv);   // rows of sample b + G
         idx_of(b + 2 * G, nidx, nqi);    // indices of sample b + 2G
         // (1) this wave's k rows -> A fragments
@@ -233,7 +246,7 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
                 split8(v, sc.s_k, ahi[a][s], alo[a][s]);
             }
         // (2) query embedding
-        if (tid < ID) qs[tid] = qv;
+        if (tid < ID) qs[tid] = q_of(qv);
 #pragma unroll
         for (int a = 0; a < NTW; ++a)
 #pragma unroll
@@ -266,7 +279,7 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
             c += __shfl_xor(c, 1, WAVE);
             c += __shfl_xor(c, 2, WAVE);
             const int j = tid >> 2;
-            if ((tid & 3) == 0 && j < DIN_H) cs[j] = c + att_b0[j];
+            if ((tid & 3) == 0 && j < DIN_H) cs[j] = c + b0j;
         }
         lds_barrier();
         // (4) MFMAs + epilogue
@@ -480,7 +493,7 @@ __device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
     return p * x + ((1.0f - p) * 0.01f) * x;
 }
 
-template <typename TT, int NI>
+template <typename TT, int NI, int NCH>
 __global__ __launch_bounds__(256) void din_wh_kernel(
     const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
     const int32_t* __restrict__ hist_idx, const float* __restrict__ mask, int64_t B, int64_t S,
@@ -489,12 +502,31 @@ __global__ __launch_bounds__(256) void din_wh_kernel(
     unsigned int* __restrict__ segmax) {
     constexpr int ID = NI * DIN_E;
     typedef float f4n __attribute__((ext_vector_type(4)));
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    typedef uint32_t u4n __attribute__((ext_vector_type(4)));
+    // gather layout: 16-B pieces of EPP elements, PPR pieces per row; lane =
+    // tg * LPT + f * PPR + c gathers piece c of feature f for slots
+    // t = tg, tg + TG, ... (a round's R loads in flight at once), and the TG
+    // partial sums are combined by an xor tree
+    constexpr int EPP = 16 / (int)sizeof(TT);
+    constexpr int PPR = DIN_E / EPP;
+    constexpr int LPT = NI * PPR;
+    constexpr int TG = 64 / LPT;
+    constexpr int R = 64 / TG < 8 ? 64 / TG : 8;
+    constexpr int HQ = DIN_H / 4;                      // 4-column chunks per h row
+    __shared__ __attribute__((aligned(16))) float dsc[4][64 * DIN_H];  // Dice(h) of the sample
+    __shared__ int32_t rr_s[4][64 * NI];
+    __shared__ float w_s[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int tg = lane / LPT, gf = (lane / PPR) % NI, gc = lane % PPR;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
     const int64_t b0 = wave * per_wave;
     const int64_t b1e = b0 + per_wave < B ? b0 + per_wave : B;
     const float ab1 = att_b1[0];
     const bool act = lane < T;
+    const int nq = T * HQ;
+    int64_t rbs[NI];
+#pragma unroll
+    for (int f = 0; f < NI; ++f) rbs[f] = row_base[n_user + f];
     int64_t cur = -1;
     float mx = 0.0f;
     auto flush = [&]() {
@@ -503,96 +535,122 @@ __global__ __launch_bounds__(256) void din_wh_kernel(
         for (int k = 32; k > 0; k >>= 1) m = fmaxf(m, __shfl_xor(m, k, WAVE));
         if (lane == 0 && cur >= 0) atomicMax(segmax + cur, __float_as_uint(m));
     };
-    // this lane's h row, history indices and mask of sample bb (prefetched one sample ahead)
-    auto fetch = [&](int64_t bb, f4n (&hv)[DIN_H / 4], int32_t (&ix)[NI], float& mk) {
-        if (act && bb < b1e) {
-            const f4n* hr = reinterpret_cast<const f4n*>(h + ((size_t)bb * T + lane) * DIN_H);
-#pragma unroll
-            for (int c = 0; c < DIN_H / 4; ++c) hv[c] = hr[c];
-#pragma unroll
-            for (int f = 0; f < NI; ++f) ix[f] = hist_idx[((size_t)bb * T + lane) * NI + f];
-            mk = mask[bb * T + lane];
-        } else {
-#pragma unroll
-            for (int c = 0; c < DIN_H / 4; ++c) hv[c] = f4n{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int f = 0; f < NI; ++f) ix[f] = 0;
-            mk = 0.0f;
-        }
-    };
-    f4n hv[DIN_H / 4];
+    // sample bb's h block [T x DIN_H] read as consecutive 16-B chunks (chunk
+    // q = 64 i + lane: one coalesced 1-KB load per i), plus lane t's history
+    // indices and mask
+    f4n hq[NCH];
     int32_t ix[NI];
     float mk;
-    fetch(b0, hv, ix, mk);
+    auto fetch = [&](int64_t bb) {
+        const bool ok = bb < b1e;
+        const f4n* hr = reinterpret_cast<const f4n*>(h + (size_t)(ok ? bb : 0) * T * DIN_H);
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int q = 64 * i + lane;
+            hq[i] = ok && q < nq ? hr[q] : f4n{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int f = 0; f < NI; ++f) ix[f] = ok && act ? hist_idx[((size_t)bb * T + lane) * NI + f] : 0;
+        mk = ok && act ? mask[bb * T + lane] : 0.0f;
+    };
+    // this segment's Dice statistics for the same chunks, kept in registers
+    f4n sm[NCH], si[NCH];
+    auto stats = [&](int64_t seg) {
+        const f4n* st = reinterpret_cast<const f4n*>(hinv_all + (size_t)seg * T * DIN_H);
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int q = 64 * i + lane;
+            const f4n s0 = q < nq ? st[2 * q] : f4n{0.0f, 1.0f, 0.0f, 1.0f};
+            const f4n s1 = q < nq ? st[2 * q + 1] : f4n{0.0f, 1.0f, 0.0f, 1.0f};
+            sm[i] = f4n{s0.x, s0.z, s1.x, s1.z};
+            si[i] = f4n{s0.y, s0.w, s1.y, s1.w};
+        }
+    };
+    fetch(b0);
     for (int64_t b = b0; b < b1e; ++b) {
         const int64_t seg = b / S;
         if (seg != cur) {
             flush();
             cur = seg;
             mx = 0.0f;
+            stats(seg);
         }
-        f4n nhv[DIN_H / 4];
-        int32_t nix[NI];
-        float nmk;
-        fetch(b + 1, nhv, nix, nmk);
-        float w = 0.0f;
-        int32_t rr[NI];
+        // Dice of every h element, chunk-parallel, staged in LDS; lane t then
+        // forms w_t = (sum_j w1_j Dice(h_tj) + b1) * mask_t over j ascending
 #pragma unroll
-        for (int f = 0; f < NI; ++f) rr[f] = 0;
+        for (int i = 0; i < NCH; ++i) {
+            const int q = 64 * i + lane;
+            if (q < nq) {
+                f4n d;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) d[e] = dice_fast(hq[i][e], sm[i][e], si[i][e]);
+                *reinterpret_cast<f4n*>(&dsc[wv][4 * q]) = d;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float w = 0.0f;
         if (act) {
-            const f4n* st = reinterpret_cast<const f4n*>(hinv_all + ((size_t)seg * T + lane) * DIN_H);
+            const f4n* dr = reinterpret_cast<const f4n*>(&dsc[wv][lane * DIN_H]);
             float sacc = 0.0f;
 #pragma unroll
-            for (int c = 0; c < DIN_H / 4; ++c) {
-                const f4n s0 = st[2 * c], s1 = st[2 * c + 1];
-                const float ms[4] = {s0.x, s0.z, s1.x, s1.z};
-                const float iv[4] = {s0.y, s0.w, s1.y, s1.w};
+            for (int c = 0; c < HQ; ++c) {
+                const f4n d = dr[c];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) sacc += att_w1[4 * c + e] * dice_fast(hv[c][e], ms[e], iv[e]);
+                for (int e = 0; e < 4; ++e) sacc += att_w1[4 * c + e] * d[e];
             }
             w = (sacc + ab1) * mk;
-#pragma unroll
-            for (int f = 0; f < NI; ++f) rr[f] = (int32_t)(row_base[n_user + f] + ix[f]);
         }
+        w_s[wv][lane] = w;
+#pragma unroll
+        for (int f = 0; f < NI; ++f) rr_s[wv][lane * NI + f] = act ? (int32_t)(rbs[f] + ix[f]) : 0;
         const uint64_t nz = __builtin_amdgcn_ballot_w64(w != 0.0f);
         const int te = nz ? 64 - __builtin_clzll(nz) : 0;
-        const int e = lane & 31, fo = lane >> 5;  // o1 = lane -> feature fo, o2 = lane + 64 -> 2 + fo
-        float s1 = 0.0f, s2 = 0.0f;
-        // 8 slots per round: all 16 gathers issued before the (in-order) adds;
-        // slots >= te carry weight +0 on row of lane 63's slot (adds exactly +0)
-        for (int t0 = 0; t0 < te; t0 += 8) {
-            float wt[8], v1[8], v2[8];
+        asm volatile("" ::: "memory");
+        fetch(b + 1);  // next sample, in flight during the gathers
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float acc[EPP];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int t = (t0 + u) & 63;
-                wt[u] = t0 + u < te ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t)) : 0.0f;
-                int32_t r[NI];
+        for (int e = 0; e < EPP; ++e) acc[e] = 0.0f;
+        for (int t0 = 0; t0 < te; t0 += TG * R) {
+            u4n raw[R];
+            float wt[R];
 #pragma unroll
-                for (int f = 0; f < NI; ++f) r[f] = __builtin_amdgcn_readlane(rr[f], t);
-                if constexpr (NI == 1) {
-                    v1[u] = tload(table + (int64_t)r[0] * DIN_E + e);
-                    v2[u] = 0.0f;
+            for (int u = 0; u < R; ++u) {
+                const int t = t0 + TG * u + tg;
+                const int tc = t < te ? t : te - 1;  // past te: weight +0 on a valid row
+                wt[u] = t < te ? w_s[wv][tc] : 0.0f;
+                const int32_t r = rr_s[wv][tc * NI + gf];
+                raw[u] = *reinterpret_cast<const u4n*>(table + (int64_t)r * DIN_E + gc * EPP);
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                if constexpr (sizeof(TT) == 4) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[e] = fmaf(wt[u], __uint_as_float(raw[u][e]), acc[e]);
                 } else {
-                    v1[u] = tload(table + (int64_t)(fo ? r[1] : r[0]) * DIN_E + e);
-                    v2[u] = NI == 4 ? tload(table + (int64_t)(fo ? r[NI - 1] : r[NI / 2]) * DIN_E + e) : 0.0f;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc[2 * i] = fmaf(wt[u], __uint_as_float(raw[u][i] << 16), acc[2 * i]);
+                        acc[2 * i + 1] = fmaf(wt[u], __uint_as_float(raw[u][i] & 0xFFFF0000u), acc[2 * i + 1]);
+                    }
                 }
             }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                s1 += wt[u] * v1[u];
-                s2 += wt[u] * v2[u];
-            }
         }
-        if (NI == 1 && lane >= 32) s1 = 0.0f;
-        float* o = wh + (size_t)b * ID;
-        if (lane < ID) o[lane] = s1;
-        if (lane + 64 < ID) o[lane + 64] = s2;
-        mx = fmaxf(mx, fmaxf(lane < ID ? fabsf(s1) : 0.0f, lane + 64 < ID ? fabsf(s2) : 0.0f));
 #pragma unroll
-        for (int c = 0; c < DIN_H / 4; ++c) hv[c] = nhv[c];
+        for (int off = LPT; off < 64; off <<= 1)
 #pragma unroll
-        for (int f = 0; f < NI; ++f) ix[f] = nix[f];
-        mk = nmk;
+            for (int e = 0; e < EPP; ++e) acc[e] += __shfl_xor(acc[e], off, WAVE);
+        if (tg == 0) {
+            f4n* o = reinterpret_cast<f4n*>(wh + (size_t)b * ID + gf * DIN_E + gc * EPP);
+#pragma unroll
+            for (int v = 0; v < EPP / 4; ++v) o[v] = f4n{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
+        }
+#pragma unroll
+        for (int e = 0; e < EPP; ++e) mx = fmaxf(mx, fabsf(acc[e]));
     }
     flush();
 }
@@ -1309,16 +1367,22 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         const int64_t waves = std::min<int64_t>(batch, 32768);
         const int64_t per_wave = (batch + waves - 1) / waves;
         const unsigned gw = (unsigned)((((batch + per_wave - 1) / per_wave) + 3) / 4);
+        const int nch = (T * (DIN_H / 4) + 63) / 64;
+#define NRK_WH_K(TT, NI, NCH)                                                                                \
+    din_wh_kernel<TT, NI, NCH><<<gw, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,      \
+                                                  hist_idx, mask, batch, S, T, per_wave, w.h, w.hinv,      \
+                                                  att_w1, att_b1, w.wh, w.whmax)
 #define NRK_WH(TT, NI)                                                                                  \
-    din_wh_kernel<TT, NI><<<gw, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,      \
-                                             hist_idx, mask, batch, S, T, per_wave, w.h, w.hinv,      \
-                                             att_w1, att_b1, w.wh, w.whmax)
+    do {                                                                                                \
+        if (nch <= 4) NRK_WH_K(TT, NI, 4); else if (nch <= 8) NRK_WH_K(TT, NI, 8); else NRK_WH_K(TT, NI, 9); \
+    } while (0)
         if (table_dtype == 0) {
             if (n_item == 4) NRK_WH(float, 4); else if (n_item == 2) NRK_WH(float, 2); else NRK_WH(float, 1);
         } else {
             if (n_item == 4) NRK_WH(uint16_t, 4); else if (n_item == 2) NRK_WH(uint16_t, 2); else NRK_WH(uint16_t, 1);
         }
 #undef NRK_WH
+#undef NRK_WH_K
         const unsigned gm = (unsigned)((batch + MLP1_ROWS - 1) / MLP1_ROWS);
 #define NRK_MLP1(TT, NTV)                                                                                 \
     din_mlp1_kernel<TT, NTV><<<gm, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,     \
