@@ -794,34 +794,35 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
     const float s_w = pow2_scale(__uint_as_float(*w1max));
     const float s_h = pow2_scale(__uint_as_float(wh_segmax[seg]));
 
-    auto idx_load = [&](int s, int a) -> int32_t {
-        if (!mok[a] || s >= KE) return 0;
-        const int64_t m = mrow[a];
-        if (s < n_user) return user_idx[m * n_user + s];
-        if (s < n_user + n_ctx) return ctx_idx[m * n_ctx + (s - n_user)];
-        return item_idx[m * n_item + (s - n_user - n_ctx)];
-    };
-    auto data_load = [&](int s, int a, int32_t idx, uint32_t (&raw)[8]) {
+    // Loads are unconditional, from a clamped row and a pointer chosen by the
+    // (uniform) k-step: a value merged from a conditional load forces a
+    // vmcnt(0) at the merge, draining the prefetches in flight.  Rows past M
+    // are zeroed at use.
+    int64_t mrc[2];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) raw[e] = 0u;
-        if (!mok[a]) return;
+    for (int a = 0; a < 2; ++a) mrc[a] = mok[a] ? mrow[a] : M - 1;
+    auto idx_load = [&](int s, int a) -> int32_t {
+        const int64_t m = mrc[a];
+        const int32_t* ip = s < n_user ? user_idx + m * n_user + s
+                            : s < n_user + n_ctx ? ctx_idx + m * n_ctx + (s - n_user)
+                            : s < KE ? item_idx + m * n_item + (s - n_user - n_ctx)
+                                     : item_idx + m * n_item;  // unused (wh k-step)
+        return *ip;
+    };
+    auto data_load = [&](int s, int a, int32_t idx, din_u4 (&raw)[2]) {
+        const din_u4* p;
         if (s >= KE) {
-            const uint4* p = reinterpret_cast<const uint4*>(wh + mrow[a] * ID + (s - KE) * DIN_E + 8 * q);
-            const uint4 x = p[0], y = p[1];
-            raw[0] = x.x; raw[1] = x.y; raw[2] = x.z; raw[3] = x.w;
-            raw[4] = y.x; raw[5] = y.y; raw[6] = y.z; raw[7] = y.w;
-            return;
+            p = reinterpret_cast<const din_u4*>(wh + mrc[a] * ID + (s - KE) * DIN_E + 8 * q);
+        } else {
+            const int64_t base = s < n_user ? row_base[s]
+                                 : s < n_user + n_ctx ? row_base[n_user + n_item + (s - n_user)]
+                                                      : row_base[n_user + (s - n_user - n_ctx)];
+            p = reinterpret_cast<const din_u4*>(table + (base + idx) * DIN_E + 8 * q);
         }
-        const int64_t base = s < n_user ? row_base[s]
-                             : s < n_user + n_ctx ? row_base[n_user + n_item + (s - n_user)]
-                                                  : row_base[n_user + (s - n_user - n_ctx)];
-        const uint4* p = reinterpret_cast<const uint4*>(table + (base + idx) * DIN_E + 8 * q);
-        const uint4 x = p[0];
-        raw[0] = x.x; raw[1] = x.y; raw[2] = x.z; raw[3] = x.w;
-        if (F32) {
-            const uint4 y = p[1];
-            raw[4] = y.x; raw[5] = y.y; raw[6] = y.z; raw[7] = y.w;
-        }
+        // the second piece is read always (a bf16 table row re-reads the
+        // first: the row may be the table's last), so no load is conditional
+        raw[0] = p[0];
+        raw[1] = p[(F32 || s >= KE) ? 1 : 0];
     };
     din_u4 stg[CPT];
     din_f4 acc[2][NT];
@@ -830,7 +831,7 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[a][j] = din_f4{0.0f, 0.0f, 0.0f, 0.0f};
 
-    uint32_t raw[2][8], nraw[2][8];
+    din_u4 raw[2][2], nraw[2][2];
     int32_t idx1[2], idx2[2];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
@@ -848,7 +849,7 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
         for (int a = 0; a < 2; ++a) {
             if (s + 1 < KS) data_load(s + 1, a, idx1[a], nraw[a]);
             idx1[a] = idx2[a];
-            idx2[a] = s + 3 < KS ? idx_load(s + 3, a) : 0;
+            idx2[a] = idx_load(s + 3 < KS ? s + 3 : KS - 1, a);
         }
         if (s == KE) {
             const float r = s_h / s_k;  // exact: both are powers of two
@@ -865,14 +866,16 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
             float v[8];
             if (F32 || s >= KE) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(raw[a][e]);
+                for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(raw[a][e >> 2][e & 3]);
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    v[2 * i] = __uint_as_float(raw[a][i] << 16);
-                    v[2 * i + 1] = __uint_as_float(raw[a][i] & 0xFFFF0000u);
+                    v[2 * i] = __uint_as_float(raw[a][0][i] << 16);
+                    v[2 * i + 1] = __uint_as_float(raw[a][0][i] & 0xFFFF0000u);
                 }
             }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = mok[a] ? v[e] : 0.0f;
             split8(v, sc, ahi[a], alo[a]);
         }
         const din_half8* wb = reinterpret_cast<const din_half8*>(wr[s & 1]);
@@ -890,9 +893,10 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
         if (s + 1 < KS) stage_store<CPT, CH>(stg, wr[(s + 1) & 1], tid);
         lds_barrier();
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) raw[a][e] = nraw[a][e];
+        for (int a = 0; a < 2; ++a) {
+            raw[a][0] = nraw[a][0];
+            raw[a][1] = nraw[a][1];
+        }
     }
     // epilogue: scale, bias, store, per-64-row-half fp64 column sums, max |z1|
     lds_barrier();  // (every wave is past its last read of wr)
