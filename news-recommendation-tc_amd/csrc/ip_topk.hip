@@ -582,50 +582,98 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         }
     }
     int cnt = 0;
-    for (int base = 0; base < nitem; base += WAVE) {
-        const int idx = base + lane;
-        bool keep = false;
-        double s = 0.0;
-        int32_t row = 0;
-        if (idx < nitem) {
-            const int b = idx >> 4, r = idx & 15;
-            const uint32_t q = (b < n0) ? cand[(2 * u) * IP_CW + b].y : cand[(2 * u + 1) * IP_CW + (b - n0)].y;
-            const int64_t rr = (int64_t)(q >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (q & 1);
-            if (rr < n_items) row = (int32_t)rr;
-            keep = rr < n_items;
-            if constexpr (DS4 > 0) {
-                if (pre && keep) {
-                    const int blk = (int)(rr >> 5), il = (int)(rr & 31);
-                    const uint8_t* bp = catalog + (size_t)blk * (64 * 4 * DS4);
-                    float acc = 0.0f;
+    auto push = [&](bool keep, double s, int32_t row) {
+        const unsigned long long bal = __ballot(keep);
+        const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+        if (keep && pos < IP_SURV) surv[wave][pos] = Cand{s, row};
+        cnt += __popcll(bal);
+    };
+    if constexpr (DS4 > 0) {
+        // Software pipeline over 64-item rounds.  Round i issues, in this
+        // order: the fp32 rows of its kept items, the packed fp16 pieces of
+        // round i+1, the band entries of round i+2.  vmcnt retires in issue
+        // order, so waiting for round i's rows does not wait for round i+1's
+        // pieces, which stay in flight across round i's exact dot products.
+        uint4 pc[DSK > 0 ? 2 * DSK : 1];
+        auto band_q = [&](int base) -> uint32_t {
+            int idx = base + lane;
+            idx = idx < nitem ? idx : nitem - 1;
+            const int bb = idx >> 4;
+            const uint2* cp = bb < n0 ? cand + (size_t)(2 * u) * IP_CW + bb
+                                      : cand + (size_t)(2 * u + 1) * IP_CW + (bb - n0);
+            return cp->y;
+        };
+        auto item_row = [&](int base, uint32_t qv, int32_t& row, bool& inb) {
+            const int idx = base + lane, r = idx & 15;
+            const int64_t rr = (int64_t)(qv >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (qv & 1);
+            inb = idx < nitem && rr < n_items;
+            row = inb ? (int32_t)rr : 0;
+        };
+        auto pieces = [&](int32_t row) {
+            if (pre) {
+                const int blk = row >> 5, il = row & 31;
+                const uint8_t* bp = catalog + (size_t)blk * (64 * 4 * DS4);
 #pragma unroll
-                    for (int st = 0; st < DSK; ++st)
+                for (int st = 0; st < DSK; ++st)
 #pragma unroll
-                        for (int hh = 0; hh < 2; ++hh) {
-                            const uint4 pc = *reinterpret_cast<const uint4*>(bp + st * 1024 + (il + 32 * hh) * 16);
-                            const f16x8 hv = __builtin_bit_cast(f16x8, pc);
-#pragma unroll
-                            for (int e = 0; e < 8; ++e)
-                                acc = fmaf((float)hv[e], ush[16 * st + 8 * hh + e], acc);
-                        }
-                    keep = acc >= pcut;
-                }
+                    for (int hh = 0; hh < 2; ++hh)
+                        pc[2 * st + hh] = *reinterpret_cast<const uint4*>(bp + st * 1024 + (il + 32 * hh) * 16);
             }
-        }
-        if constexpr (DS4 > 0) {
-            // coalesced staging of this round's 64 rows
+        };
+        int32_t row;
+        bool inb;
+        item_row(0, band_q(0), row, inb);
+        pieces(row);
+        uint32_t q1 = band_q(WAVE < nitem ? WAVE : 0);
+        for (int base = 0; base < nitem; base += WAVE) {
+            // (1) fp16 prefilter of this round: every band item's scaled fp16
+            // score from its 64-B packed row, kept when it reaches the cut
+            // (|fp16 score - exact| <= eps as in the screen)
+            bool keep = inb;
+            if (pre && inb) {
+                float acc = 0.0f;
+#pragma unroll
+                for (int st = 0; st < DSK; ++st)
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const f16x8 hv = __builtin_bit_cast(f16x8, pc[2 * st + hh]);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            acc = fmaf((float)hv[e], ush[16 * st + 8 * hh + e], acc);
+                    }
+                keep = acc >= pcut;
+            }
+            // (2) this round's kept fp32 rows, whole-row coalesced float4
+            // pieces (64 / DS4 rows per instruction), unconditional loads
+            float4 v[DS4];
+            bool okv[DS4];
 #pragma unroll
             for (int it = 0; it < DS4; ++it) {
                 const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
                 const int r_item = __shfl(row, item, WAVE);
-                const bool ok_item = __shfl((int)keep, item, WAVE) != 0;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (ok_item) v = reinterpret_cast<const float4*>(items + (int64_t)r_item * dim)[part];
-                stage[wave][item * RS + part] = v;
+                okv[it] = __shfl((int)keep, item, WAVE) != 0;
+                v[it] = reinterpret_cast<const float4*>(items + (int64_t)r_item * dim)[part];
+            }
+            const int32_t row_cur = row;
+            // (3) next round's rows and packed pieces, then the band entries
+            // of the round after it
+            const int nb = base + WAVE;
+            if (nb < nitem) {
+                item_row(nb, q1, row, inb);
+                pieces(row);
+                q1 = band_q(nb + WAVE < nitem ? nb + WAVE : nb);
+            }
+            // (4) stage, then each lane sums its own row sequentially (the
+            // oracle's order)
+#pragma unroll
+            for (int it = 0; it < DS4; ++it) {
+                const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
+                stage[wave][item * RS + part] = okv[it] ? v[it] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double sd = 0.0;
             if (keep) {
                 const float4* a4 = reinterpret_cast<const float4*>(uv);
                 const float4* b4 = &stage[wave][lane * RS];
@@ -638,20 +686,31 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
                     acc += (double)x.z * (double)y.z;
                     acc += (double)x.w * (double)y.w;
                 }
-                s = acc + 0.0;
-                keep = s >= thr;
+                sd = acc + 0.0;
+                keep = sd >= thr;
             }
             __builtin_amdgcn_wave_barrier();  // the stage is rewritten next round
-        } else {
-            if (keep) {
-                s = exact_dot(uv, items + (int64_t)row * dim, dim);
-                keep = s >= thr;
-            }
+            push(keep, sd, row_cur);
         }
-        const unsigned long long bal = __ballot(keep);
-        const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
-        if (keep && pos < IP_SURV) surv[wave][pos] = Cand{s, row};
-        cnt += __popcll(bal);
+    } else {
+        for (int base = 0; base < nitem; base += WAVE) {
+            const int idx = base + lane;
+            bool keep = false;
+            double sd = 0.0;
+            int32_t row = 0;
+            if (idx < nitem) {
+                const int bb = idx >> 4, r = idx & 15;
+                const uint32_t q = (bb < n0) ? cand[(2 * u) * IP_CW + bb].y : cand[(2 * u + 1) * IP_CW + (bb - n0)].y;
+                const int64_t rr = (int64_t)(q >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (q & 1);
+                if (rr < n_items) row = (int32_t)rr;
+                keep = rr < n_items;
+                if (keep) {
+                    sd = exact_dot(uv, items + (int64_t)row * dim, dim);
+                    keep = sd >= thr;
+                }
+            }
+            push(keep, sd, row);
+        }
     }
     if (cnt > IP_SURV) {  // dense exact ties: hand the user to the exact fallback
         if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
