@@ -652,7 +652,8 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
                 const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
                 const int r_item = __shfl(row, item, WAVE);
                 okv[it] = __shfl((int)keep, item, WAVE) != 0;
-                v[it] = reinterpret_cast<const float4*>(items + (int64_t)r_item * dim)[part];
+                // dropped items read row 0 (one shared line) instead of their own
+                v[it] = reinterpret_cast<const float4*>(items + (int64_t)(okv[it] ? r_item : 0) * dim)[part];
             }
             const int32_t row_cur = row;
             // (3) next round's rows and packed pieces, then the band entries
