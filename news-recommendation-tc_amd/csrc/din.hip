@@ -477,15 +477,19 @@ __global__ __launch_bounds__(256) void din_att_out_kernel(
 // ----------------------------------------------------- 3'. att wh (fast) --
 // Fast path (T <= 64, h1 <= 256): only the weighted history sum wh [B, ID]
 // is materialised -- GEMM1 (din_mlp1_kernel) gathers the user / context /
-// candidate embeddings itself.  One wave per sample: lane t < T reduces its
-// Dice row of h (w_t = (sum_j w1_j Dice(h_tj) + b1) * mask_t, DIN.py:117-124)
-// and holds the table rows of history slot t; lane l then forms wh[o] for
-// o = l, l + 64 (< ID) over t ascending (:276), w_t and the rows broadcast by
-// readlane.  Slots after the last nonzero weight add exactly +0 and are
-// skipped.  Dice here uses the hardware exp / reciprocal (~1 ulp each; the
-// parity bar is 1e-5), with (mean, 1 / (std + 1e-8)) per column from
-// col_stats.  The next sample's h row, indices and mask are loaded while the
-// current one is reduced.  Each wave owns a contiguous run of samples and
+// candidate embeddings itself.  One wave per sample.  The sample's h block
+// [T x 36] is read as consecutive 16-B chunks (one coalesced 1-KB load per
+// 64 chunks; a lane-per-row read touches 64 cache lines per instruction) and
+// Dice'd against the batch statistics of the same chunks, held in registers
+// per Dice batch; lane t < T then reduces w_t = (sum_j w1_j Dice(h_tj) + b1)
+// * mask_t over j ascending from LDS (DIN.py:117-124).  wh = sum_t w_t k_t
+// (:276): every lane gathers 16-B pieces of history rows for slots t = tg,
+// tg + TG, ... (a round's loads in flight together) and the slot groups are
+// combined by an xor tree; slots after the last nonzero weight add exactly
+// +0 and are skipped.  Dice uses the hardware exp / reciprocal (~1 ulp each;
+// the parity bar is 1e-5), (mean, 1 / (std + 1e-8)) per column from
+// col_stats.  The next sample's h block, indices and mask are in flight
+// during the gathers.  Each wave owns a contiguous run of samples and
 // publishes max |wh| per Dice batch (atomicMax on the float bits) for
 // GEMM1's fp16 scale.
 __device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
