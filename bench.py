@@ -419,8 +419,8 @@ def main():
                     help="N>1 layout: users-sharded (weak scaling, no collective) or "
                          "catalog-sharded (BASELINE config 4: all_to_all of shard top-k + merge)")
     ap.add_argument("--din-samples", type=int, default=DIN_SAMPLES)
-    ap.add_argument("--din-steps", type=int, default=3)
-    ap.add_argument("--din-warmup", type=int, default=1)
+    ap.add_argument("--din-steps", type=int, default=10)
+    ap.add_argument("--din-warmup", type=int, default=2)
     ap.add_argument("--din-cpu-sample", type=int, default=4096)
     args = ap.parse_args()
 
