@@ -593,16 +593,25 @@ __global__ __launch_bounds__(256) void rc_cand_kernel(
         if (sl < 0) continue;
         const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
         int64_t c = cand_off[q];
+        // history of <= 64 clicks held one per lane: the in-history test is
+        // then L shuffles instead of L dependent global loads per neighbour
+        const int32_t hl = lane < L ? items[b + lane] : -1;
         for (int64_t loc = 0; loc < L; ++loc) {
             const int32_t i = items[b + loc];
             const int n = nbr_cnt[i];
             // position_weight(len(hist) - loc) (:92-95)
             const double lw = pow(prm.loc_beta, (double)(L - loc));
-            for (int x = lane; x < n; x += 64) {
-                const int32_t j = nbr_cols[(int64_t)i * prm.topn + x];
-                const double wij = nbr_vals[(int64_t)i * prm.topn + x];
+            for (int x0 = 0; x0 < n; x0 += 64) {  // uniform: the shuffles run converged
+                const int x = x0 + lane;
+                const int32_t j = x < n ? nbr_cols[(int64_t)i * prm.topn + x] : -2;
                 bool inh = false;
-                for (int64_t l = 0; l < L && !inh; ++l) inh = items[b + l] == j;
+                if (L <= 64) {
+                    for (int l = 0; l < (int)L; ++l) inh |= __shfl(hl, l, 64) == j;
+                } else if (x < n) {
+                    for (int64_t l = 0; l < L && !inh; ++l) inh = items[b + l] == j;
+                }
+                if (x >= n) continue;
+                const double wij = nbr_vals[(int64_t)i * prm.topn + x];
                 uint64_t key = sentinel;
                 double v = 0.0;
                 if (!inh) {
