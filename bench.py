@@ -396,9 +396,75 @@ def run_din(args, device, rank, world):
     return out
 
 
-def main():
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """``--gpus N`` with no torch.distributed launcher around us: start N
+    worker processes of this script (one per GPU, RANK = LOCAL_RANK = r,
+    WORLD_SIZE = N, 127.0.0.1 rendezvous) and wait for them.  Runs before
+    this process touches the GPU (no HIP call, no exec).  Rank 0 prints the
+    JSON line; the parent returns non-zero if any rank fails, and stops the
+    remaining ranks (by their own PIDs) so none waits forever in a
+    collective."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env))
+    log(f"[launcher] started {n} ranks: pids {[p.pid for p in procs]}, master 127.0.0.1:{port}")
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                log(f"[launcher] rank {procs.index(p)} exited with {code}; stopping the others")
+                for o in live:
+                    o.terminate()
+    return rc
+
+
+def dry_run(args, world, rank, local):
+    """--dry-run: the launcher and rendezvous without the workload (CPU
+    tests use it with --backend gloo): every rank joins the process group,
+    checks the world with an all_reduce, and rank 0 prints a JSON line."""
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group(args.backend or "gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        assert int(t.item()) == world, (t, world)
+    log(f"[rank {rank}/{world}] local_rank {local} pid {os.getpid()} backend {args.backend or 'gloo'} (dry run)")
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the env, bench.py starts them itself")
+    ap.add_argument("--backend", default=None, help="process-group backend (default nccl = RCCL)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher + rendezvous only, no workload")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--users", type=int, default=250_000)
@@ -422,20 +488,27 @@ def main():
     ap.add_argument("--din-steps", type=int, default=10)
     ap.add_argument("--din-warmup", type=int, default=2)
     ap.add_argument("--din-cpu-sample", type=int, default=4096)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[rank {rank}] note: WORLD_SIZE={world} from the launcher, --gpus {args.gpus}; using {world}")
+    if args.dry_run:
+        return dry_run(args, world, rank, local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    log(f"[rank {rank}/{world}] device {device} ({torch.cuda.get_device_name(device)}), pid {os.getpid()}")
 
     from nrk import ops
 
