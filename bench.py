@@ -529,32 +529,33 @@ def main(argv=None):
     item_vec = ops.tt_item_fwd(wl["item_table"], torch.arange(I, dtype=torch.int32, device=device))
     row_lo = 0
     if catalog_mode:
-        from nrk.dist import catalog_sharded_topk, shard_range
+        from nrk.dist import HipShard, catalog_sharded_topk, gather_users, shard_range
 
         row_lo, row_hi = shard_range(I, world, rank)
         item_vec = item_vec[row_lo:row_hi].contiguous()
+        ulo, uhi = shard_range(U, world, rank)  # this rank's user-tower block
     cat = ops.Catalog(item_vec)
-    ws = ops.ip_topk_workspace(U, cat, K, device)
-    out_s = torch.empty((U, K), dtype=torch.float32, device=device)
-    out_r = torch.empty((U, K), dtype=torch.int32, device=device)
+    if catalog_mode:
+        shard = HipShard(cat, row_lo, K, U)
+    else:
+        ws = ops.ip_topk_workspace(U, cat, K, device)
+        out_s = torch.empty((U, K), dtype=torch.float32, device=device)
+        out_r = torch.empty((U, K), dtype=torch.int32, device=device)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s: U={U} I={I} D={D} K={K} clicks={wl['n_clicks']}")
 
-    def local_topk(users, shard, k, lo):
-        ops.ip_topk_screen(users, shard, k, ws)
-        ops.ip_topk_finish(users, shard, k, ws, out_s, out_r, row_offset=lo, out_exact=out_e)
-        return out_e, out_r
-
-    out_e = torch.empty((U, K), dtype=torch.float64, device=device) if catalog_mode else None
-
     def step_catalog(ev=None):
+        # tower for this rank's users only, all_gather -> every user on every
+        # rank; screen the shard, all_reduce(MAX) the bounds, refine above the
+        # global bound, all_to_all + merge (nrk.dist.catalog_sharded_topk)
         if ev is not None:
             ev[0].record()
-        u = ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"], wl["hist"],
-                            wl["hist_len"], wl["w0"], wl["b0"], wl["w1"], wl["b1"])
+        u_loc = ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"][ulo:uhi], wl["hist"][ulo:uhi],
+                                wl["hist_len"][ulo:uhi], wl["w0"], wl["b0"], wl["w1"], wl["b1"])
+        u = gather_users(u_loc, U)
         if ev is not None:
             ev[1].record()
-        res = catalog_sharded_topk(u, cat, row_lo, K, local=local_topk)
+        res = catalog_sharded_topk(u, shard, K)
         if ev is not None:
             ev[2].record()
             ev[3].record()

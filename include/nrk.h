@@ -100,6 +100,25 @@ int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
                        double* out_exact, void* workspace, size_t workspace_bytes,
                        nrk_stream_t stream);
 
+/* Catalog-sharded runs, between screen and
+ * finish:
+ *   nrk_ip_topk_bound writes, per user, the m (<= 32) largest exact lower
+ *   bounds this shard's screen found, descending, fp32 [n_users, m], -inf
+ *   padded: each one bounds a distinct item's exact score from below.
+ *   After an all_gather of every shard's [n_users, m] block (layout
+ *   [n_lists][n_users][m], n_lists * m <= 64), nrk_ip_topk_apply_bound takes
+ *   the k-th largest of the user's n_lists * m values -- a lower bound of
+ *   the user's k-th exact score over the WHOLE catalog -- and raises the
+ *   shard's refine cut to it, so finish rescores only the candidates that
+ *   can still reach the merged top-k (the output then holds the shard's
+ *   top-k among items with exact score >= the global bound, -1 padded).
+ *   k > n_lists * m leaves the cut unchanged.  New: no reference
+ *   counterpart (a Faiss search is single-index). */
+int nrk_ip_topk_bound(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
+                      int m, float* out_bound, void* workspace, size_t workspace_bytes, nrk_stream_t stream);
+int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, int m, int k, void* workspace,
+                            size_t workspace_bytes, nrk_stream_t stream);
+
 /* Merge n_lists per-shard top-k_in lists (fp64 exact scores + global rows,
  * list l of user u at [l * list_stride + u * k_in]) into the top-k_out by
  * (score desc, row asc).  New: the catalog-sharded multi-GPU merge

@@ -40,7 +40,7 @@ constexpr int IP_CW = 48;  // candidate entries per (user, half) slot of the wor
 constexpr int IP_KMAX = 32;
 constexpr size_t CATALOG_HDR = 256;
 
-static inline int pad_dim(int d) {
+__host__ __device__ static inline int pad_dim(int d) {
     return d <= 16 ? 16 : d <= 32 ? 32 : d <= 64 ? 64 : d <= 128 ? 128 : 256;
 }
 __host__ __device__ static inline int64_t n_blocks_of(int64_t n_items) { return (n_items + 31) / 32; }
@@ -558,29 +558,49 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         thr = (double)ce.x + (double)ce.y;
         thr = thr - fabs(thr) * 1e-15 - 1e-300;  // round down
     }
-    const int nitem = (n0 + n1) * 16;
-    // fp16 prefilter (DS4 > 0 with a packed catalog): recompute every band
-    // item's scaled fp16 score from the 64-B packed row and keep it when it
-    // reaches the screen's cut -- |fp16 score - exact| <= eps as in the
-    // screen, so every item with exact >= cut + eps passes.  Only those rows
-    // are then fetched in fp32 for the exact score.
+    // The screen's cut in its scaled fp16 units (exact power-of-two rescale):
+    // |fp16 score - exact| <= eps, so every item with exact >= cut + eps has
+    // an fp16 score >= cut.  Used twice: (a) band entries (half-blocks) whose
+    // listed fp16 max is below it are dropped -- none on one GPU (the final
+    // flush kept only entries >= cut), most of the band on a catalog shard
+    // after nrk_ip_topk_apply_bound raised the cut to the global bound; (b)
+    // the fp16 prefilter (DS4 > 0): every band item's fp16 score recomputed
+    // from its 64-B packed row, only items reaching the cut are fetched in
+    // fp32 for the exact score.
     constexpr int DSK = DS4 / 4;  // 16-dim k-steps of the packed layout
-    bool pre = DS4 > 0 && catalog != nullptr && ce.x != -INFINITY;
+    const bool pre = catalog != nullptr && ce.x != -INFINITY;
     float ush[DS4 > 0 ? 4 * DS4 : 1];
     float pcut = 0.0f;
-    if constexpr (DS4 > 0) {
-        if (pre) {
-            const int nblk_c = (int)((n_items + 31) >> 5);
-            const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk_c * 64 * (4 * DS4));
-            float ua = 0.0f;
-#pragma unroll
-            for (int d = 0; d < 4 * DS4; ++d) ua = fmaxf(ua, fabsf(uv[d]));
-            const float su = pow2_scale(ua);
+    if (pre) {
+        const int dpc = pad_dim(dim);
+        const int64_t nblk_c = (n_items + 31) >> 5;
+        const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk_c * 64 * dpc);
+        float ua = 0.0f;
+        for (int d = 0; d < dim; ++d) ua = fmaxf(ua, fabsf(uv[d]));
+        const float su = pow2_scale(ua);
+        if constexpr (DS4 > 0) {
 #pragma unroll
             for (int d = 0; d < 4 * DS4; ++d) ush[d] = (float)(_Float16)(uv[d] * su);
-            pcut = ce.x * (su * hdr->scale);  // exact power-of-two rescale
         }
+        pcut = ce.x * (su * hdr->scale);
     }
+    // (a) compact the band of both halves into LDS (list order kept)
+    __shared__ uint32_t bandq[4][2 * IP_CW];
+    int nband = 0;
+    for (int b0 = 0; b0 < n0 + n1; b0 += WAVE) {
+        const int e = b0 + lane;
+        uint2 ent = make_uint2(0u, 0u);
+        if (e < n0 + n1)
+            ent = e < n0 ? cand[(size_t)(2 * u) * IP_CW + e] : cand[(size_t)(2 * u + 1) * IP_CW + (e - n0)];
+        const bool kp = e < n0 + n1 && (!pre || __uint_as_float(ent.x) >= pcut);
+        const unsigned long long bal = __ballot(kp);
+        if (kp) bandq[wave][nband + __popcll(bal & ((1ull << lane) - 1ull))] = ent.y;
+        nband += __popcll(bal);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int nitem = nband * 16;
     int cnt = 0;
     auto push = [&](bool keep, double s, int32_t row) {
         const unsigned long long bal = __ballot(keep);
@@ -598,10 +618,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         auto band_q = [&](int base) -> uint32_t {
             int idx = base + lane;
             idx = idx < nitem ? idx : nitem - 1;
-            const int bb = idx >> 4;
-            const uint2* cp = bb < n0 ? cand + (size_t)(2 * u) * IP_CW + bb
-                                      : cand + (size_t)(2 * u + 1) * IP_CW + (bb - n0);
-            return cp->y;
+            return bandq[wave][idx > 0 ? idx >> 4 : 0];
         };
         auto item_row = [&](int base, uint32_t qv, int32_t& row, bool& inb) {
             const int idx = base + lane, r = idx & 15;
@@ -701,7 +718,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
             int32_t row = 0;
             if (idx < nitem) {
                 const int bb = idx >> 4, r = idx & 15;
-                const uint32_t q = (bb < n0) ? cand[(2 * u) * IP_CW + bb].y : cand[(2 * u + 1) * IP_CW + (bb - n0)].y;
+                const uint32_t q = bandq[wave][bb];
                 const int64_t rr = (int64_t)(q >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (q & 1);
                 if (rr < n_items) row = (int32_t)rr;
                 keep = rr < n_items;
@@ -870,6 +887,81 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
             out_r[u * k_out + idx] = ok ? x[e].row : -1;
             if (out_e) out_e[u * k_out + idx] = ok ? x[e].s : -INFINITY;
         }
+    }
+}
+
+// ------------------------------------------------- catalog-shard bound --
+constexpr int IP_BOUND_MMAX = 32;
+
+// Per user, the m largest listed half-block maxima of this shard's band as
+// exact lower bounds: a half-block whose fp16 max is x (scaled units, scl =
+// su * catalog scale) holds an item with exact score >= x / scl - eps.
+// Distinct half-blocks are distinct items, so any k of these values bound k
+// distinct items from below.  Descending, -inf padded (fp32, rounded down).
+template <int MM>
+__global__ void ip_bound_kernel(const float* __restrict__ users, int64_t n_users, int dim,
+                                const CatalogHdr* __restrict__ hdr, const uint2* __restrict__ cand,
+                                const int32_t* __restrict__ cand_cnt, const float2* __restrict__ ucut,
+                                int m, float* __restrict__ out) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n_users) return;
+    float best[MM];
+#pragma unroll
+    for (int j = 0; j < MM; ++j) best[j] = -INFINITY;
+    const int n0 = cand_cnt[2 * u], n1 = cand_cnt[2 * u + 1];
+    if (n0 + n1 > 0) {
+        const float* uv = users + u * dim;
+        float ua = 0.0f;
+        for (int d = 0; d < dim; ++d) ua = fmaxf(ua, fabsf(uv[d]));
+        const double inv = 1.0 / ((double)pow2_scale(ua) * (double)hdr->scale);  // exact power of two
+        const double eps = (double)ucut[u].y;
+        for (int e = 0; e < n0 + n1; ++e) {
+            const uint2 c = e < n0 ? cand[(size_t)(2 * u) * IP_CW + e] : cand[(size_t)(2 * u + 1) * IP_CW + (e - n0)];
+            const double t = (double)__uint_as_float(c.x) * inv - eps;
+            float v = (float)t;
+            if ((double)v > t) v = nextafterf(v, -INFINITY);
+            // insertion into the descending top-m
+#pragma unroll
+            for (int j = 0; j < MM; ++j) {
+                const bool in = j < m && v > best[j];
+                const float o = best[j];
+                best[j] = in ? v : o;
+                v = in ? o : v;
+            }
+        }
+    }
+    for (int j = 0; j < m; ++j) out[u * m + j] = best[j];
+}
+
+// G = the k-th largest of the n_lists * m bounds of the user (lists laid out
+// [n_lists][n_users][m]; -inf when there are fewer than k finite values) is a
+// lower bound of the user's k-th exact score over the whole catalog.  Raise
+// the shard's cut to G - eps (rounded down to fp32): the refine then keeps
+// exact >= cut + eps <= G, and the band / prefilter tests use the raised cut.
+// One wave per user: one value per lane, wave bitonic sort (n_lists * m <= 64).
+__global__ __launch_bounds__(256) void ip_apply_bound_kernel(float2* __restrict__ ucut, int64_t n_users,
+                                                             const float* __restrict__ vals, int n_lists,
+                                                             int m, int k) {
+    const int lane = threadIdx.x & 63;
+    const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (u >= n_users) return;
+    Cand x[1];
+    x[0].row = lane;
+    x[0].s = -(double)INFINITY;
+    if (lane < n_lists * m) {
+        const int l = lane / m, j = lane - l * m;
+        x[0].s = (double)vals[((int64_t)l * n_users + u) * m + j];
+    }
+    wave_bitonic_sort<1>(x);
+    const double G = __shfl(x[0].s, k - 1, WAVE);
+    if (lane != 0 || !(G > -(double)INFINITY)) return;
+    float2 c = ucut[u];
+    const double t = G - (double)c.y;
+    float f = (float)t;
+    if ((double)f > t) f = nextafterf(f, -INFINITY);
+    if (f > c.x) {
+        c.x = f;
+        ucut[u] = c;
     }
 }
 
@@ -1045,6 +1137,50 @@ int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const v
     if (rc != NRK_OK) return rc;
     return nrk_ip_topk_finish(users, n_users, items, catalog, n_items, dim, k, row_offset, out_scores,
                               out_rows, out_exact, workspace, workspace_bytes, stream);
+}
+
+int nrk_ip_topk_bound(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
+                      int m, float* out_bound, void* workspace, size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    int rc = ip_check(users, n_users, (const float*)catalog, catalog, n_items, dim, 1, workspace,
+                      workspace_bytes);
+    if (rc != NRK_OK) return rc;
+    NRK_REQUIRE(m >= 1 && m <= IP_BOUND_MMAX, "m must be in [1, 32]");
+    if (n_users == 0) return NRK_OK;
+    NRK_REQUIRE(out_bound != nullptr, "null pointer");
+    const IpWs w = ip_ws_layout(workspace, n_users);
+    hipStream_t s = as_stream(stream);
+    if (n_items == 0) {
+        // empty shard: no bound (the screen wrote no band)
+        (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * 2 * sizeof(int32_t), s);
+    }
+    const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(
+        reinterpret_cast<const uint8_t*>(catalog) + catalog_body_bytes(n_items, pad_dim(dim)));
+    const int grid = (int)((n_users + 255) / 256);
+    if (m <= 8)
+        ip_bound_kernel<8><<<grid, 256, 0, s>>>(users, n_users, dim, hdr, w.cand, w.cnt, w.ucut, m, out_bound);
+    else
+        ip_bound_kernel<IP_BOUND_MMAX><<<grid, 256, 0, s>>>(users, n_users, dim, hdr, w.cand, w.cnt, w.ucut, m,
+                                                            out_bound);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, int m, int k, void* workspace,
+                            size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_users >= 0 && n_users < (1ll << 30), "n_users out of range");
+    NRK_REQUIRE(n_lists >= 1 && m >= 1 && n_lists * m <= 64, "need 1 <= n_lists * m <= 64");
+    NRK_REQUIRE(k >= 1 && k <= IP_KMAX, "k must be in [1, 32]");
+    if (n_users == 0) return NRK_OK;
+    NRK_REQUIRE(bounds && workspace, "null pointer");
+    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users).bytes, "workspace too small");
+    const IpWs w = ip_ws_layout(workspace, n_users);
+    if (k > n_lists * m) return NRK_OK;  // fewer values than k: no bound, cut unchanged
+    ip_apply_bound_kernel<<<(int)((n_users + 3) / 4), 256, 0, as_stream(stream)>>>(w.ucut, n_users, bounds,
+                                                                                 n_lists, m, k);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
 }
 
 int nrk_topk_merge(const double* in_exact, const int32_t* in_rows, int n_lists, int64_t list_stride,

@@ -3,11 +3,13 @@ torch.distributed over RCCL ("nccl" on ROCm), 127.0.0.1 rendezvous.
 
 * users-sharded  -- every rank scores its own contiguous user block against
   the full (replicated) catalog.  No data-path collective (weak scaling).
-* catalog-sharded (BASELINE config 4) -- rank r holds items [lo_r, hi_r) and
-  scores ALL users of the batch against its shard (global row ids via
-  row_offset).  One exchange step: all_to_all of the shard-local top-k
-  (fp64 exact score + int32 global row, 12 B per entry) so that the owner of
-  each user block receives every shard's list for its users, then
+* catalog-sharded (BASELINE config 4) -- rank r holds items [lo_r, hi_r).
+  Each rank runs the user tower for its own user block and all_gathers the
+  vectors (gather_users); every rank then screens ALL users against its
+  shard, the per-user screen bounds are all_reduced (MAX) so every shard
+  refines only candidates above the global k-th-score bound, and an
+  all_to_all of the shard-local top-k (fp64 exact score + int32 global row,
+  12 B per entry) hands each user block's lists to its owner, where
   nrk_topk_merge orders by (score desc, row asc) -- the same tie-break as a
   single GPU, so the merged lists are identical to the 1-GPU result.
 * users-sharded ItemCF similarity (itemcf_sim_sharded) -- rank r holds the
@@ -31,11 +33,47 @@ def shard_range(n: int, world: int, rank: int):
     return lo, min(n, lo + per)
 
 
-def _default_local(users, shard, k, row_lo):
-    from . import ops
+class HipShard:
+    """This rank's catalog shard on the HIP path (nrk_ip_topk_screen ->
+    nrk_ip_topk_bound / _apply_bound -> nrk_ip_topk_finish), with its
+    workspace and outputs allocated once for ``n_users`` queries."""
 
-    s, r, e = ops.ip_topk(users, shard, k, row_offset=row_lo, exact=True)
-    return e, r
+    def __init__(self, catalog, row_lo: int, k: int, n_users: int):
+        from . import ops
+
+        self.ops, self.cat, self.row_lo, self.k = ops, catalog, int(row_lo), int(k)
+        dev = catalog.items.device
+        self.ws = ops.ip_topk_workspace(n_users, catalog, k, dev)
+        self.s = torch.empty((n_users, k), dtype=torch.float32, device=dev)
+        self.r = torch.empty((n_users, k), dtype=torch.int32, device=dev)
+        self.e = torch.empty((n_users, k), dtype=torch.float64, device=dev)
+
+    def screen(self, users, m: int):
+        """fp16 MFMA screen; returns this shard's m largest exact lower
+        bounds per user (fp32 [U, m])."""
+        self.ops.ip_topk_screen(users, self.cat, self.k, self.ws)
+        return self.ops.ip_topk_bound(users, self.cat, m, self.ws)
+
+    def finish(self, users, bounds=None):
+        """Exact refine -> (exact f64 [U, k], global rows i32 [U, k]) of this
+        shard; with ``bounds`` ([n_lists, U, m], every shard's screen bounds)
+        the cut is first raised to the k-th largest of each user's values."""
+        n = users.shape[0]
+        if bounds is not None:
+            self.ops.ip_topk_apply_bound(bounds, self.k, self.ws)
+        self.ops.ip_topk_finish(users, self.cat, self.k, self.ws, self.s[:n], self.r[:n],
+                                out_exact=self.e[:n], row_offset=self.row_lo)
+        return self.e[:n], self.r[:n]
+
+
+def bound_width(k: int, world: int) -> int:
+    """Bounds per user and shard for the exchange: world * m >= k values
+    (so the k-th largest exists) with a little slack, world * m <= 64; 0 =
+    no exchange (one rank, or too many ranks for one wave's sort)."""
+    if world <= 1:
+        return 0
+    m = min(32, -(-k // world) + 1)
+    return m if world * m <= 64 and world * m >= k else 0
 
 
 def _default_merge(exact_lists, row_lists, k):
@@ -44,19 +82,56 @@ def _default_merge(exact_lists, row_lists, k):
     return ops.topk_merge(exact_lists, row_lists, k)
 
 
-def catalog_sharded_topk(users, shard, row_lo: int, k: int, group=None, local=None, merge=None):
+def gather_users(u_local, n_users: int, group=None):
+    """Every rank computed the user tower for its own block
+    shard_range(n_users, world, rank); all_gather -> the full [n_users, D]
+    on every rank (the catalog-sharded screen needs every user)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return u_local
+    per = -(-n_users // world)
+    buf = torch.empty((per * world,) + tuple(u_local.shape[1:]), dtype=u_local.dtype, device=u_local.device)  # rank-major blocks
+    send = u_local
+    if u_local.shape[0] < per:
+        send = torch.zeros((per,) + tuple(u_local.shape[1:]), dtype=u_local.dtype, device=u_local.device)
+        send[: u_local.shape[0]] = u_local
+    dist.all_gather_into_tensor(buf, send.contiguous(), group=group)
+    if per * world == n_users:
+        return buf
+    parts = [buf[r * per: r * per + (shard_range(n_users, world, r)[1] - shard_range(n_users, world, r)[0])]
+             for r in range(world)]
+    return torch.cat(parts).contiguous()
+
+
+def catalog_sharded_topk(users, shard, k: int, group=None, merge=None, exchange_bound: bool = True):
     """Exact top-k of ``users`` (replicated on every rank, [U, D]) over the
-    catalog split across the ranks of ``group``.  ``shard`` is this rank's
-    ops.Catalog (rows [row_lo, row_lo + shard.ntotal)).  Returns the merged
-    (scores f32, rows i32, exact f64) for THIS rank's user block
-    shard_range(U, world, rank).  ``local`` / ``merge`` default to the HIP
-    kernels; tests inject CPU stand-ins to run the exchange under gloo."""
-    local = local or _default_local
+    catalog split across the ranks of ``group``.  ``shard`` (HipShard, or a
+    stand-in with the same screen / finish methods in the gloo tests) holds
+    this rank's rows [row_lo, row_lo + n) and reports global rows.
+
+    Two exchanges:
+      1. all_gather of every shard's m largest screen bounds per user
+         (fp32 [U, m], bound_width(k, world)) between screen and refine: the
+         k-th largest of a user's world * m values bounds the user's GLOBAL
+         k-th exact score from below, so each shard rescores only the
+         candidates that can still reach the merged top-k;
+      2. all_to_all of the shard-local top-k (fp64 exact + int32 global row)
+         to the owner of each user block, then the (score desc, row asc)
+         merge -- the same tie-break as one GPU.
+    Returns the merged (scores f32, rows i32, exact f64) of THIS rank's user
+    block shard_range(U, world, rank)."""
     merge = merge or _default_merge
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     U = users.shape[0]
-    e, r = local(users, shard, k, row_lo)  # [U, k] each
+    m = bound_width(k, world) if exchange_bound else 0
+    b = shard.screen(users, max(m, 1))
+    bounds = None
+    if m:
+        bounds = torch.empty((world * b.shape[0], b.shape[1]), dtype=b.dtype, device=b.device)
+        dist.all_gather_into_tensor(bounds, b.contiguous(), group=group)
+        bounds = bounds.view(world, b.shape[0], b.shape[1])
+    e, r = shard.finish(users, bounds)  # [U, k] each
     if world == 1:
         return merge(e.unsqueeze(0).contiguous(), r.unsqueeze(0).contiguous(), k)
     per = -(-U // world)

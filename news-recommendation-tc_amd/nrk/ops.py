@@ -164,6 +164,30 @@ def ip_topk_finish(users, catalog: Catalog, k: int, workspace, out_scores, out_r
               workspace.numel(), _stream())
 
 
+def ip_topk_bound(users, catalog: Catalog, m: int, workspace):
+    """After ip_topk_screen: per user the m largest exact lower bounds of
+    this shard (fp32 [n, m], descending, -inf padded), each bounding a
+    distinct item's exact score."""
+    _dev(users, workspace)
+    n = users.shape[0]
+    out = torch.empty((n, m), dtype=torch.float32, device=users.device)
+    _lib.call("nrk_ip_topk_bound", _ptr(users), n, _ptr(catalog.packed), catalog.n, catalog.d, int(m), _ptr(out),
+              _ptr(workspace), workspace.numel(), _stream())
+    return out
+
+
+def ip_topk_apply_bound(bounds, k: int, workspace):
+    """bounds [n_lists, n, m] fp32 (every shard's ip_topk_bound): raise this
+    shard's refine cut to the k-th largest of each user's n_lists * m values."""
+    _dev(bounds, workspace)
+    _need(bounds, torch.float32, name="bounds")
+    if bounds.dim() != 3:
+        raise ValueError("bounds must be [n_lists, n_users, m]")
+    L, n, m = bounds.shape
+    _lib.call("nrk_ip_topk_apply_bound", n, _ptr(bounds), L, m, int(k), _ptr(workspace), workspace.numel(),
+              _stream())
+
+
 def row_normalize(x, norms=False):
     """x / ||x|| per row, bit-identical to numpy float32 (similarity/embedding.py:41)."""
     _dev(x)

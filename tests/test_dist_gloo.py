@@ -37,34 +37,63 @@ def _np_merge(exact_lists, row_lists, k):
             torch.from_numpy(np.where(ok, oe, -np.inf)))
 
 
-def _oracle_local(users, shard, k, row_lo):
-    from oracle import oracle
+class _OracleShard:
+    """CPU stand-in for nrk.dist.HipShard: the screen's bounds are the
+    shard's m largest exact scores minus a margin (valid lower bounds of
+    distinct items, like the HIP screen's half-block maxima - eps); finish
+    takes the k-th largest of every shard's bounds and returns the shard's
+    top-k restricted to exact >= that bound (-1 padded), the contract of
+    nrk_ip_topk_apply_bound."""
 
-    s, r, e = oracle.ip_topk(users.numpy(), shard, k, exact=True)
-    r = np.where(r >= 0, r + row_lo, -1)
-    return torch.from_numpy(e), torch.from_numpy(r.astype(np.int32))
+    def __init__(self, items, lo, k):
+        self.items, self.lo, self.k, self.dropped = items, lo, k, 0
+
+    def screen(self, users, m):
+        sc = users.double().numpy() @ self.items.astype(np.float64).T
+        top = -np.sort(-sc, axis=1)[:, :m] - 1e-9
+        if top.shape[1] < m:
+            top = np.concatenate([top, np.full((len(top), m - top.shape[1]), -np.inf)], 1)
+        return torch.from_numpy(top.astype(np.float32) - np.float32(1e-6))
+
+    def finish(self, users, bounds):
+        from oracle import oracle
+
+        s, r, e = oracle.ip_topk(users.numpy(), self.items, self.k, exact=True)
+        r = np.where(r >= 0, r + self.lo, -1)
+        if bounds is not None:
+            L, U, m = bounds.shape
+            vals = bounds.permute(1, 0, 2).reshape(U, L * m).double().numpy()
+            g = -np.sort(-vals, axis=1)[:, self.k - 1]
+            drop = (r >= 0) & (e < g[:, None])
+            self.dropped += int(drop.sum())
+            r = np.where(drop, -1, r)
+            e = np.where(drop, -np.inf, e)
+        return torch.from_numpy(e), torch.from_numpy(r.astype(np.int32))
 
 
 def _worker(rank, world, port, U, I, D, k, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from nrk.dist import catalog_sharded_topk, shard_range
+        from nrk.dist import catalog_sharded_topk, gather_users, shard_range
 
         rng = np.random.default_rng(7)
         users = rng.standard_normal((U, D)).astype(np.float32)
         items = rng.standard_normal((I, D)).astype(np.float32)
         items[I // 2 + 1] = items[3]  # cross-shard exact tie -> lower row must win
         lo, hi = shard_range(I, world, rank)
-        s, r, e = catalog_sharded_topk(torch.from_numpy(users), items[lo:hi], lo, k,
-                                       local=_oracle_local, merge=_np_merge)
         ulo, uhi = shard_range(U, world, rank)
-        q.put((rank, ulo, uhi, s.numpy(), r.numpy()))
+        # the user tower runs per user block; all_gather gives every rank all users
+        full = gather_users(torch.from_numpy(users[ulo:uhi]), U)
+        assert torch.equal(full, torch.from_numpy(users))
+        shard = _OracleShard(items[lo:hi], lo, k)
+        s, r, e = catalog_sharded_topk(full, shard, k, merge=_np_merge)
+        q.put((rank, ulo, uhi, s.numpy(), r.numpy(), shard.dropped))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("U,I,k", [(37, 101, 31), (64, 40, 31), (5, 7, 10)])
+@pytest.mark.parametrize("U,I,k", [(37, 101, 31), (64, 40, 31), (5, 7, 10), (50, 400, 8)])
 def test_catalog_sharded_matches_single(U, I, k):
     from oracle import oracle
 
@@ -84,9 +113,11 @@ def test_catalog_sharded_matches_single(U, I, k):
     items = rng.standard_normal((I, D)).astype(np.float32)
     items[I // 2 + 1] = items[3]
     so, ro = oracle.ip_topk(users, items, k)
-    for rank, ulo, uhi, s, r in got:
+    for rank, ulo, uhi, s, r, _ in got:
         assert np.array_equal(r, ro[ulo:uhi]), rank
         assert np.array_equal(s, so[ulo:uhi]), rank
+    if I >= 2 * k:  # the global bound cut the shard lists (the refine-shrinking exchange ran)
+        assert sum(g[5] for g in got) > 0
 
 
 def test_shard_range_covers():

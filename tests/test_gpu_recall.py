@@ -184,24 +184,54 @@ def test_catalog_shards_merge_equals_single(ops, n_shards):
     """Config-4 data path on one GPU: per-shard exact top-k with global rows
     (row_offset) + nrk_topk_merge == the unsharded result, incl. a cross-shard
     exact tie (lower global row wins)."""
-    from nrk.dist import catalog_sharded_topk, shard_range
+    from nrk.dist import HipShard, bound_width, catalog_sharded_topk, shard_range
 
     rng = np.random.default_rng(n_shards)
     users = _unit(rng.standard_normal((300, 32)))
+    users[7] = 0.0  # zero user: all-tie row, lowest global rows win
     items = _unit(rng.standard_normal((5000, 32)))
     items[4990] = items[10]
     K = 31
     so, ro = oracle.ip_topk(users, items, K)
-    es, rs = [], []
-    for r in range(n_shards):
-        lo, hi = shard_range(len(items), n_shards, r)
-        cat = ops.Catalog(_dev(items[lo:hi]))
-        _, rr, ee = ops.ip_topk(_dev(users), cat, K, row_offset=lo, exact=True)
-        es.append(ee)
-        rs.append(rr)
-    s, r, e = ops.topk_merge(torch.stack(es).contiguous(), torch.stack(rs).contiguous(), K)
-    assert np.array_equal(r.cpu().numpy(), ro)
-    assert np.array_equal(s.cpu().numpy(), so)
+    u = _dev(users)
+    for exchange in (False, True):
+        shards = []
+        for r in range(n_shards):
+            lo, hi = shard_range(len(items), n_shards, r)
+            shards.append(HipShard(ops.Catalog(_dev(items[lo:hi])), lo, K, len(users)))
+        m = bound_width(K, n_shards)
+        bounds = torch.stack([sh.screen(u, max(m, 1)) for sh in shards]).contiguous()  # = the all_gather
+        lists = [sh.finish(u, bounds if exchange and m else None) for sh in shards]
+        es = torch.stack([x[0] for x in lists]).contiguous()
+        rs = torch.stack([x[1] for x in lists]).contiguous()
+        s, r, e = ops.topk_merge(es, rs, K)
+        assert np.array_equal(r.cpu().numpy(), ro), exchange
+        assert np.array_equal(s.cpu().numpy(), so), exchange
+        if exchange:  # the global bound left each shard about its share of the top-k
+            assert int((rs >= 0).sum()) < 2 * len(users) * K
     # the single-rank code path of nrk.dist (no process group)
-    s1, r1, _ = catalog_sharded_topk(_dev(users), ops.Catalog(_dev(items)), 0, K)
+    s1, r1, _ = catalog_sharded_topk(u, HipShard(ops.Catalog(_dev(items)), 0, K, len(users)), K)
     assert np.array_equal(r1.cpu().numpy(), ro)
+
+
+def test_catalog_shards_bound_full_size(ops):
+    """8-shard replay of config 4 at the full catalog (364,047 x 32) with the
+    bound exchange: merged rows / scores bit-exact vs the oracle on a sample."""
+    from nrk.dist import HipShard, bound_width, shard_range
+
+    U, I, D, K, N = 4096, 364_047, 32, 31, 8
+    g = torch.Generator(device="cuda").manual_seed(5)
+    users = torch.nn.functional.normalize(torch.randn(U, D, device="cuda", generator=g), dim=1).contiguous()
+    items = torch.nn.functional.normalize(torch.randn(I, D, device="cuda", generator=g), dim=1).contiguous()
+    shards = [HipShard(ops.Catalog(items[lo:hi].contiguous()), lo, K, U)
+              for lo, hi in (shard_range(I, N, r) for r in range(N))]
+    m = bound_width(K, N)
+    gb = torch.stack([sh.screen(users, m) for sh in shards]).contiguous()
+    lists = [sh.finish(users, gb) for sh in shards]
+    s, r, e = ops.topk_merge(torch.stack([x[0] for x in lists]).contiguous(),
+                             torch.stack([x[1] for x in lists]).contiguous(), K)
+    torch.cuda.synchronize()
+    sample = np.arange(0, U, 16)
+    so, ro = oracle.ip_topk(users[sample].cpu().numpy(), items.cpu().numpy(), K, nthreads=8)
+    assert np.array_equal(r[sample].cpu().numpy().astype(np.int64), ro)
+    assert np.array_equal(s[sample].cpu().numpy(), so)
