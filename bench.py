@@ -46,6 +46,23 @@ PEAK_HBM_GBS = 8000.0
 
 
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
+BUSY_FILE = os.path.join(REPO, "profiles", "r02_busy.json")
+
+
+def pmc_busy(kernels, default_config):
+    """MFMA-busy / VALU-busy / stall shares of ``kernels`` from the committed
+    rocprofv3 SQ-counter passes of this bench's default workloads
+    (tools/pmc_busy.sh -> tools/pmc_busy.py); None off the default config."""
+    if not default_config or not os.path.exists(BUSY_FILE):
+        return None
+    b = json.load(open(BUSY_FILE))
+    out = {}
+    for k in kernels:
+        m = [v for name, v in b.items() if name.startswith(k)]
+        if m:
+            out[k.replace("nrk::", "")] = {x: m[0].get(x) for x in ("mfma_busy", "valu_busy", "wait_any", "wait_inst",
+                                                                     "active")}
+    return out or None
 
 
 def _traffic_file():
@@ -370,7 +387,9 @@ def run_din(args, device, rank, world):
                         "traffic_unit": "bytes per pass, every launch of one nrk_din_forward_segments call (profiles/r01_traffic.json din_pass)",
                         "kernel": f"nrk_din_forward_segments ({n} samples in Dice batches of {B}, one call)",
                         "kernel_ms": round(pass_ms, 4),
-                        "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * n}}
+                        "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * n,
+                        "busy": pmc_busy(["nrk::din_att", "nrk::din_wh", "nrk::din_mlp1", "nrk::din_mlp2",
+                                          "nrk::din_head"], n == DIN_SAMPLES)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle
 
@@ -612,7 +631,10 @@ def main(argv=None):
                 "traffic": round(traffic) if traffic else None,
                 "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_traffic.json)",
                 "kernel": "ip_screen_kernel<32> (fp16 MFMA 32x32x16)", "kernel_ms": round(screen_ms, 4),
-                "algorithmic_flop_per_launch": flops}
+                "algorithmic_flop_per_launch": flops,
+                "busy": pmc_busy(["nrk::ip_screen_kernel", "nrk::ip_refine_kernel", "nrk::tt_user_kernel"], default_cfg),
+                "busy_source": "profiles/r02_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
+                               "SQ_WAIT_ANY, GRBM_GUI_ACTIVE passes; tools/pmc_busy.py)"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
