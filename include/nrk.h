@@ -312,6 +312,39 @@ int nrk_din_assemble(const int32_t* rec_rows, const float* rec_scores, int64_t n
                      int64_t nu, int32_t* out_user, int32_t* out_item, int32_t* out_hist, int32_t* out_ctx,
                      float* out_mask, int32_t* out_cand, nrk_stream_t stream);
 
+/* Row gather of 4-byte words (int32 codes or f32 mask values): out[b] =
+ * src[idx[b]] (row_words words per row), zeros when idx[b] is outside
+ * [0, n_rows).  The device half of the vectorised DIN encoder
+ * (nrk/rank/encode.py): DINDataset.__getitem__ + collate_fn (src/rank/
+ * DIN.py:358-520) look every sample's user profile, candidate item features
+ * and last-T history up in per-user / per-item dicts; here those lookups
+ * become row indices into encoded tables resident in HBM. */
+int nrk_gather_rows(const void* src, int64_t n_rows, int row_words, const int32_t* idx, int64_t n, void* out,
+                    nrk_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Recall fusion                                                          */
+/* ---------------------------------------------------------------------- */
+
+/* RecallFusion.fuse (src/recall/fusion.py:267-342) for every user at once.
+ * Entries of all recall methods' lists grouped by user (offsets [n_users+1]),
+ * inside a user in method order then list order: item (dense int32 code),
+ * raw score (f64), method index, position in its list.  weight [n_methods].
+ * strategy: 0 weighted_sum, 1 weighted_avg, 2 max_score, 3 harmonic_mean,
+ * 4 diversity_weighted, 5 rrf (:189-265).  norm: 0 local (per list min-max,
+ * :71-98), 1 global (gmin / gmax from nrk_fuse_minmax, :100-134), 2 z-score
+ * (zmean / zstd per method, :136-187).  Optional seen_off / seen: per-user
+ * item codes removed after the merge (:320-326).  Output: the top-k items
+ * by (merged score desc, first appearance asc) -- the reference's stable
+ * sort of its insertion-ordered dict -- -1 padded, and the count per user.
+ * At most 256 entries per user and 16 methods. */
+int nrk_fuse_minmax(const double* score, int64_t n, double* out_minmax, nrk_stream_t stream);
+int nrk_fuse(const int64_t* offsets, int64_t n_users, const int32_t* item, const double* score,
+             const int32_t* method, const int32_t* rank, int n_methods, const double* weight, int strategy,
+             int norm, double gmin, double gmax, const double* zmean, const double* zstd, const int64_t* seen_off,
+             const int32_t* seen, int topk, int32_t* out_item, double* out_score, int32_t* out_cnt,
+             nrk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,23 @@ __global__ __launch_bounds__(256) void din_assemble_kernel(
     }
 }
 
+// Row gather of 4-byte words: out[b] = idx[b] in [0, n_rows) ? src[idx[b]] : 0.
+// One thread per (row, word), rows of W words contiguous in both buffers:
+// consecutive threads write consecutive words (coalesced stores); the reads
+// are W-word runs of random rows (the tables are small and cache-resident).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint32_t* __restrict__ src, int64_t n_rows, int W,
+                                                          const int32_t* __restrict__ idx, int64_t n,
+                                                          uint32_t* __restrict__ out) {
+    const int64_t total = n * W;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = e / W;
+        const int w = (int)(e - b * W);
+        const int32_t r = idx[b];
+        out[e] = (r >= 0 && r < n_rows) ? src[(int64_t)r * W + w] : 0u;
+    }
+}
+
 }  // namespace nrk
 
 using namespace nrk;
@@ -99,6 +116,20 @@ int nrk_din_assemble(const int32_t* rec_rows, const float* rec_scores, int64_t n
         rec_rows, rec_scores, k_in, skip, k_use, user_feat, n_user, item_feat, n_item, user_hist, hist_len, T,
         n_ctx, ctx_bins, score_lo, score_hi, seed, u0, n_pairs, out_user, out_item, out_hist, out_ctx,
         out_mask, out_cand);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_gather_rows(const void* src, int64_t n_rows, int row_words, const int32_t* idx, int64_t n, void* out,
+                    nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_rows >= 0 && n >= 0 && row_words >= 1, "bad sizes");
+    if (n == 0) return NRK_OK;
+    NRK_REQUIRE(idx && out && (src || n_rows == 0), "null pointer");
+    const int64_t total = n * row_words;
+    const int64_t g = (total + 255) / 256;
+    gather_rows_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, as_stream(stream)>>>(
+        reinterpret_cast<const uint32_t*>(src), n_rows, row_words, idx, n, reinterpret_cast<uint32_t*>(out));
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

@@ -53,6 +53,9 @@ SIGNATURES = {
                                 INT, P, P, P, P, P, SZ, P]),
     "nrk_din_assemble": (INT, [P, P, I64, INT, INT, INT, P, INT, P, I64, INT, P, P, INT, INT, INT,
                                ctypes.c_float, ctypes.c_float, ctypes.c_uint32, I64, I64, P, P, P, P, P, P, P]),
+    "nrk_gather_rows": (INT, [P, I64, INT, P, I64, P, P]),
+    "nrk_fuse_minmax": (INT, [P, I64, P, P]),
+    "nrk_fuse": (INT, [P, I64, P, P, P, P, INT, P, INT, INT, F64, F64, P, P, P, P, INT, P, P, P, P]),
     "nrk_din_prep_bytes": (SZ, [INT]),
     "nrk_din_prepare": (INT, [P, INT, P, INT, I64, P, P]),
     "nrk_din_workspace_bytes": (SZ, [I64, INT, INT, INT, INT, INT, INT]),

@@ -139,39 +139,10 @@ def minmax_created(art: Articles) -> np.ndarray:
 
 
 def youtubednn_histories(log: ClickLog, seq_max_len: int = 30):
-    """User-tower inputs exactly as youtubednn_recaller.py:425-443 builds them.
+    """extractors.youtubednn_histories over a ClickLog (kept for the tests)."""
+    from .extractors import youtubednn_histories as _h
 
-    Users are label-encoded (sorted raw ids -> 0..U-1); each user's history is
-    their rows in ``click_df`` row order (groupby, not time-sorted, :432-436)
-    with item ids label-encoded; the FIRST ``seq_max_len`` are kept and the
-    rest zero-padded (collate_fn :63-70).  Returns (uid[U], hist[U,T],
-    hist_len[U], item_raw_ids (encoded -> raw), first_occurrence item order).
-    """
-    u_raw = log.user_id
-    i_raw = log.click_article_id
-    u_classes, u_enc = np.unique(u_raw, return_inverse=True)
-    i_classes, i_enc = np.unique(i_raw, return_inverse=True)
-    # stable sort by encoded user keeps click_df row order inside a user
-    order = np.argsort(u_enc, kind="stable")
-    ue = u_enc[order]
-    ie = i_enc[order]
-    n_u = len(u_classes)
-    counts = np.bincount(ue, minlength=n_u)
-    offs = np.concatenate([[0], np.cumsum(counts)[:-1]])
-    pos = np.arange(len(ue)) - np.repeat(offs, counts)
-    keep = pos < seq_max_len
-    hist = np.zeros((n_u, seq_max_len), dtype=np.int64)
-    hist[ue[keep], pos[keep]] = ie[keep]
-    hist_len = np.minimum(counts, seq_max_len).astype(np.int64)
-    _, first_idx = np.unique(i_enc, return_index=True)
-    item_profile = i_enc[np.sort(first_idx)]  # encoded ids, first-occurrence order
-    return (
-        np.arange(n_u, dtype=np.int64),
-        hist,
-        hist_len,
-        i_classes.astype(np.int64),
-        item_profile.astype(np.int64),
-    )
+    return _h(log.user_id, log.click_article_id, seq_max_len)
 
 
 def din_batch(

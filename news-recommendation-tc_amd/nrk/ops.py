@@ -481,6 +481,22 @@ def din_assemble(rec_rows, rec_scores, user_feat, item_feat, user_hist, hist_len
     return out
 
 
+def gather_rows(src, idx):
+    """out[b] = src[idx[b]] for a [n_rows, ...] table of 4-byte elements
+    (int32 / float32); rows whose index is outside [0, n_rows) are zeros."""
+    _dev(src, idx)
+    _need(idx, torch.int32, name="idx")
+    if src.dtype not in (torch.int32, torch.float32):
+        raise ValueError("src must be int32 or float32")
+    W = 1
+    for d in src.shape[1:]:
+        W *= int(d)
+    n = idx.numel()
+    out = torch.empty((n,) + tuple(src.shape[1:]), dtype=src.dtype, device=idx.device)
+    _lib.call("nrk_gather_rows", _ptr(src), src.shape[0], W, _ptr(idx), n, _ptr(out), _stream())
+    return out
+
+
 # ---------------------------------------------------- users-sharded ItemCF --
 def itemcf_pairs(offsets, items, ts, created, n_items, slot_base=0, loc_alpha=1.0, loc_alpha_rev=0.7,
                  loc_beta=0.9, time_alpha=0.7, created_alpha=0.8):

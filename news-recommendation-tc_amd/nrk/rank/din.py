@@ -1,9 +1,10 @@
 """GPU DIN ranker: drop-in for src/rank/DIN.py's scoring path.
 
-* ``encode_samples`` restates DINDataset.__getitem__ + collate_fn
-  (DIN.py:289-520) as a vectorised host encoder that produces the same int
-  index tensors (0 = pad / unknown, class index + 1 otherwise; LAST T history
-  items, left aligned, prefix mask).
+* ``encode_samples`` / ``DinEncoder`` (nrk/rank/encode.py) restate
+  DINDataset.__getitem__ + collate_fn (DIN.py:289-520) without a per-row
+  loop: the same int index tensors (0 = pad / unknown, class index + 1
+  otherwise; LAST T history items, left aligned, prefix mask), the lookups
+  gathered on the device for ``DINRanker.predict``.
 * ``DINScorer`` holds a trained DINModel's state_dict in kernel layout and
   scores batches with the HIP kernels (nrk_din_forward).
 * ``DINRanker.predict`` mirrors DINRanker.predict (DIN.py:1219-1283): every
@@ -23,93 +24,18 @@ from .. import ops
 from ..config import RankConfig
 
 
-def _cache(label_encoders, feat):
-    enc = label_encoders.get(feat) if label_encoders else None
-    if enc is None:
-        return None
-    return {str(c): i + 1 for i, c in enumerate(enc.classes_)}
-
-
-def _code(cache, raw):
-    if cache is None:
-        return raw  # DINDataset._encode_feature_fast without an encoder (DIN.py:348-349)
-    return cache.get(str(raw), 0)
-
-
-def iloc_columns(df, cols):
-    """Column values exactly as ``main_df.iloc[idx][col]`` presents them
-    (DIN.py:369-371, 407).  pandas upcasts a row to the frame's common dtype:
-    with float context columns an int user_id reads back as 1013.0, so
-    ``str(row["user_id"])`` is "1013.0", misses the str(int) keys of the
-    profile / feature / history dicts and every user, item and history
-    feature encodes to 0.  That quirk is part of the reference's output and
-    is reproduced here, not repaired."""
-    if len(df) == 0:
-        return {c: [] for c in cols}
-    dt = df.iloc[0].dtype
-    if dt == object:
-        return {c: df[c].tolist() for c in cols}
-    return {c: df[c].astype(dt).tolist() for c in cols}
+from .encode import DinEncoder, iloc_columns  # noqa: F401  (re-exported)
 
 
 def encode_samples(user_ids, item_ids, ctx_cols, user_profile_dict, item_features_dict,
                    user_history_dict, user_features, item_features, ctx_features,
                    label_encoders, seq_max_len):
-    """Vectorised DINDataset + collate_fn.  ``user_ids``/``item_ids`` and
-    ``ctx_cols`` (feature -> list of raw values) as the reference reads them
-    from main_df rows (see ``iloc_columns``)."""
-    n = len(user_ids)
-    uc = [_cache(label_encoders, f) for f in user_features]
-    ic = [_cache(label_encoders, f) for f in item_features]
-    cc = [_cache(label_encoders, f) for f in ctx_features]
-    user_vec: Dict[str, List[int]] = {}
-    item_vec: Dict[str, List[int]] = {}
-
-    def uvec(u):
-        v = user_vec.get(u)
-        if v is None:
-            prof = user_profile_dict.get(u)
-            v = ([_code(c, prof.get(f, 0)) for c, f in zip(uc, user_features)]
-                 if prof is not None else [0] * len(user_features))
-            user_vec[u] = v
-        return v
-
-    def ivec(i):
-        v = item_vec.get(i)
-        if v is None:
-            feat = item_features_dict.get(i)
-            v = ([_code(c, feat.get(f, 0)) for c, f in zip(ic, item_features)]
-                 if feat is not None else [0] * len(item_features))
-            item_vec[i] = v
-        return v
-
-    T = seq_max_len
-    user = np.zeros((n, len(user_features)), np.int64)
-    item = np.zeros((n, len(item_features)), np.int64)
-    hist = np.zeros((n, T, len(item_features)), np.int64)
-    mask = np.zeros((n, T), np.float32)
-    ctx = np.zeros((n, len(ctx_features)), np.int64)
-    hist_cache: Dict[str, np.ndarray] = {}
-    for r in range(n):
-        u = str(user_ids[r])
-        it = str(item_ids[r])
-        user[r] = uvec(u)
-        item[r] = ivec(it)
-        h = hist_cache.get(u)
-        if h is None:
-            lst = user_history_dict.get(u, [])
-            if len(lst) > T:
-                lst = lst[-T:]  # LAST T (DIN.py:481-482)
-            h = np.array([ivec(x) for x in lst], np.int64).reshape(-1, len(item_features))
-            hist_cache[u] = h
-        L = h.shape[0]
-        hist[r, :L] = h
-        mask[r, :L] = 1.0
-    if len(ctx_features):
-        for k, f in enumerate(ctx_features):
-            cache = cc[k]
-            ctx[:, k] = [_code(cache, v) for v in ctx_cols[f]]
-    return {"user": user, "item": item, "hist": hist, "ctx": ctx, "mask": mask}
+    """DINDataset + collate_fn for a list of samples (host arrays).
+    ``user_ids``/``item_ids`` and ``ctx_cols`` (feature -> raw values) as the
+    reference reads them from main_df rows (see ``iloc_columns``)."""
+    enc = DinEncoder(user_profile_dict, item_features_dict, user_history_dict, user_features,
+                     item_features, ctx_features, label_encoders, seq_max_len)
+    return enc.encode_host(user_ids, item_ids, ctx_cols)
 
 
 class DINScorer:
@@ -135,11 +61,12 @@ class DINScorer:
         """All rows in order, reference batching (DIN.py:1245-1283).  With a
         batch size that is a multiple of 64 every batch is scored in one
         nrk_din_forward_segments call (each batch keeps its own Dice
-        statistics); otherwise one call per batch."""
+        statistics); otherwise one call per batch.  ``enc`` holds numpy
+        arrays or device tensors (DinEncoder.encode_device)."""
         n = enc["mask"].shape[0]
         if n >= 2 and (batch_size % 64 == 0 or n <= batch_size):
             d = self.device
-            t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a)).to(d, dt).contiguous()  # noqa: E731
+            t = lambda a, dt: torch.as_tensor(a).to(d, dt).contiguous()  # noqa: E731
             p = ops.din_forward(self.params, t(enc["user"], torch.int32), t(enc["item"], torch.int32),
                                 t(enc["hist"], torch.int32), t(enc["ctx"], torch.int32),
                                 t(enc["mask"], torch.float32), batch_size=batch_size)
@@ -150,8 +77,9 @@ class DINScorer:
             if e - s == 1:
                 out[s] = np.nan  # std over one sample is NaN in the reference too
                 continue
-            p = self.forward(enc["user"][s:e], enc["item"][s:e], enc["hist"][s:e],
-                             enc["ctx"][s:e], enc["mask"][s:e])
+            host = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in enc.items()}
+            p = self.forward(host["user"][s:e], host["item"][s:e], host["hist"][s:e],
+                             host["ctx"][s:e], host["mask"][s:e])
             out[s:e] = p.cpu().numpy()
         return out
 
@@ -178,6 +106,13 @@ class DINRanker:
         self.item_features = list(item_features)
         self.context_features = list(context_features)
         self.label_encoders = label_encoders
+        # the encoded lookup tables, built once per data set (the reference's
+        # _build_encoding_cache, DIN.py:330-342, plus the per-user / per-item
+        # dict lookups of __getitem__ turned into table rows)
+        self.encoder = DinEncoder(user_profile_dict, item_features_dict, user_history_dict,
+                                  self.user_profile_features, self.item_features, self.context_features,
+                                  label_encoders, self.config.din_seq_max_len)
+        self._tables = None
         return self
 
     def load_model(self, state_dict):
@@ -189,10 +124,10 @@ class DINRanker:
     def predict(self):
         if self.scorer is None:
             raise ValueError("Model is not trained yet. Please train the model before prediction.")
+        if getattr(self, "encoder", None) is None:
+            raise ValueError("set_data() must be called before predict()")
         cols = iloc_columns(self.main_df, ["user_id", "item_id"] + self.context_features)
-        enc = encode_samples(cols["user_id"], cols["item_id"], cols,
-                             self.user_profile_dict, self.item_features_dict,
-                             self.user_history_dict, self.user_profile_features,
-                             self.item_features, self.context_features, self.label_encoders,
-                             self.config.din_seq_max_len)
+        if self._tables is None:
+            self._tables = self.encoder.device_tables(self.scorer.device)
+        enc = self.encoder.encode_device(self._tables, cols["user_id"], cols["item_id"], cols)
         return self.scorer.predict(enc, self.config.batch_size)

@@ -19,11 +19,12 @@ from __future__ import annotations
 from typing import Dict, List, Tuple
 
 import numpy as np
+import pandas as pd
 import torch
 
 from .. import ops
 from ..config import RecallConfig
-from ..data import synth
+from ..data import extractors
 from .base import BaseRecaller
 
 
@@ -73,14 +74,10 @@ class YoutubeDNNRecaller(BaseRecaller):
               for k, v in state_dict.items()}
         if len([k for k in sd if k.startswith("user_tower.") and k.endswith(".weight")]) != 2:
             raise NotImplementedError("the GPU user tower is compiled for two hidden layers")
-        log = synth.ClickLog(
-            np.asarray(click_df["user_id"], np.int64),
-            np.asarray(click_df["click_article_id"], np.int64),
-            np.asarray(click_df["click_timestamp"], np.int64) if "click_timestamp" in click_df
-            else np.zeros(len(click_df), np.int64),
-        )
-        uid, hist, hlen, item_raw, profile = synth.youtubednn_histories(log, self.seq_max_len)
-        user_raw = np.unique(log.user_id)
+        user_col = np.asarray(click_df["user_id"], np.int64)
+        uid, hist, hlen, item_raw, profile = extractors.youtubednn_histories(
+            user_col, np.asarray(click_df["click_article_id"], np.int64), self.seq_max_len)
+        user_raw = np.unique(user_col)
         dev = self.device
         f = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         ue = ops.tt_user_fwd(
@@ -103,6 +100,7 @@ class YoutubeDNNRecaller(BaseRecaller):
         self.item_index_2_rawid = {i: int(r) for i, r in enumerate(item_raw)}
         self.item_rawid_2_index = {int(r): i for i, r in enumerate(item_raw)}
         self._item_raw = np.asarray(item_raw, np.int64)
+        self._user_index = pd.Index(np.asarray(user_raw, np.int64))
         self.catalog = ops.Catalog(ie)
 
     # ------------------------------------------------------------- recall --
@@ -110,30 +108,42 @@ class YoutubeDNNRecaller(BaseRecaller):
         return self.batch_recall([user_id], topk)[user_id]
 
     def batch_recall(self, user_ids: List[int], topk: int = 20) -> Dict[int, List[Tuple[int, float]]]:
+        """BaseRecaller.batch_recall (recall/base.py:24-40) as ONE device
+        top-(k+1) search; the result dict is built with vectorised id mapping
+        (row r -> item_index_2_rawid[r], the reference's quirk) and one
+        zip per user instead of a per-item Python loop."""
         if self.user_embeddings is None or self.catalog is None:
             raise ValueError("Model not trained. Call train() first.")
         n_users = self.user_embeddings.shape[0]
-        idx = np.array([self.user_rawid_2_index.get(u, -1) for u in user_ids], np.int64)
+        try:
+            idx = self._user_index.get_indexer(np.asarray(user_ids, dtype=np.int64))
+        except (TypeError, ValueError, OverflowError):  # non-integer ids: the dict's own lookup
+            idx = np.array([self.user_rawid_2_index.get(u, -1) for u in user_ids], np.int64)
         known = (idx >= 0) & (idx < n_users)
-        results: Dict[int, List[Tuple[int, float]]] = {u: [] for u in user_ids}
+        results: Dict[int, List[Tuple[int, float]]] = dict.fromkeys(user_ids)
+        for u in results:
+            results[u] = []
         if not known.any():
             return results
         rows_needed = torch.as_tensor(idx[known], device=self.device)
         q = self.user_embeddings.index_select(0, rows_needed).contiguous()
         s, r = ops.ip_topk(q, self.catalog, topk + 1)
-        s = s.cpu().numpy()
-        r = r.cpu().numpy().astype(np.int64)
+        s = s[:, 1:].cpu().numpy()  # rank 0 dropped (youtubednn_recaller.py:524)
+        r = r[:, 1:].cpu().numpy().astype(np.int64)
         n_map = len(self._item_raw)
+        ok = (r >= 0) & (r < n_map)
+        items = self._item_raw[np.where(ok, r, 0)]
         kn = [u for u, k in zip(user_ids, known) if k]
-        for n, u in enumerate(kn):
-            res = []
-            for i in range(1, topk + 1):  # skip rank 0 (youtubednn_recaller.py:524)
-                row = r[n, i]
-                if 0 <= row < n_map:
-                    res.append((int(self._item_raw[row]), float(s[n, i])))
-                if len(res) >= topk:
-                    break
-            results[u] = res
+        full = ok.all(1)
+        it_l, sc_l = items.tolist(), s.tolist()
+        if full.all():
+            results.update(zip(kn, map(list, map(zip, it_l, sc_l))))
+        else:
+            for n, u in enumerate(kn):
+                if full[n]:
+                    results[u] = list(zip(it_l[n], sc_l[n]))
+                else:  # -1 padding (fewer than topk + 1 items): skipped like :528
+                    results[u] = [(it_l[n][i], sc_l[n][i]) for i in range(topk) if ok[n, i]]
         return results
 
     def construct_embedding_dict(self, save: bool = False):

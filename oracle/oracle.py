@@ -17,6 +17,7 @@ Each function restates the reference (file:line cited) in numpy / C:
 * ``itemcf_topn``        -- ItemCFRecaller._precompute_topk_similar_items, itemcf_recaller.py:41-54
 * ``itemcf_recall``      -- ItemCFRecaller.recall, itemcf_recaller.py:56-129
 * ``din_forward``        -- Dice / ActivationUnit / DINModel.forward, DIN.py:29-286
+* ``fuse``               -- RecallFusion.fuse, recall/fusion.py:67-342
 
 Pinning: tests/test_oracle_golden.py checks every function against the golden
 fixtures produced by executing the reference (tests/golden/make_golden.py).
@@ -272,3 +273,67 @@ def bf16_round(x):
     b = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
     b = (b + 0x7FFF + ((b >> 16) & 1)) >> 16
     return (b.astype(np.uint32) << 16).view(np.float32).reshape(np.shape(x))
+
+
+def fuse(methods, weights, strategy="weighted_avg", norm="local", topk=30, user_history=None, remove_seen=True):
+    """RecallFusion.fuse (recall/fusion.py:267-342): ``methods`` = ordered
+    {name: {user: [(item, score), ...]}}, ``weights`` = {name: w}.  Plain
+    Python floats in the reference's operation order."""
+    # normalisation (:289-304)
+    normed = {}
+    if norm == "global":  # _global_normalize :100-134
+        allv = [s for d in methods.values() for lst in d.values() for _, s in lst]
+        gmin, gmax = (min(allv), max(allv)) if allv else (0.0, 0.0)
+        for m, d in methods.items():
+            normed[m] = {u: [(i, (s - gmin) / (gmax - gmin) if gmax > gmin else 1.0) for i, s in lst]
+                         for u, lst in d.items()}
+    elif norm == "z-score":  # _zscore_normalize :136-187 (numpy mean / std, sigmoid via np.exp)
+        for m, d in methods.items():
+            allv = [s for lst in d.values() for _, s in lst]
+            if not allv:
+                normed[m] = {}
+                continue
+            mu, sd = np.mean(allv), np.std(allv)
+            normed[m] = {u: [(i, 1.0 / (1.0 + np.exp(-((s - mu) / sd))) if sd > 0 else 0.5) for i, s in lst]
+                         for u, lst in d.items()}
+    else:  # _normalize_scores :71-98 per list
+        for m, d in methods.items():
+            out = {}
+            for u, lst in d.items():
+                if len(lst) <= 1:
+                    out[u] = [(lst[0][0], 1.0)] if lst else []
+                    continue
+                mn, mx = min(s for _, s in lst), max(s for _, s in lst)
+                out[u] = [(i, (s - mn) / (mx - mn) if mx > mn else 1.0) for i, s in lst]
+            normed[m] = out
+    users = set()
+    for d in normed.values():
+        users.update(d.keys())
+    res = {}
+    for u in users:
+        src = {}
+        for m, d in normed.items():  # _weighted_merge :189-265
+            if u not in d:
+                continue
+            w = weights.get(m, 1.0)
+            for r, (i, s) in enumerate(d[u]):
+                src.setdefault(i, []).append((w, s, r))
+        merged = {}
+        for i, ss in src.items():
+            if strategy == "weighted_sum":
+                merged[i] = sum(w * s for w, s, _ in ss)
+            elif strategy == "max_score":
+                merged[i] = max(w * s for w, s, _ in ss)
+            elif strategy == "harmonic_mean":
+                merged[i] = len(ss) / sum(1.0 / (w * s + 1e-8) for w, s, _ in ss)
+            elif strategy == "diversity_weighted":
+                merged[i] = sum(w * s for w, s, _ in ss) * (1 + len(ss) * 0.1)
+            elif strategy == "rrf":
+                merged[i] = sum(w / (60 + r) for w, _, r in ss)
+            else:
+                tw = sum(w for w, _, _ in ss)
+                merged[i] = sum(w * s for w, s, _ in ss) / tw if tw > 0 else 0
+        if remove_seen and user_history and u in user_history:
+            merged = {i: s for i, s in merged.items() if i not in user_history[u]}
+        res[u] = sorted(merged.items(), key=lambda x: x[1], reverse=True)[:topk]
+    return res

@@ -543,6 +543,71 @@ def gen_din_encode(tmp):
     print("din_encode_small: host encoding fixture")
 
 
+# --------------------------------------------------------------------------
+# RecallFusion.fuse (fusion.py:67-342), every strategy x normalisation
+# --------------------------------------------------------------------------
+def fusion_inputs():
+    """Synthetic recall dicts shaped like RecallPipeline's (itemcf with its
+    negative hot-fill scores, youtubednn, a third method), with overlaps,
+    repeated items inside a list, empty and one-entry lists, equal scores
+    (ties) and users present in only some methods."""
+    rng = np.random.default_rng(13)
+    users = (rng.permutation(400) * 5 + 1000).tolist()
+    pool = rng.permutation(3000) * 3 + 7
+    methods = {}
+    for name, n_u, scale in (("itemcf", 320, 3.0), ("youtubednn", 300, 1.0), ("usercf", 150, 0.5)):
+        res = {}
+        for u in rng.choice(users, n_u, replace=False).tolist():
+            L = int(rng.choice([0, 1, 2, 5, 20, 30, 30, 30]))
+            its = pool[rng.integers(0, 120, L)].tolist()  # small pool per user: overlaps and repeats
+            sc = np.round(rng.standard_normal(L) * scale, 2)  # rounding makes ties
+            if name == "itemcf" and L > 3:
+                sc[-2:] = [-(its[-2] % 50) - 100.0, -(its[-1] % 50) - 100.0]  # hot fill (:116-122)
+            if name == "youtubednn":
+                sc = sc.astype(np.float32).astype(np.float64)
+            res[u] = [(int(i), float(s)) for i, s in zip(its, sc)]
+        methods[name] = res
+    weights = {"itemcf": 1.0, "youtubednn": 0.8, "usercf": 0.5}
+    history = {u: set(pool[rng.integers(0, 120, 8)].tolist()) for u in users[:200]}
+    return methods, weights, history
+
+
+def _flat_dict(d):
+    keys = list(d.keys())
+    lens = [len(d[k]) for k in keys]
+    items = [t[0] for k in keys for t in d[k]]
+    scores = [t[1] for k in keys for t in d[k]]
+    return (np.array(keys, np.int64), np.concatenate([[0], np.cumsum(lens)]).astype(np.int64),
+            np.array(items, np.int64), np.array(scores, np.float64))
+
+
+def gen_fusion(tmp):
+    from src.utils.config import RecallConfig
+    from src.recall.fusion import RecallFusion
+
+    methods, weights, history = fusion_inputs()
+    out = {"methods": np.array(list(methods)), "weights": np.array([weights[m] for m in methods])}
+    for m, d in methods.items():
+        out[f"in::{m}::users"], out[f"in::{m}::offsets"], out[f"in::{m}::items"], out[f"in::{m}::scores"] = \
+            _flat_dict(d)
+    hu = list(history)
+    out["hist_users"] = np.array(hu, np.int64)
+    out["hist_offsets"] = np.concatenate([[0], np.cumsum([len(history[u]) for u in hu])]).astype(np.int64)
+    out["hist_items"] = np.array([i for u in hu for i in sorted(history[u])], np.int64)
+    cases = [(s, n, False) for s in ("weighted_sum", "weighted_avg", "max_score", "harmonic_mean",
+                                     "diversity_weighted", "rrf") for n in ("local", "global", "z-score")]
+    cases.append(("weighted_avg", "global", True))
+    for strat, norm, seen in cases:
+        f = RecallFusion(RecallConfig(_project_root=tmp), fusion_strategy=strat, normalize_method=norm)
+        for m, d in methods.items():
+            f.add_recall_result(m, d, weight=weights[m])
+        res = f.fuse(topk=30, user_history=history if seen else None, remove_seen=seen)
+        tag = f"out::{strat}::{norm}::{int(seen)}"
+        out[tag + "::users"], out[tag + "::offsets"], out[tag + "::items"], out[tag + "::scores"] = \
+            _flat_dict(res)
+    np.savez_compressed(os.path.join(HERE, "fusion_small.npz"), **out)
+
+
 def main():
     import_reference()
     tmp = tempfile.mkdtemp(prefix="nrk_golden_")
@@ -551,7 +616,15 @@ def main():
     gen_youtubednn(tmp)
     gen_din(tmp)
     gen_din_encode(tmp)
+    gen_embsim(tmp)
+    gen_fusion(tmp)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:  # regenerate selected fixtures: make_golden.py fusion embsim ...
+        import_reference()
+        tmp = tempfile.mkdtemp(prefix="nrk_golden_")
+        for name in sys.argv[1:]:
+            globals()["gen_" + name](tmp)
+    else:
+        main()
