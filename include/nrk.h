@@ -345,6 +345,66 @@ int nrk_fuse(const int64_t* offsets, int64_t n_users, const int32_t* item, const
              const int32_t* seen, int topk, int32_t* out_item, double* out_score, int32_t* out_cnt,
              nrk_stream_t stream);
 
+/* ---------------------------------------------------------------------- */
+/* Ranker context features                                                */
+/* ---------------------------------------------------------------------- */
+
+/* FeatureExtractor._extract_context_features
+ * (src/features/feature_extractor.py:440-723) for every (user, recalled
+ * item) row, then the fitted binning (_apply_binning :838-898) and context
+ * LabelEncoder codes (src/rank/DIN.py:330-353, :560-617).  Features per row,
+ * F = 1 + 3 * last_n + 6 (16 at last_n = 3), in feature_lists order:
+ *   score, (sim_i, time_diff_i, word_diff_i) i = 1..last_n, sim_max,
+ *   sim_mean, sim_min, sim_std, item_user_sim, recall_in_user_cat.
+ * Rows are processed in user groups (group_off / pair_pos); tables are
+ * indexed by dense user / item rows.  Outputs (either may be NULL):
+ * out_raw [n_rows, F] f64 (the reference's column values: float32 features
+ * exactly representable, NaN where the reference leaves NaN) and out_codes
+ * [n_rows, code_stride] int32 (spec[f] applied to feature f). */
+typedef struct {
+    int64_t n_groups;           /* user groups                                      */
+    const int64_t* group_off;   /* [n_groups + 1] into the grouped pair order       */
+    const int32_t* group_user;  /* [n_groups] user row (-1: no such user)           */
+    const int64_t* pair_pos;    /* [n_pairs] output row of grouped pair q (NULL: q) */
+    const int32_t* pair_item;   /* [n_rows] item row of output row (-1: unknown)    */
+    const double* pair_score;   /* [n_rows] recall score                            */
+    int32_t last_n;             /* history items used (config.last_N = 3), <= 4     */
+    int32_t code_stride;        /* row stride of out_codes (>= F)                   */
+    const int32_t* hist_last;   /* [n_users, last_n] last items, oldest first, -1 = unknown item */
+    const int32_t* hist_n;      /* [n_users] min(len, last_n); -1 = no history entry */
+    const int64_t* ucat_off;    /* [n_users + 1] */
+    const int32_t* ucat;        /* distinct categories of each user's whole history */
+    const float* user_yt;       /* [n_users, dy] YouTubeDNN user vectors, or NULL   */
+    const uint8_t* user_yt_ok;  /* [n_users] */
+    int64_t n_items;
+    const float* w2v;           /* [n_items, dw] article-id Word2Vec vectors        */
+    const uint8_t* w2v_ok;      /* [n_items] */
+    int32_t dw;
+    const double* content;      /* [n_items, dc] content embeddings (float64)       */
+    const uint8_t* content_flags; /* bit 0 row present, bit 1 f32 row not all zero */
+    int32_t dc;
+    const double* created;      /* [n_items] MinMax created time, NaN = missing     */
+    const int32_t* category;    /* [n_items] category, -1 = missing                 */
+    const float* item_yt;       /* [n_items, dy] YouTubeDNN item vectors            */
+    const uint8_t* item_yt_ok;  /* [n_items] */
+    int32_t dy;
+} nrk_ctx_tables;
+
+/* One feature's fitted encoding.  kind 0 (KBins-binned): NaN -> fill, bin =
+ * #(edges[k] <= value) over the inner edges, code = lut[bin] (0 past n_lut).
+ * kind 1 (unbinned): code = codes[k] where vals[k] == value, else 0. */
+typedef struct {
+    int32_t kind, n_edges, n_lut, n_vals;
+    double fill;
+    double edges[16];
+    double vals[32];
+    int32_t lut[32];
+    int32_t codes[32];
+} nrk_ctx_spec;
+
+int nrk_ctx_features(const nrk_ctx_tables* tables, const nrk_ctx_spec* spec, double* out_raw, int32_t* out_codes,
+                     nrk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -56,6 +56,7 @@ SIGNATURES = {
     "nrk_gather_rows": (INT, [P, I64, INT, P, I64, P, P]),
     "nrk_fuse_minmax": (INT, [P, I64, P, P]),
     "nrk_fuse": (INT, [P, I64, P, P, P, P, INT, P, INT, INT, F64, F64, P, P, P, P, INT, P, P, P, P]),
+    "nrk_ctx_features": (INT, [P, P, P, P, P]),
     "nrk_din_prep_bytes": (SZ, [INT]),
     "nrk_din_prepare": (INT, [P, INT, P, INT, I64, P, P]),
     "nrk_din_workspace_bytes": (SZ, [I64, INT, INT, INT, INT, INT, INT]),

@@ -449,10 +449,14 @@ def itemcf_recall(q_slot, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created, 
 
 
 def din_assemble(rec_rows, rec_scores, user_feat, item_feat, user_hist, hist_len, u0, nu, k_use=30, skip=1,
-                 n_ctx=16, ctx_bins=10, score_lo=-1.0, score_hi=1.0, seed=23, out=None):
+                 n_ctx=16, ctx_bins=10, score_lo=-1.0, score_hi=1.0, seed=23, out=None, validate=True,
+                 ctx_width=None):
     """DIN inputs of the recalled pairs of users [u0, u0 + nu) (nrk_din_assemble).
-    Returns dict user [P, Fu], item [P, Fi], hist [P, T, Fi], ctx [P, n_ctx],
-    mask [P, T] f32, cand [P] (item rows), P = nu * k_use."""
+    Returns dict user [P, Fu], item [P, Fi], hist [P, T, Fi], ctx [P, ctx_width]
+    (the first n_ctx columns filled: synthetic score / hash bins),
+    mask [P, T] f32, cand [P] (item rows), P = nu * k_use.  ``validate``
+    checks every index the kernel gathers (rec_rows, user_hist, hist_len);
+    callers that validated their resident tables once pass False."""
     _dev(rec_rows, rec_scores, user_feat, item_feat, user_hist, hist_len)
     n_users, k_in = rec_rows.shape
     _need(rec_rows, torch.int32, name="rec_rows")
@@ -464,13 +468,27 @@ def din_assemble(rec_rows, rec_scores, user_feat, item_feat, user_hist, hist_len
     Fu, Fi, T = user_feat.shape[1], item_feat.shape[1], user_hist.shape[1]
     if user_feat.shape[0] != n_users or user_hist.shape[0] != n_users:
         raise ValueError("user tables must have one row per recalled user")
+    if not (0 <= u0 and u0 + nu <= n_users):
+        raise ValueError("user range out of bounds")
+    if validate and nu:
+        n_items = item_feat.shape[0]
+        r = rec_rows[u0:u0 + nu]
+        if int(r.max()) >= n_items:
+            raise ValueError("rec_rows out of [0, n_items)")
+        if int(user_hist.min()) < 0 or int(user_hist.max()) >= n_items:
+            raise ValueError("user_hist rows out of [0, n_items)")
+        if int(hist_len.min()) < 0 or int(hist_len.max()) > T:
+            raise ValueError("hist_len out of [0, T]")
+    W = n_ctx if ctx_width is None else ctx_width
+    if n_ctx and W != n_ctx:
+        raise ValueError("ctx_width must equal n_ctx when the assembly fills the context block")
     P = nu * k_use
     dev = rec_rows.device
     if out is None:
         out = {"user": torch.empty((P, Fu), dtype=torch.int32, device=dev),
                "item": torch.empty((P, Fi), dtype=torch.int32, device=dev),
                "hist": torch.empty((P, T, Fi), dtype=torch.int32, device=dev),
-               "ctx": torch.empty((P, n_ctx), dtype=torch.int32, device=dev),
+               "ctx": torch.empty((P, W), dtype=torch.int32, device=dev),
                "mask": torch.empty((P, T), dtype=torch.float32, device=dev),
                "cand": torch.empty(P, dtype=torch.int32, device=dev)}
     _lib.call("nrk_din_assemble", _ptr(rec_rows), _ptr(rec_scores), n_users, k_in, int(skip), int(k_use),

@@ -18,6 +18,8 @@ Each function restates the reference (file:line cited) in numpy / C:
 * ``itemcf_recall``      -- ItemCFRecaller.recall, itemcf_recaller.py:56-129
 * ``din_forward``        -- Dice / ActivationUnit / DINModel.forward, DIN.py:29-286
 * ``fuse``               -- RecallFusion.fuse, recall/fusion.py:67-342
+* ``ctx_features``       -- FeatureExtractor._extract_context_features,
+                            features/feature_extractor.py:440-723
 
 Pinning: tests/test_oracle_golden.py checks every function against the golden
 fixtures produced by executing the reference (tests/golden/make_golden.py).
@@ -337,3 +339,78 @@ def fuse(methods, weights, strategy="weighted_avg", norm="local", topk=30, user_
             merged = {i: s for i, s in merged.items() if i not in user_history[u]}
         res[u] = sorted(merged.items(), key=lambda x: x[1], reverse=True)[:topk]
     return res
+
+
+def ctx_features(main_users, main_items, main_scores, user_history, w2v, content, created, ctype, user_yt=None,
+                 art_yt=None, last_n=3, emb_dim=64):
+    """FeatureExtractor._extract_context_features
+    (features/feature_extractor.py:440-723) restated in the reference's own
+    numpy operations, per user group.  main_* are the main_df columns (str
+    user / item ids, float64 scores); returns {feature: column}."""
+    import pandas as pd
+
+    n = len(main_items)
+    N = last_n
+    sim = np.full((n, N), np.nan, dtype=np.float32)
+    tdf = np.zeros((n, N), dtype=np.float32)
+    wdf = np.zeros((n, N), dtype=np.float32)
+    stats = np.full((n, 4), np.nan, dtype=np.float32)
+    ius = np.zeros(n, dtype=np.float32)
+    ric = np.zeros(n, dtype=np.int8)
+    ucats = {}
+    for u, h in user_history.items():  # :497-506
+        ucats[u] = {ctype[i] for i in h if i in ctype}
+    zid = np.zeros(emb_dim, dtype=np.float32)
+    zc = np.zeros(250, dtype=np.float32)
+    groups = pd.Series(np.arange(n)).groupby(pd.Series(main_users)).apply(lambda s: s.to_numpy())
+    items = np.asarray(main_items, dtype=object)
+    for u, rows in groups.items():  # :527-690
+        u = str(u)
+        if u not in user_history:
+            continue
+        hist = user_history[u][-N:]
+        rec = items[rows]
+        if user_yt is not None and art_yt is not None:
+            ue = user_yt.get(u)
+            if ue is not None:
+                ie = np.array([art_yt.get(i, zid) for i in rec], dtype=np.float32)
+                ius[rows] = ie @ ue
+        rid = np.array([w2v.get(i, zid) for i in rec], dtype=np.float32)
+        rc = np.array([content.get(i, zc) for i in rec], dtype=np.float32)
+        rt = np.array([created.get(i, np.nan) for i in rec], dtype=np.float32)
+        for k, h in enumerate(hist):
+            hid, hc, ht = w2v.get(h), content.get(h), created.get(h, np.nan)
+            s = rid @ hid if hid is not None else np.zeros(len(rows), dtype=np.float32)
+            if not np.isnan(ht):
+                t = np.abs(rt - ht)
+                t = np.where(np.isnan(t), 0, t)
+            else:
+                t = np.zeros(len(rows), dtype=np.float32)
+            if hc is not None:
+                w = np.linalg.norm(rc - hc[np.newaxis, :], axis=1)
+                w = np.where(np.any(rc != 0, axis=1), w, 0)
+            else:
+                w = np.zeros(len(rows), dtype=np.float32)
+            sim[rows, k] = s
+            tdf[rows, k] = t
+            wdf[rows, k] = w
+        us = sim[rows, :]
+        with np.errstate(all="ignore"):
+            import warnings
+
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                stats[rows, 0] = np.nanmax(us, axis=1)
+                stats[rows, 1] = np.nanmean(us, axis=1)
+                stats[rows, 2] = np.nanmin(us, axis=1)
+                stats[rows, 3] = np.nanstd(us, axis=1)
+        cats = ucats.get(u, set())
+        if cats:
+            ric[rows] = np.array([1 if ctype.get(i) in cats else 0 for i in rec], dtype=np.int8)
+    out = {"score": np.asarray(main_scores, np.float64)}
+    for k in range(N):
+        out[f"sim_{k + 1}"], out[f"time_diff_{k + 1}"], out[f"word_diff_{k + 1}"] = sim[:, k], tdf[:, k], wdf[:, k]
+    for k, f in enumerate(("sim_max", "sim_mean", "sim_min", "sim_std")):
+        out[f] = stats[:, k]
+    out["item_user_sim"], out["recall_in_user_cat"] = ius, ric
+    return out

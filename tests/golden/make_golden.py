@@ -608,6 +608,117 @@ def gen_fusion(tmp):
     np.savez_compressed(os.path.join(HERE, "fusion_small.npz"), **out)
 
 
+# --------------------------------------------------------------------------
+# Context features (feature_extractor.py:440-723), binning (:838-898),
+# context label encoders (DIN.py:560-617) and the dataset's codes (:330-353)
+# --------------------------------------------------------------------------
+CTX_FEATS = ["score", "sim_1", "time_diff_1", "word_diff_1", "sim_2", "time_diff_2", "word_diff_2",
+             "sim_3", "time_diff_3", "word_diff_3", "sim_max", "sim_mean", "sim_min", "sim_std",
+             "item_user_sim", "recall_in_user_cat"]
+
+
+def ctxfeat_inputs():
+    """Synthetic inputs of FeatureExtractor._extract_context_features: the
+    dicts load_data builds (str item ids), a train click log, and a recall
+    main_df.  Gaps on purpose: items missing from each dict, all-zero content
+    rows, users without history / without a YouTubeDNN vector, users with
+    fewer than last_N history items."""
+    import pandas as pd
+
+    rng = np.random.default_rng(31)
+    n_items, n_users, dw, dy = 600, 260, 64, 64  # dy = embedding_dim: the zero default (:523) is that wide
+    ids = [str(i * 7 + 3) for i in range(n_items)]
+    keep = lambda frac: [i for i in ids if rng.random() < frac]  # noqa: E731
+    w2v = {i: rng.standard_normal(dw).astype(np.float32) * 0.3 for i in keep(0.92)}
+    content = {i: rng.standard_normal(250).astype(np.float64) for i in keep(0.9)}
+    for i in list(content)[:12]:
+        content[i] = np.zeros(250)  # an all-zero content row (word_diff -> 0)
+    created = {i: np.float64(rng.random()) for i in keep(0.9)}
+    ctype = {i: int(rng.integers(0, 8)) for i in keep(0.95)}
+    art_yt = {i: rng.standard_normal(dy).astype(np.float32) for i in keep(0.9)}
+    users = [int(u) for u in rng.permutation(5000)[:n_users] + 10]
+    rows = []
+    for u in users[:220]:  # the last 40 users have no clicks (no history)
+        L = int(rng.integers(1, 9))
+        its = rng.integers(0, n_items, L)
+        ts = 1_507_000_000_000 + np.cumsum(rng.integers(1, 10_000, L))
+        rows += [(u, int(ids[i]), int(t)) for i, t in zip(its, ts)]
+    click = pd.DataFrame(rows, columns=["user_id", "click_article_id", "click_timestamp"])
+    user_yt = {str(u): rng.standard_normal(dy).astype(np.float32) for u in users if rng.random() < 0.85}
+    mrows = []
+    for u in users:
+        for i in rng.integers(0, n_items + 40, int(rng.integers(5, 31))):  # ids >= n_items: unknown items
+            iid = ids[i] if i < n_items else str(100_000 + int(i))
+            mrows.append((str(u), iid, float(np.round(rng.random(), 3))))
+    main_df = pd.DataFrame(mrows, columns=["user_id", "item_id", "score"])
+    return dict(w2v=w2v, content=content, created=created, ctype=ctype, art_yt=art_yt, user_yt=user_yt,
+                click=click, main_df=main_df)
+
+
+def gen_ctxfeat(tmp):
+    import types as _types
+
+    import pandas as pd
+
+    # gensim (Word2Vec) is not installed: a stand-in module satisfies the
+    # import; Word2Vec itself is never called -- the article-id vectors are
+    # an input here (_get_article_id_embeddings is replaced by the dict).
+    gm = _types.ModuleType("gensim")
+    gmm = _types.ModuleType("gensim.models")
+    gmm.Word2Vec = None
+    gm.models = gmm
+    sys.modules.setdefault("gensim", gm)
+    sys.modules.setdefault("gensim.models", gmm)
+    from src.utils.config import RecallConfig, RankConfig
+    from src.features.feature_extractor import FeatureExtractor
+    from src.rank.DIN import DINRanker, DINDataset
+
+    inp = ctxfeat_inputs()
+    fe = FeatureExtractor(RecallConfig(_project_root=tmp))
+    fe.train_click_df = inp["click"]
+    fe.main_df = inp["main_df"].copy()
+    fe.article_type_dict = inp["ctype"]
+    fe.article_content_emb_dict = inp["content"]
+    fe.article_created_time_dict = inp["created"]
+    fe.user_youtubednn_emb_dict = inp["user_yt"]
+    fe.article_youtubednn_emb_dict = inp["art_yt"]
+    fe._get_article_id_embeddings = lambda: inp["w2v"]
+    fe._extract_context_features()
+    assert fe.context_features == CTX_FEATS
+    raw = fe.main_df[CTX_FEATS].copy()
+    fe._apply_binning()
+    binned = fe.main_df[CTX_FEATS].copy()
+    ns = _types.SimpleNamespace(user_profile_dict={}, item_features_dict={}, main_df=fe.main_df,
+                                context_features=CTX_FEATS, user_profile_features=[], item_features=[],
+                                label_encoders={})
+    DINRanker._prepare_vocab_dicts(ns)
+    ds = DINDataset(fe.main_df, {}, {}, fe.user_history_dict, [], [], CTX_FEATS, label_col="score",
+                    label_encoders=ns.label_encoders)
+    codes = np.array([[ds[i]["context"][f] for f in CTX_FEATS] for i in range(len(fe.main_df))], np.int64)
+    out = {"ctx_feats": np.array(CTX_FEATS)}
+    for k in ("w2v", "content", "created", "ctype", "art_yt", "user_yt"):
+        d = inp[k]
+        out[f"in::{k}::keys"] = np.array(list(d.keys()))
+        out[f"in::{k}::vals"] = np.array(list(d.values()))
+    for c in ("user_id", "click_article_id", "click_timestamp"):
+        out[f"in::click::{c}"] = inp["click"][c].to_numpy(np.int64)
+    out["in::main::user_id"] = inp["main_df"]["user_id"].to_numpy().astype(str)
+    out["in::main::item_id"] = inp["main_df"]["item_id"].to_numpy().astype(str)
+    out["in::main::score"] = inp["main_df"]["score"].to_numpy(np.float64)
+    hu = list(fe.user_history_dict)
+    out["hist_users"] = np.array(hu)
+    out["hist_offsets"] = np.concatenate([[0], np.cumsum([len(fe.user_history_dict[u]) for u in hu])])
+    out["hist_items"] = np.array([i for u in hu for i in fe.user_history_dict[u]])
+    for f in CTX_FEATS:
+        out[f"raw::{f}"] = raw[f].to_numpy()
+        out[f"binned::{f}"] = binned[f].to_numpy()
+        if f in fe.discretizers:
+            out[f"edges::{f}"] = np.asarray(fe.discretizers[f].bin_edges_[0], np.float64)
+        out[f"classes::{f}"] = np.asarray(ns.label_encoders[f].classes_).astype(str)
+    out["codes"] = codes
+    np.savez_compressed(os.path.join(HERE, "ctxfeat_small.npz"), **out)
+
+
 def main():
     import_reference()
     tmp = tempfile.mkdtemp(prefix="nrk_golden_")
@@ -618,6 +729,7 @@ def main():
     gen_din_encode(tmp)
     gen_embsim(tmp)
     gen_fusion(tmp)
+    gen_ctxfeat(tmp)
 
 
 if __name__ == "__main__":

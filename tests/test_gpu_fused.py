@@ -110,3 +110,104 @@ def test_fused_recall_rank_vs_oracle(chunk):
         po, _, _ = oracle.din_forward(sd, a["user"][sl], a["item"][sl], a["hist"][sl], a["ctx"][sl], a["mask"][sl],
                                       feats, round_bf16=True)
         np.testing.assert_allclose(probs[sl], po, atol=TOL, rtol=0)
+
+
+def _ctx_world(rng, users, items, user_hist, hist_len, n_cat=12):
+    """Context tables over catalog rows / user rows (str keys for the oracle),
+    with gaps: items without a w2v vector / content row / created time, all-zero
+    content rows, users without history."""
+    I, U = len(items), len(users)
+    w2v = {str(i): (rng.standard_normal(64) * 0.3).astype(np.float32) for i in range(I) if rng.random() < 0.9}
+    content = {str(i): rng.standard_normal(250) for i in range(I) if rng.random() < 0.9}
+    for key in list(content)[:20]:
+        content[key] = np.zeros(250)
+    created = {str(i): np.float64(rng.random()) for i in range(I) if rng.random() < 0.9}
+    ctype = {str(i): int(rng.integers(0, n_cat)) for i in range(I)}
+    hist = {str(u): [str(x) for x in user_hist[u, :hist_len[u]]] for u in range(U) if hist_len[u] > 0}
+    user_yt = {str(u): users[u] for u in range(U)}
+    art_yt = {str(i): items[i] for i in range(I)}
+    return w2v, content, created, ctype, hist, user_yt, art_yt
+
+
+def test_fused_with_context_features():
+    """Config-5 path with the reference's context features: the fused
+    pipeline's codes are the fitted spec applied to nrk_ctx_features' raw
+    values, those raw values match the oracle restatement of
+    feature_extractor.py:440-723 (1e-5; exact for the float64 paths), and the
+    DIN probabilities match the oracle on the same codes (1e-5)."""
+    import warnings
+
+    from nrk import ops
+    from nrk.features import CtxSpec, CtxTables, ctx_feature_names, ctx_features
+    from nrk.pipeline import FusedRecallRank
+    from test_ctxfeat_oracle import apply_spec_host
+    from test_gpu_din import synth_model
+
+    warnings.simplefilter("ignore")
+    rng = np.random.default_rng(41)
+    U, I, D, T, k = 700, 1500, 64, 50, 30
+    vu, vi, vc = [50, 300, 7, 2000, 90], [60, 900, 5000, 70], [24] * 16
+    users, items, user_feat, item_feat, user_hist, hist_len = _world(rng, U, I, D, T, vu, vi)
+    w2v, content, created, ctype, hist, user_yt, art_yt = _ctx_world(rng, users, items, user_hist, hist_len)
+    tables = CtxTables([str(i) for i in range(I)], [str(u) for u in range(U)], w2v, content, created, ctype, hist,
+                       user_yt=user_yt, item_yt=art_yt)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    so, ro = oracle.ip_topk(users, items, k + 1)
+    names = ctx_feature_names()
+    pu = np.repeat(np.arange(U), k).astype(np.int32)
+    pi = ro[:, 1:].reshape(-1).astype(np.int32)
+    ps = so[:, 1:].reshape(-1).astype(np.float64)
+    raw, _ = ctx_features(tables, d(pu), d(pi), d(ps))
+    raw = raw.cpu().numpy()
+    exp = oracle.ctx_features([str(u) for u in pu], [str(i) for i in pi], ps, hist, w2v, content, created, ctype,
+                              user_yt, art_yt)
+    for j, f in enumerate(names):
+        if f.startswith("sim") or f == "item_user_sim":
+            np.testing.assert_allclose(raw[:, j], exp[f], rtol=1e-5, atol=1e-5, equal_nan=True, err_msg=f)
+        else:
+            assert np.array_equal(raw[:, j], exp[f].astype(np.float64), equal_nan=True), f
+    spec = CtxSpec.fit({f: (raw[:, j].astype(np.float32) if f != "score" else raw[:, j]) for j, f in enumerate(names)},
+                       names)
+    codes = np.stack([apply_spec_host(spec.specs[j], raw[:, j]) for j in range(len(names))], 1)
+    sd, feats = synth_model(rng, vu, vi, vc)
+    p = ops.DinParams(sd, *feats, table_dtype="bf16")
+    fused = FusedRecallRank(ops.Catalog(d(items)), p, d(user_feat), d(item_feat), d(user_hist), d(hist_len),
+                            k=k, chunk_users=2048, ctx=(tables, spec))
+    s, r = fused.recall(d(users))
+    assert np.array_equal(r.cpu().numpy().astype(np.int64), ro)
+    probs, cand = fused.rank(s, r)
+    probs = probs.cpu().numpy()
+    a = ref_assemble(ro.astype(np.int32), so, user_feat, item_feat, user_hist, hist_len, 0, U, k, 1, 16,
+                     10, -1.0, 1.0, 23)
+    B = 4096
+    for b0 in range(0, U * k, B):
+        sl = slice(b0, min(b0 + B, U * k))
+        po, _, _ = oracle.din_forward(sd, a["user"][sl], a["item"][sl], a["hist"][sl], codes[sl], a["mask"][sl],
+                                      feats, round_bf16=True)
+        np.testing.assert_allclose(probs[sl], po, atol=TOL, rtol=0)
+
+
+def test_fused_rejects_bad_tables():
+    from nrk import ops
+    from nrk.pipeline import FusedRecallRank
+    from test_gpu_din import synth_model
+
+    rng = np.random.default_rng(3)
+    U, I, D, T = 100, 300, 32, 50
+    vu, vi, vc = [50, 300, 7, 2000, 90], [60, 900, 5000, 70], [11] * 16
+    users, items, user_feat, item_feat, user_hist, hist_len = _world(rng, U, I, D, T, vu, vi)
+    sd, feats = synth_model(rng, vu, vi, vc)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    p = ops.DinParams(sd, *feats, table_dtype="bf16")
+    bad_hist = user_hist.copy()
+    bad_hist[5, 3] = I  # out of the item table
+    with pytest.raises(ValueError):
+        FusedRecallRank(ops.Catalog(d(items)), p, d(user_feat), d(item_feat), d(bad_hist), d(hist_len))
+    bad_feat = item_feat.copy()
+    bad_feat[7, 2] = 5000  # == vocab
+    with pytest.raises(ValueError):
+        FusedRecallRank(ops.Catalog(d(items)), p, d(user_feat), d(bad_feat), d(user_hist), d(hist_len))
+    bad_len = hist_len.copy()
+    bad_len[0] = T + 1
+    with pytest.raises(ValueError):
+        FusedRecallRank(ops.Catalog(d(items)), p, d(user_feat), d(item_feat), d(user_hist), d(bad_len))
