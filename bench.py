@@ -214,6 +214,47 @@ def run_itemcf(args, device):
     return out
 
 
+def fused_ctx_tables(users, items, user_hist, hist_len, device, gi, g, n_cat=461):
+    """Config-5 context tables in HBM (synthetic, Tianchi-shaped): article-id
+    Word2Vec vectors [I, 64] f32, 250-d float64 content rows (5% missing, 1%
+    all zero), MinMax created times (5% missing), categories, each user's
+    last-3 history rows + the categories of the whole history, and the
+    recall's own user / item vectors for item_user_sim.  Returns (tables,
+    None): the spec is fitted on the first chunk."""
+    from nrk.features import CtxTables
+
+    I, U, T = items.shape[0], users.shape[0], user_hist.shape[1]
+    w2v = (torch.randn(I, 64, device=device, generator=gi) * 0.3).contiguous()
+    content = torch.randn(I, 250, device=device, dtype=torch.float64, generator=gi)
+    present = torch.rand(I, device=device, generator=gi) >= 0.05
+    zero = torch.rand(I, device=device, generator=gi) < 0.01
+    content[~present | zero] = 0.0
+    flags = (present.to(torch.uint8) | ((present & ~zero).to(torch.uint8) << 1)).contiguous()
+    created = torch.rand(I, device=device, dtype=torch.float64, generator=gi)
+    created[torch.rand(I, device=device, generator=gi) < 0.05] = float("nan")
+    category = torch.randint(0, n_cat, (I,), device=device, generator=gi, dtype=torch.int32)
+    N = 3
+    L = hist_len.long()
+    t = torch.arange(N, device=device)
+    # the last min(L, N) history rows, oldest first (user_history_dict[u][-N:]), -1 after
+    start = (L - N).clamp(min=0)
+    idx = (start[:, None] + t[None, :]).clamp(max=T - 1)
+    keep = t[None, :] < L.clamp(max=N)[:, None]
+    hl = torch.where(keep, torch.gather(user_hist.long(), 1, idx), torch.full_like(idx, -1)).to(torch.int32).contiguous()
+    hn = torch.where(L > 0, L.clamp(max=N), torch.full_like(L, -1)).to(torch.int32).contiguous()
+    valid = torch.arange(T, device=device)[None, :] < L[:, None]
+    ucat = category[user_hist.long()][valid].contiguous()
+    uoff = torch.zeros(U + 1, dtype=torch.int64, device=device)
+    uoff[1:] = torch.cumsum(L, 0)
+    ones_u = torch.ones(U, dtype=torch.uint8, device=device)
+    ones_i = torch.ones(I, dtype=torch.uint8, device=device)
+    tensors = {"w2v": w2v, "w2v_ok": ones_i, "content": content.contiguous(), "flags": flags, "created": created,
+               "category": category, "hist_last": hl, "hist_n": hn, "ucat_off": uoff,
+               "ucat": ucat if ucat.numel() else torch.zeros(1, dtype=torch.int32, device=device),
+               "user_yt": users, "user_yt_ok": ones_u, "item_yt": items, "item_yt_ok": ones_i}
+    return CtxTables.from_device(tensors, last_n=N), None
+
+
 def run_fused(args, device, rank, world, dist):
     """BASELINE config 5 (10M users x 5M items, D=128, fused recall -> DIN),
     weak-scaled: every rank recalls its own 10M / N users (--fused-users
@@ -238,7 +279,29 @@ def run_fused(args, device, rank, world, dist):
     hist_len = rnd(T + 1, (U,), g)
     sd, feats, _, _ = din_workload(101, 64, T, "cpu")
     p = ops.DinParams(sd, *feats, table_dtype="bf16", device=device)
-    fused = FusedRecallRank(cat, p, user_feat, item_feat, user_hist, hist_len, k=k)
+    ctx = None
+    if not args.fused_hash_ctx:
+        ctx = fused_ctx_tables(users, items, user_hist, hist_len, device, gi, g)
+    if ctx is None:
+        fused = FusedRecallRank(cat, p, user_feat, item_feat, user_hist, hist_len, k=k)
+    else:
+        # fit the binning + label codes on the first chunk's raw features
+        # (the reference fits on its whole main_df, offline; untimed here)
+        from nrk.features import CtxSpec, ctx_feature_names, ctx_features
+
+        n0 = min(U, 4096)
+        s0, r0 = ops.ip_topk(users[:n0].contiguous(), cat, k + 1)
+        pi = r0[:, 1:].reshape(-1).contiguous()
+        ps = s0[:, 1:].to(torch.float64).reshape(-1).contiguous()
+        goff = torch.arange(0, (n0 + 1) * k, k, dtype=torch.int64, device=device)
+        gus = torch.arange(0, n0, dtype=torch.int32, device=device)
+        raw, _ = ctx_features(ctx[0], None, pi, ps, groups=(goff, gus, None))
+        names = ctx_feature_names()
+        rawn = raw.cpu().numpy()
+        cols = {f: (rawn[:, j] if f == "score" else rawn[:, j].astype(np.float32)) for j, f in enumerate(names)}
+        cols["recall_in_user_cat"] = rawn[:, -1].astype(np.int8)
+        spec = CtxSpec.fit(cols, names)
+        fused = FusedRecallRank(cat, p, user_feat, item_feat, user_hist, hist_len, k=k, ctx=(ctx[0], spec))
     probs = torch.empty(U * k, dtype=torch.float32, device=device)
 
     def step(ev=None):
@@ -278,7 +341,10 @@ def run_fused(args, device, rank, world, dist):
         "unit": "scored pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp16 screen + fp64 exact recall; fp32-class DIN, bf16 tables",
-        "data": "synthetic: random unit user / item vectors, uniform feature indices, random-init DIN",
+        "data": ("synthetic: random unit user / item vectors, uniform feature indices, random-init DIN, "
+                 + ("hash-bin context" if args.fused_hash_ctx else
+                    "context features computed on the device from synthetic w2v / content / created / "
+                    "category tables (nrk_ctx_features)")),
         "config": {"workload": "BASELINE config 5: fused recall (exact top-31 IP, D=128) -> DIN rank of the "
                                "30 recalled items per user", "users_per_gpu": U, "items": I, "dim": D, "topk": k,
                    "seq_len": T, "dice_batch": 4096, "parallelism": f"users-sharded x{world}"},
@@ -500,6 +566,8 @@ def main(argv=None):
                     help="BASELINE config 5 instead: fused recall -> DIN, 10M users / N per rank x 5M items, D=128")
     ap.add_argument("--fused-users", type=int, default=0, help="users per rank for --fused (default 10M / N)")
     ap.add_argument("--fused-items", type=int, default=5_000_000)
+    ap.add_argument("--fused-hash-ctx", action="store_true",
+                    help="config 5 with the synthetic hash-bin context instead of the real context features")
     ap.add_argument("--shard", choices=["users", "catalog"], default="users",
                     help="N>1 layout: users-sharded (weak scaling, no collective) or "
                          "catalog-sharded (BASELINE config 4: all_to_all of shard top-k + merge)")
