@@ -144,6 +144,102 @@ def cpu_baseline_recall(users_np, items_np, k, sample, threads, seconds):
     return done * (k - 1) / dt, dt, done
 
 
+def cpu_baseline_recall_gemm(users_np, items_np, k, sample, seconds):
+    """batched GEMM + top-k on torch-CPU with every host
+    thread, chunks of ``sample`` users until ``seconds`` of CPU work."""
+    it = torch.from_numpy(items_np)
+    torch.topk(torch.from_numpy(users_np[:8]) @ it.T, k, dim=1)  # warm
+    done, dt = 0, 0.0
+    while dt < seconds and done < len(users_np):
+        q = torch.from_numpy(users_np[done:done + sample])
+        t0 = time.perf_counter()
+        torch.topk(q @ it.T, k, dim=1)
+        dt += time.perf_counter() - t0
+        done += q.shape[0]
+    return done * (k - 1) / dt, dt, done
+
+
+def host_info():
+    """nproc, CPU model, torch threads, GPU count."""
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model, "torch_threads": torch.get_num_threads(),
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "gpus_visible": torch.cuda.device_count()}
+
+
+def run_plugins(args, device, u_vec, item_vec, sd, feats):
+    """Plugin-level throughput: the drop-in entry points a reference user
+    calls, timed end to end on the host clock (host prep, H2D, kernels, D2H,
+    building the returned Python containers):
+      * YoutubeDNNRecaller.batch_recall(all 250k users, topk=30) -> the
+        Dict[user, List[(item, score)]] of recall/base.py:24-40;
+      * DINRanker.predict() over a 675,653-row main_df (object rows, ids
+        found in the dicts), batches of 4096 -> np.ndarray probabilities
+        (DIN.py:1219-1283), encoding included (DinEncoder + nrk_gather_rows).
+    Setup (dicts, label encoders, tables) is untimed, as the reference's
+    set_data / load_model are."""
+    import pandas as pd
+
+    from nrk.config import RankConfig
+    from nrk.rank.din import DINRanker
+    from nrk.recall.youtubednn_recaller import YoutubeDNNRecaller
+
+    out = {}
+    U, I = u_vec.shape[0], item_vec.shape[0]
+    rec = YoutubeDNNRecaller.from_embeddings(u_vec, item_vec, np.arange(U) * 3 + 1, np.arange(I) * 7 + 11,
+                                             device=device)
+    uids = (np.arange(U) * 3 + 1).tolist()
+    rec.batch_recall(uids[:1000], topk=30)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = rec.batch_recall(uids, topk=30)
+    dt = time.perf_counter() - t0
+    out["batch_recall"] = {"value": round(sum(len(v) for v in res.values()) / dt, 1), "unit": "recalled pairs/s",
+                           "users": U, "seconds": round(dt, 3)}
+    del res
+
+    class _Enc:
+        def __init__(self, c):
+            self.classes_ = c
+
+    rng = np.random.default_rng(5)
+    n, T = args.din_samples, 50
+    uf, itf, cf = feats
+    NU, NI = 200_000, 300_000
+    uv = [rng.integers(0, v - 1, NU) for v in DIN_VOCAB_U]
+    iv = [rng.integers(0, v - 1, NI) for v in DIN_VOCAB_I]
+    upd = {str(u): {f: float(uv[j][u]) for j, f in enumerate(uf)} for u in range(NU)}
+    ifd = {str(i): {f: int(iv[j][i]) for j, f in enumerate(itf)} for i in range(NI)}
+    L = np.minimum(rng.geometric(1 / 8, NU), 200)
+    uhd = {str(u): [str(x) for x in rng.integers(0, NI, L[u])] for u in range(NU)}
+    enc = {f: _Enc(np.unique(uv[j].astype(float))) for j, f in enumerate(uf)}
+    enc.update({f: _Enc(np.unique(iv[j])) for j, f in enumerate(itf)})
+    enc.update({f: _Enc(np.arange(DIN_VOCAB_C - 1)) for f in cf})
+    df = pd.DataFrame({"user_id": rng.integers(0, NU, n).astype(str), "item_id": rng.integers(0, NI, n).astype(str)})
+    for f in cf:
+        df[f] = rng.integers(0, DIN_VOCAB_C - 1, n)
+    cfg = RankConfig()
+    cfg.din_seq_max_len, cfg.batch_size = T, 4096
+    rk = DINRanker(cfg, device=device, table_dtype="bf16").set_data(df, upd, ifd, uhd, uf, itf, cf, enc)
+    rk.load_model(sd)
+    rk.predict()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    probs = rk.predict()
+    dt = time.perf_counter() - t0
+    assert probs.shape == (n,) and np.isfinite(probs).all()
+    out["din_predict"] = {"value": round(n / dt, 1), "unit": "DIN scored pairs/s (incl. encoding)", "samples": n,
+                          "seconds": round(dt, 3)}
+    return out
+
+
 def run_itemcf(args, device):
     """Informational ItemCF leg: the whole similarity
     (nrk_itemcf_sim, item_cf.py:17-89), per-item top-20 (A9) and the recall of
@@ -461,20 +557,22 @@ def run_din(args, device, rank, world):
 
         m = args.din_cpu_sample
         sdn = {k: v.numpy() for k, v in sd.items()}
+        model = oracle.DinTorchCPU(sdn, feats, round_bf16=True)
+        tt = {k: torch.from_numpy(v) if k == "mask" else torch.from_numpy(v.astype(np.int64)) for k, v in enc.items()}
         cdt, nb = 0.0, 0
         while cdt < args.cpu_seconds and (nb + 1) * m <= n:  # whole B-sample batches, like the reference
-            sl = {k: v[nb * m:(nb + 1) * m] for k, v in enc.items()}
+            sl = {k: v[nb * m:(nb + 1) * m] for k, v in tt.items()}
             t1 = time.perf_counter()
-            pb, _, _ = oracle.din_forward(sdn, sl["user"], sl["item"], sl["hist"], sl["ctx"], sl["mask"], feats,
-                                          round_bf16=True)
+            model(sl["user"], sl["item"], sl["hist"], sl["ctx"], sl["mask"])
             cdt += time.perf_counter() - t1
-            if nb == 0:
-                po = pb
             nb += 1
+        sl0 = {k: v[:m] for k, v in enc.items()}
+        po, _, _ = oracle.din_forward(sdn, sl0["user"], sl0["item"], sl0["hist"], sl0["ctx"], sl0["mask"], feats,
+                                      round_bf16=True)
         out["cpu_baseline"] = {"value": round(nb * m / cdt, 1), "unit": "DIN scored pairs/s",
                                "cores": torch.get_num_threads(), "kind": "port",
-                               "sample": f"{nb} batches x {m} samples of the same workload, numpy fp32 forward "
-                                         f"(oracle/oracle.py), {cdt:.1f}s"}
+                               "sample": f"{nb} batches x {m} samples of the same workload, torch-CPU eval forward "
+                                         f"of DINModel's formulation (oracle.DinTorchCPU, fp32), {cdt:.1f}s"}
         gp = ops.din_forward(p, *(dev[k][:m] for k in ("user", "item", "hist", "ctx", "mask")), workspace=ws)
         err = float(np.abs(gp.cpu().numpy() - po).max())
         log(f"DIN spot-check vs oracle ({m} samples): max |dp| = {err:.2e}")
@@ -562,6 +660,7 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-din", action="store_true")
     ap.add_argument("--no-itemcf", action="store_true", help="skip the informational ItemCF leg")
+    ap.add_argument("--no-plugins", action="store_true", help="skip the plugin-level (end-to-end API) leg")
     ap.add_argument("--fused", action="store_true",
                     help="BASELINE config 5 instead: fused recall -> DIN, 10M users / N per rank x 5M items, D=128")
     ap.add_argument("--fused-users", type=int, default=0, help="users per rank for --fused (default 10M / N)")
@@ -713,7 +812,12 @@ def main(argv=None):
                                         args.cpu_sample, threads, args.cpu_seconds)
         cpu = {"value": round(v, 1), "unit": "recalled pairs/s", "cores": threads, "kind": "port",
                "sample": f"first {nu} of the same {U} users x {I} items, exact fp64 top-{K} scan "
-                         f"(oracle/nrk_oracle.c, {dt:.1f}s)"}
+                         f"(oracle/nrk_oracle.c, the reference's per-user nq=1 shape, {dt:.1f}s)"}
+        vg, dtg, nug = cpu_baseline_recall_gemm(u.cpu().numpy(), item_vec.cpu().numpy(), K, args.cpu_sample,
+                                                args.cpu_seconds / 2)
+        cpu["variants"] = [{"value": round(vg, 1), "unit": "recalled pairs/s", "cores": torch.get_num_threads(),
+                            "kind": "port", "sample": f"first {nug} users, batched fp32 GEMM + torch.topk on "
+                                                      f"torch-CPU ({dtg:.1f}s; fp32 scores, not exact ties)"}]
         # correctness spot check of the timed outputs against the oracle
         from oracle import oracle
 
@@ -725,6 +829,13 @@ def main(argv=None):
     if not args.no_din:
         din = run_din(args, device, rank, world)
         log(f"DIN: {din['value']:.0f} pairs/s, {din['ms_per_pass']:.1f} ms/pass, device {din['roofline']['kernel_ms']:.3f} ms")
+
+    plugins = None
+    if world == 1 and not args.no_plugins:
+        sd_p, feats_p, _, _ = din_workload(101, 64, 50, "cpu")
+        plugins = run_plugins(args, device, step(), item_vec, sd_p, feats_p)
+        log(f"plugins: batch_recall {plugins['batch_recall']['value']:.0f} pairs/s, "
+            f"DINRanker.predict {plugins['din_predict']['value']:.0f} pairs/s")
 
     itemcf = None
     if world == 1 and not args.no_itemcf:
@@ -746,7 +857,8 @@ def main(argv=None):
                                        else f"users-sharded x{world}" if world > 1 else "single")},
             "phase_ms": {"tower": round(tower_ms, 4), "screen": round(screen_ms, 4),
                          "finish": round(finish_ms, 4)},
-            "roofline": roofline, "cpu_baseline": cpu, "din": din, "itemcf": itemcf,
+            "roofline": roofline, "cpu_baseline": cpu, "din": din, "itemcf": itemcf, "plugins": plugins,
+            "host": host_info(),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

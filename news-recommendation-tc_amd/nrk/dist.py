@@ -162,6 +162,17 @@ def _default_reduce(keys, slots, w, n_items, cnt):
     return ops.itemcf_reduce(keys, slots, w, n_items, cnt)
 
 
+SLOT_LIMIT = (1 << 31) - (1 << 16)  # int32 global slots, minus the radix sort's tile slack
+
+
+def check_slot_range(total_pairs: int):
+    """The pair tuples carry int32 GLOBAL slots (the first-encounter order):
+    the whole log's ordered pair count must stay below 2^31 (minus the sort
+    tile), or slots would wrap and break the reference's dict order."""
+    if total_pairs >= SLOT_LIMIT:
+        raise ValueError(f"{total_pairs} ordered pairs: int32 global slots need < {SLOT_LIMIT}")
+
+
 def itemcf_sim_sharded(offsets, items, ts, created, n_items: int, group=None, pairs=None, reduce=None):
     """ItemCF similarity (item_cf.py:17-89) with users sharded over the ranks
     of ``group``.  ``offsets`` / ``items`` / ``ts`` are THIS rank's users (a
@@ -182,8 +193,10 @@ def itemcf_sim_sharded(offsets, items, ts, created, n_items: int, group=None, pa
         all_tot = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
         dist.all_gather(all_tot, tot, group=group)
         base = int(sum(int(t) for t in all_tot[:rank]))
+        check_slot_range(sum(int(t) for t in all_tot))
     else:
         base = 0
+        check_slot_range(n_local)
     keys, slots, w, cnt = pairs(offsets, items, ts, created, n_items, base)
     if world == 1:
         return reduce(keys, slots, w, n_items, cnt)

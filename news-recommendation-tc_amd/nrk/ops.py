@@ -530,6 +530,8 @@ def itemcf_pairs(offsets, items, ts, created, n_items, slot_base=0, loc_alpha=1.
     pair_off = torch.empty(n_users + 1, dtype=torch.int64, device=dev)
     _lib.call("nrk_itemcf_pair_offsets", _ptr(offsets), n_users, _ptr(pair_off), _stream())
     n = int(pair_off[-1])
+    if int(slot_base) < 0 or int(slot_base) + n >= (1 << 31) - (1 << 16):
+        raise ValueError("slot_base + pairs must stay below 2^31 (int32 global slots)")
     keys = torch.empty(n, dtype=torch.int64, device=dev)
     slots = torch.empty(n, dtype=torch.int32, device=dev)
     w = torch.empty(n, dtype=torch.float64, device=dev)

@@ -110,7 +110,19 @@ class ItemCFRecaller(BaseRecaller):
             nb_vals[rp, :cols_raw.shape[1]] = np.where(valid, vals, 0.0)
             nb_cnt[rp] = cnt
         ct = self.item_created_time_dict
-        created = np.fromiter((float(ct.get(int(x), 0.0)) for x in ids), np.float64, len(ids))
+        created = np.fromiter((float(ct.get(int(x), np.nan)) for x in ids), np.float64, len(ids))
+        # recall() reads created[i] and created[j] for every history item i with
+        # a neighbour j (itemcf_recaller.py:92-96): those must exist, as there
+        hist_rows = np.searchsorted(ids, hist) if len(hist) else np.zeros(0, np.int64)
+        looked = np.zeros(len(ids), bool)
+        hr = hist_rows[nb_cnt[hist_rows] > 0] if len(hist_rows) else hist_rows
+        looked[hr] = True
+        nbr = nb_cols[hr][nb_cols[hr] >= 0] if len(hr) else np.zeros(0, np.int64)
+        looked[nbr] = True
+        missing = looked & np.isnan(created)
+        if missing.any():
+            raise KeyError(int(ids[np.argmax(missing)]))
+        created = np.where(np.isnan(created), 0.0, created)  # hot-fill only items: never read
         self._ids = ids
         self._slot = {u: k for k, u in enumerate(users)}
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(d)  # noqa: E731

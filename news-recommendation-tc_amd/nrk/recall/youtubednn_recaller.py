@@ -58,8 +58,9 @@ class YoutubeDNNRecaller(BaseRecaller):
         """Wrap already-extracted embeddings (the state after
         _extract_embeddings, youtubednn_recaller.py:425-495)."""
         self = cls(config, device)
-        ue = torch.as_tensor(np.asarray(user_embeddings, np.float32)).to(self.device).contiguous()
-        ie = torch.as_tensor(np.asarray(item_embeddings, np.float32)).to(self.device).contiguous()
+        dev = lambda x: (x.to(self.device, torch.float32) if torch.is_tensor(x)  # noqa: E731
+                         else torch.as_tensor(np.asarray(x, np.float32)).to(self.device)).contiguous()
+        ue, ie = dev(user_embeddings), dev(item_embeddings)
         self._set_state(ue, ie, _as_mapping_array(user_index_2_rawid),
                         _as_mapping_array(item_index_2_rawid))
         return self

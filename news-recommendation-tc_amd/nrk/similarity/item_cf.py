@@ -52,15 +52,20 @@ class ItemCFSimilarity(BaseSimilarityCalculator):
         c = self.config
         ids, dense = np.unique(items_raw, return_inverse=True)
         L = np.diff(offsets)
-        in_pairs = np.repeat(L >= 2, L)
-        created = np.empty(len(ids), np.float64)
-        for n, raw in enumerate(ids.tolist()):
-            val = item_created_time_dict.get(raw)
-            if val is None:
-                if in_pairs[dense == n].any():
-                    raise KeyError(raw)  # the reference's item_created_time_dict[i] lookup fails too
-                val = 0.0
-            created[n] = val
+        # item_created_time_dict[i] is read only for pairs i != j (item_cf.py:47-64):
+        # an item needs a created time iff its user's list holds >= 2 distinct items
+        uid = np.repeat(np.arange(len(L)), L)
+        distinct = np.zeros(len(L), np.int64)
+        if len(dense):
+            up = np.unique(uid.astype(np.int64) * (len(ids) + 1) + dense)
+            distinct = np.bincount(up // (len(ids) + 1), minlength=len(L))
+        needs = np.zeros(len(ids), bool)
+        needs[dense[np.repeat(distinct >= 2, L)]] = True
+        created = np.array([item_created_time_dict.get(raw, np.nan) for raw in ids.tolist()], np.float64)
+        missing = needs & np.isnan(created)
+        if missing.any():
+            raise KeyError(ids[np.argmax(missing)].item())  # the reference's dict lookup fails too
+        created = np.where(np.isnan(created), 0.0, created)  # never read by any pair
         # row order: first click of each item in the CSR walk (i2i_sim.setdefault, item_cf.py:44)
         _, first_pos = np.unique(dense, return_index=True)
         row_order = np.argsort(first_pos, kind="stable")

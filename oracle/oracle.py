@@ -270,6 +270,53 @@ def din_forward(sd, user, item, hist, ctx, mask, feats, round_bf16=False):
     return prob, logit, w
 
 
+class DinTorchCPU:
+    """torch-CPU eval forward in the reference's own formulation
+    (DINModel.forward, DIN.py:214-286: nn.Embedding lookups, ActivationUnit
+    Linear(512->36) on [k, q, q-k, q*k] + Dice + Linear(36->1) * mask, the
+    weighted history sum, Linear/Dice MLP, sigmoid) -- the CPU baseline of
+    BASELINE.md §3 for config 3, run on pre-encoded int tensors with every
+    host thread torch has.  Bench-only (cpu_baseline leg)."""
+
+    def __init__(self, sd, feats, round_bf16=False):
+        import torch
+
+        uf, itf, cf = feats
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(bf16_round(a) if round_bf16 else a, np.float32))  # noqa
+        self.U = [t(sd[f"user_profile_embedding_dict.{f}.weight"]) for f in uf]
+        self.I = [t(sd[f"item_embedding_dict.{f}.weight"]) for f in itf]
+        self.C = [t(sd[f"context_embedding_dict.{f}.weight"]) for f in cf]
+        g = lambda k: torch.from_numpy(np.ascontiguousarray(sd[k], np.float32))  # noqa: E731
+        self.a0w, self.a0b = g("activation_unit.mlp.0.weight"), g("activation_unit.mlp.0.bias")
+        self.a2w, self.a2b = g("activation_unit.mlp.2.weight"), g("activation_unit.mlp.2.bias")
+        self.m = [(g(f"mlp.{i}.weight"), g(f"mlp.{i}.bias")) for i in (0, 2, 4)]
+
+    @staticmethod
+    def _dice(x):
+        import torch
+
+        mean, std = x.mean(0), x.std(0)
+        p = torch.sigmoid((x - mean) / (std + 1e-8))
+        return p * x + (1 - p) * 0.01 * x
+
+    def __call__(self, user, item, hist, ctx, mask):
+        import torch
+        import torch.nn.functional as F
+
+        with torch.no_grad():
+            u = torch.cat([E[user[:, n]] for n, E in enumerate(self.U)], 1)
+            q = torch.cat([E[item[:, n]] for n, E in enumerate(self.I)], 1)
+            k = torch.cat([E[hist[:, :, n]] for n, E in enumerate(self.I)], 2)
+            c = torch.cat([E[ctx[:, n]] for n, E in enumerate(self.C)], 1)
+            qq = q.unsqueeze(1).expand_as(k)
+            h = self._dice(F.linear(torch.cat([k, qq, qq - k, qq * k], -1), self.a0w, self.a0b))
+            w = F.linear(h, self.a2w, self.a2b) * mask.unsqueeze(-1)
+            x = torch.cat([u, c, q, (w * k).sum(1)], 1)
+            x = self._dice(F.linear(x, *self.m[0]))
+            x = self._dice(F.linear(x, *self.m[1]))
+            return torch.sigmoid(F.linear(x, *self.m[2]).squeeze(-1))
+
+
 def bf16_round(x):
     """Round-to-nearest-even fp32 -> bf16 -> fp32 (finite inputs)."""
     b = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)

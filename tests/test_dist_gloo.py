@@ -252,3 +252,14 @@ def test_itemcf_users_sharded_gloo(world):
     order = np.argsort(gf, kind="stable")  # first-encounter order = the oracle's
     assert np.array_equal(gi[order], oi) and np.array_equal(gj[order], oj)
     np.testing.assert_allclose(gv[order], ov, rtol=1e-12, atol=0)
+
+
+def test_itemcf_slot_range_guard():
+    """the sharded ItemCF's int32 global slots must not wrap."""
+    from nrk.dist import SLOT_LIMIT, check_slot_range
+
+    check_slot_range(SLOT_LIMIT - 1)
+    with pytest.raises(ValueError):
+        check_slot_range(SLOT_LIMIT)
+    with pytest.raises(ValueError):
+        check_slot_range(3 * (1 << 30))
