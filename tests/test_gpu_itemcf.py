@@ -149,6 +149,22 @@ def test_itemcf_topn_vs_oracle(topn):
     assert np.array_equal(gv.cpu().numpy(), ov)
 
 
+def _near_ties_only(g_idx, o_idx, o_val_ext, valid, rtol=1e-12):
+    """Every position where the device's index differs from the oracle's
+    holds an oracle value within ``rtol`` of a neighbouring oracle value
+    (o_val_ext has one extra column: the first entry past the cut) -- i.e.
+    only near-ties that the last ulp of exp / pow can reorder."""
+    mism = (g_idx != o_idx) & valid
+    r, p = np.nonzero(mism)
+    if len(r) == 0:
+        return True
+    v = o_val_ext
+    tol = rtol * np.abs(v[r, p])
+    left = (p > 0) & (np.abs(v[r, p] - v[r, np.maximum(p - 1, 0)]) <= tol)
+    right = np.abs(v[r, p] - v[r, p + 1]) <= tol
+    return bool((left | right).all())
+
+
 def test_itemcf_full_size():
     """250k-user / 364,047-item synthetic Tianchi log (BASELINE sizes): the
     whole similarity against the oracle, plus top-20 per item."""
@@ -163,9 +179,14 @@ def test_itemcf_full_size():
     roff, cols, vals = oracle.sim_to_rows(oi, oj, ov, len(ids))
     oc, ovv, on = oracle.itemcf_topn(roff, cols, vals, 20)
     assert np.array_equal(gn.cpu().numpy(), on)
-    same = gc.cpu().numpy() == oc
-    # identical except where device/libm last-ulp differences reorder near-ties
-    assert same.mean() > 0.9999
+    # identical except where device / libm last-ulp differences reorder an
+    # exact-arithmetic near-tie: every differing position must sit next to an
+    # oracle value within 1e-12 of its own (the 21st entry included), and the
+    # sorted values agree to 1e-12
+    _, ov21, _ = oracle.itemcf_topn(roff, cols, vals, 21)
+    valid = np.arange(20)[None, :] < on[:, None]
+    assert _near_ties_only(gc.cpu().numpy(), oc, ov21, valid)
+    np.testing.assert_allclose(gv.cpu().numpy()[valid], ovv[valid], rtol=1e-12, atol=0)
 
 
 # ------------------------------------------------------------ A10 recall --
@@ -263,9 +284,11 @@ def test_itemcf_recall_full_size():
     assert np.array_equal(gn.cpu().numpy(), on)
     gi = gi.cpu().numpy()
     valid = np.arange(30)[None, :] < on[:, None]
-    same = (gi == oi) | ~valid
-    assert same.all(axis=1).mean() > 0.9999
-    np.testing.assert_allclose(np.sort(gs.cpu().numpy()[valid]), np.sort(os_[valid]), rtol=1e-11)
+    # exact except certified near-ties (see _near_ties_only), scores to 1e-11
+    _, os31, _ = oracle.itemcf_recall(q, offs, dense, nc.cpu().numpy(), nv.cpu().numpy(), nn.cpu().numpy(),
+                                      created, hot, 31, len(ids))
+    assert _near_ties_only(gi, oi, os31, valid, rtol=1e-11)
+    np.testing.assert_allclose(gs.cpu().numpy()[valid], os_[valid], rtol=1e-11, atol=0)
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
