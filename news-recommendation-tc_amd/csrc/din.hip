@@ -221,8 +221,8 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
     for (int64_t b = seg * S + blockIdx.x % G; b < b_end; b += G) {
         u4n nraw[NTW][NI][RW];
         uint32_t nqv;
-        rows_of(nidx, nqi, nraw, nqv);   // rows of sample b + G
-        idx_of(b + 2 * G, nidx, nqi);    // indices of sample b + 2G
+        rows_of(nidx, nqi, nraw, nqv);      // rows of sample b + G
+        idx_of(b + 2 * G, nidx, nqi);       // indices of sample b + 2G
         // (1) this wave's k rows -> A fragments
         din_half8 ahi[NTW][NI], alo[NTW][NI];
 #pragma unroll
@@ -498,7 +498,7 @@ __device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
 }
 
 template <typename TT, int NI, int NCH>
-__global__ __launch_bounds__(256) void din_wh_kernel(
+__global__ __launch_bounds__(256, 2) void din_wh_kernel(
     const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
     const int32_t* __restrict__ hist_idx, const float* __restrict__ mask, int64_t B, int64_t S,
     int T, int64_t per_wave, const float* __restrict__ h, const float2* __restrict__ hinv_all,
@@ -542,20 +542,29 @@ __global__ __launch_bounds__(256) void din_wh_kernel(
     // sample bb's h block [T x DIN_H] read as consecutive 16-B chunks (chunk
     // q = 64 i + lane: one coalesced 1-KB load per i), plus lane t's history
     // indices and mask
+    // masked rows' weights are multiplied by 0, so their h is never needed:
+    // their chunks read one shared, always-finite chunk instead --
+    // unconditional loads, no traffic.  The mask of the fetched
+    // sample was loaded one sample earlier (mk_n), so the chunk addresses do
+    // not wait on a load in flight.
     f4n hq[NCH];
     int32_t ix[NI];
     float mk;
-    auto fetch = [&](int64_t bb) {
+    const f4n* hdummy = reinterpret_cast<const f4n*>(hinv_all);
+    auto load_mask = [&](int64_t bb) -> float { return (bb < b1e && act) ? mask[bb * T + lane] : 0.0f; };
+    auto fetch = [&](int64_t bb, float mbb) {
         const bool ok = bb < b1e;
         const f4n* hr = reinterpret_cast<const f4n*>(h + (size_t)(ok ? bb : 0) * T * DIN_H);
+        const uint64_t live = __builtin_amdgcn_ballot_w64(mbb != 0.0f);  // unmasked rows (wave-uniform)
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
             const int q = 64 * i + lane;
-            hq[i] = ok && q < nq ? hr[q] : f4n{0.0f, 0.0f, 0.0f, 0.0f};
+            const bool on = ok && q < nq && ((live >> (q / HQ)) & 1ull);
+            hq[i] = *(on ? hr + q : hdummy);
         }
 #pragma unroll
         for (int f = 0; f < NI; ++f) ix[f] = ok && act ? hist_idx[((size_t)bb * T + lane) * NI + f] : 0;
-        mk = ok && act ? mask[bb * T + lane] : 0.0f;
+        mk = mbb;
     };
     // this segment's Dice statistics for the same chunks, kept in registers
     f4n sm[NCH], si[NCH];
@@ -570,7 +579,9 @@ __global__ __launch_bounds__(256) void din_wh_kernel(
             si[i] = f4n{s0.y, s0.w, s1.y, s1.w};
         }
     };
-    fetch(b0);
+    float mk_n = load_mask(b0);
+    fetch(b0, mk_n);
+    mk_n = load_mask(b0 + 1);
     for (int64_t b = b0; b < b1e; ++b) {
         const int64_t seg = b / S;
         if (seg != cur) {
@@ -612,7 +623,8 @@ __global__ __launch_bounds__(256) void din_wh_kernel(
         const uint64_t nz = __builtin_amdgcn_ballot_w64(w != 0.0f);
         const int te = nz ? 64 - __builtin_clzll(nz) : 0;
         asm volatile("" ::: "memory");
-        fetch(b + 1);  // next sample, in flight during the gathers
+        fetch(b + 1, mk_n);  // next sample, in flight during the gathers
+        mk_n = load_mask(b + 2);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1336,12 +1348,12 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     do {                                                                                               \
         if (T <= 64)                                                                                   \
             din_att_h_kernel<TT, NI, 1><<<(unsigned)nb_att, 256, 0, s>>>(                              \
-                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G, \
-                T, pf, att_b0, w.h, w.hpart);                                                          \
+                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G,    \
+                T, pf, att_b0, w.h, w.hpart);                                                       \
         else                                                                                           \
             din_att_h_kernel<TT, NI, 2><<<(unsigned)nb_att, 256, 0, s>>>(                              \
-                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G, \
-                T, pf, att_b0, w.h, w.hpart);                                                          \
+                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G,    \
+                T, pf, att_b0, w.h, w.hpart);                                                       \
     } while (0)
     if (table_dtype == 0) {
         if (n_item == 4) NRK_ATT_H(float, 4); else if (n_item == 2) NRK_ATT_H(float, 2); else NRK_ATT_H(float, 1);

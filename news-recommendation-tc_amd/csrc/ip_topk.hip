@@ -28,6 +28,7 @@
 #include "nrk_common.h"
 
 #include <float.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -143,7 +144,7 @@ __device__ __forceinline__ float round_down_sub(float theta, float two_eps) {
 // the 32 lanes of a half-wave touch 128 consecutive bytes.  Both lanes of a
 // user (h = 0, 1: the two 16-item halves of every 32-item block) append to
 // the same list and keep identical copies of its count n, cut tau and theta.
-constexpr int SC_CL = 64;  // entries per user list
+constexpr int SC_CL = 64;  // entries per user list (default variant)
 
 __device__ __forceinline__ float lds_rd(uint32_t a) {
     float v;
@@ -214,6 +215,7 @@ __device__ __forceinline__ void sort32_desc(float (&x)[32]) {
 // partner[31 - i]) (one bitonic merge step), sorted again to read the k-th.
 // A user whose kept band does not leave room for the next tile's appends
 // (dense exact ties) stops appending and is redone by the exact fallback.
+template <int CL>
 __device__ __forceinline__ void user_flush(uint32_t ls, uint32_t li, int h, int& n, float& tau,
                                            float& theta, bool& ovf, int k, float eps, int cap) {
     const uint32_t as = ls + (uint32_t)h * (32u * 32u * 4u), ai = li + (uint32_t)h * (32u * 32u * 4u);
@@ -270,7 +272,7 @@ __device__ __forceinline__ void user_flush(uint32_t ls, uint32_t li, int h, int&
     const int c_own = __popc(keepm);
     const int c_par = (int)partner32((uint32_t)c_own, h);
     int pos = h ? c_par : 0;
-    const uint32_t ls0 = ls - (uint32_t)0, dump = (uint32_t)(SC_CL - 1) * 128u;
+    const uint32_t ls0 = ls - (uint32_t)0, dump = (uint32_t)(CL - 1) * 128u;
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
         const bool kp = (keepm >> i) & 1u;
@@ -298,8 +300,8 @@ __device__ __forceinline__ void user_flush(uint32_t ls, uint32_t li, int h, int&
 // is nearly full; a flush requested by any wave is joined by the others at
 // the same tile (they all meet at the per-tile barrier anyway), through an
 // LDS hint word.
-template <int DP, int NW>
-__global__ __launch_bounds__(NW * 64, NW / 4) void ip_screen_kernel(
+template <int DP, int NW, int NSL = 3, int CL = SC_CL>
+__global__ __launch_bounds__(NW * 64, (NW == 4 && CL < 64) ? 2 : NW / 4) void ip_screen_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog,
     int n_items, int dim, int k, uint2* __restrict__ cand, int32_t* __restrict__ cand_cnt,
     float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
@@ -310,9 +312,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void ip_screen_kernel(
     constexpr int TILE_BYTES = TB * BLOCK_BYTES;
     constexpr int LPT = TILE_BYTES / (NW * 64 * 16);  // 1-KB LDS-DMA pieces per wave per tile
     static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
-    constexpr int NSLOT = 3;
-    constexpr int WLIST = 2 * SC_CL * 32 * 4;  // one wave's score + id planes
-    constexpr int CAP = SC_CL - 2 * TB;        // list size that still takes one tile of appends
+    constexpr int NSLOT = NSL;
+    constexpr int WLIST = 2 * CL * 32 * 4;  // one wave's score + id planes
+    constexpr int CAP = CL - 2 * TB;        // list size that still takes one tile of appends
     constexpr int LDS = NSLOT * TILE_BYTES + NW * WLIST + 16;
     static_assert(LDS <= 163840, "LDS budget");
     __shared__ __attribute__((aligned(16))) uint8_t smem[LDS];
@@ -368,7 +370,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void ip_screen_kernel(
     const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
     const uint32_t lst = lds_base + NSLOT * TILE_BYTES + wave * WLIST;
     const uint32_t ls = lst + q * 4;                       // score plane, entry j at + j * 128
-    const uint32_t li = lst + SC_CL * 32 * 4 + q * 4;      // id plane
+    const uint32_t li = lst + CL * 32 * 4 + q * 4;      // id plane
     const uint32_t hint = lds_base + NSLOT * TILE_BYTES + NW * WLIST;
     if (tid == 0) lds_wr(hint, 0xFFFFFFFFu);
 
@@ -469,11 +471,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void ip_screen_kernel(
         const bool need = __builtin_amdgcn_ballot_w64(n > CAP) != 0;
         const bool soon = __builtin_amdgcn_ballot_w64(n > CAP - 2 * TB) != 0;
         if (soon && lane == 0) lds_wr(hint, (uint32_t)(t + 1));
-        if (need || (hv == t && __builtin_amdgcn_ballot_w64(n > SC_CL / 2) != 0))
-            user_flush(ls, li, h, n, tau, theta, ovf, k, eps_s, CAP);
+        if (need || (hv == t && __builtin_amdgcn_ballot_w64(n > CL / 2) != 0))
+            user_flush<CL>(ls, li, h, n, tau, theta, ovf, k, eps_s, CAP);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
-    user_flush(ls, li, h, n, tau, theta, ovf, k, eps_s, CAP);
+    user_flush<CL>(ls, li, h, n, tau, theta, ovf, k, eps_s, CAP);
 
     if (!active) return;
     float cut = theta;
@@ -1085,13 +1087,30 @@ int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog,
     ip_screen_kernel<DPV, NWV><<<(int)((n_users + 32 * NWV - 1) / (32 * NWV)), 64 * NWV, 0, s>>>( \
         users, (int)n_users, cat, (int)n_items, dim, k, w.cand, w.cnt, w.ucut, w.ovf_flag,       \
         w.ovf_list, w.ovf_count)
-        switch (dp) {
+        // 4 waves (128 users) per workgroup, a 2-tile LDS-DMA ring and 62-entry
+        // lists: 79.9 KB of LDS, so two workgroups share a CU and each one's
+        // per-tile barrier / DMA wait is covered by the other (9.5 ms at config
+        // 2 against 10.3 ms for one 8-wave workgroup with a 3-tile ring;
+        // tools/screen_variants.sh).  NRK_SCREEN_VARIANT=0 selects the latter.
+        static const int var = [] { const char* e = getenv("NRK_SCREEN_VARIANT"); return e ? atoi(e) : 1; }();
+#define NRK_SCREEN_V(DPV, NWV, NSV, CLV)                                                                   \
+    ip_screen_kernel<DPV, NWV, NSV, CLV><<<(int)((n_users + 32 * NWV - 1) / (32 * NWV)), 64 * NWV, 0, s>>>( \
+        users, (int)n_users, cat, (int)n_items, dim, k, w.cand, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,        \
+        w.ovf_count)
+        if (var == 1 && dp <= 64) {  // D = 128 (config 5): the 8-wave form measured 0.8% faster
+            switch (dp) {
+                case 16: NRK_SCREEN_V(16, 4, 2, 62); break;
+                case 32: NRK_SCREEN_V(32, 4, 2, 62); break;
+                default: NRK_SCREEN_V(64, 4, 2, 62); break;
+            }
+        } else switch (dp) {
             case 16: NRK_SCREEN(16, 8); break;
             case 32: NRK_SCREEN(32, 8); break;
             case 64: NRK_SCREEN(64, 8); break;
             case 128: NRK_SCREEN(128, 8); break;
             default: NRK_SCREEN(256, 4); break;
         }
+#undef NRK_SCREEN_V
 #undef NRK_SCREEN
     }
     NRK_CHECK_LAUNCH();
