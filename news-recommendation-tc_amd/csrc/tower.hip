@@ -16,38 +16,70 @@ __global__ __launch_bounds__(256) void tt_user_kernel(
     const int32_t* __restrict__ hist_len, int64_t n, int T, const float* __restrict__ w0,
     const float* __restrict__ b0, int h0, const float* __restrict__ w1,
     const float* __restrict__ b1, int h1, float* __restrict__ out) {
+    // weight rows padded by one word: lane o reads row o, so an unpadded
+    // power-of-two row stride would put all 64 lanes on one LDS bank
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* sw0 = lds;               // [h0][2D]
-    float* sb0 = sw0 + h0 * 2 * D;  // [h0]
-    float* sw1 = sb0 + h0;          // [h1][h0]
-    float* sb1 = sw1 + h1 * h0;     // [h1]
-    for (int i = threadIdx.x; i < h0 * 2 * D; i += blockDim.x) sw0[i] = w0[i];
+    const int S0 = 2 * D + 1, S1 = h0 + 1;
+    float* sw0 = lds;               // [h0][S0]
+    float* sb0 = sw0 + h0 * S0;     // [h0]
+    float* sw1 = sb0 + h0;          // [h1][S1]
+    float* sb1 = sw1 + h1 * S1;     // [h1]
+    for (int i = threadIdx.x; i < h0 * 2 * D; i += blockDim.x) sw0[(i / (2 * D)) * S0 + i % (2 * D)] = w0[i];
     for (int i = threadIdx.x; i < h0; i += blockDim.x) sb0[i] = b0[i];
-    for (int i = threadIdx.x; i < h1 * h0; i += blockDim.x) sw1[i] = w1[i];
+    for (int i = threadIdx.x; i < h1 * h0; i += blockDim.x) sw1[(i / h0) * S1 + i % h0] = w1[i];
     for (int i = threadIdx.x; i < h1; i += blockDim.x) sb1[i] = b1[i];
     __syncthreads();  // the only block barrier: the user loop below is per wave
 
     constexpr int P = WAVE / D;  // history phases per lane group
+    constexpr int CH = 8;        // history rows in flight per lane
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int d = lane % D, ph = lane / D;
     const int64_t wstride = (int64_t)gridDim.x * 4;
-    for (int64_t u = (int64_t)blockIdx.x * 4 + wave; u < n; u += wstride) {
-        const int len = hist_len[u];
-        const int32_t* hr = hist + u * T;
+    // software pipeline over this wave's users: the next user's length, id and
+    // history indices (lane t holds index t; T <= 64) are loaded while this
+    // user's rows are summed, and the rows themselves are issued CH at a time
+    // (unconditional loads: slots past the length read row 0 and are not
+    // added), so no load waits on another in flight.
+    auto meta = [&](int64_t uu, int& len, int32_t& uidv, int32_t& hv) {
+        const bool ok = uu < n;
+        len = ok ? hist_len[uu] : 0;
+        uidv = ok ? uid[uu] : 0;
+        hv = ok && lane < T ? hist[uu * T + lane] : 0;
+    };
+    int64_t u = (int64_t)blockIdx.x * 4 + wave;
+    int len, uidv;
+    int32_t hv;
+    meta(u, len, uidv, hv);
+    for (; u < n; u += wstride) {
+        int nlen, nuid;
+        int32_t nhv;
+        meta(u + wstride, nlen, nuid, nhv);
+        const float xu = user_table[(int64_t)uidv * D + d];
         float sum = 0.0f;
-        for (int t = ph; t < len; t += P) sum += item_table[(int64_t)hr[t] * D + d];
+        const int nit = (len + P - 1) / P;  // wave-uniform
+        for (int i0 = 0; i0 < nit; i0 += CH) {
+            float v[CH];
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                const int t = ph + P * (i0 + e);
+                const int32_t r = __shfl(hv, t < T ? t : 0, WAVE);
+                v[e] = item_table[(int64_t)(t < len ? r : 0) * D + d];
+            }
+#pragma unroll
+            for (int e = 0; e < CH; ++e)
+                if (ph + P * (i0 + e) < len) sum += v[e];  // t ascending, as before
+        }
 #pragma unroll
         for (int off = D; off < WAVE; off <<= 1) sum += __shfl_xor(sum, off, WAVE);
         // lane q < D holds x[q] = E_u[uid][q] and x[D + q] = mean[q]
-        const float xu = user_table[(int64_t)uid[u] * D + d];
         const float xm = sum / ((float)len + 1e-8f);
         // layer 0: lane o (and o + 64) owns output o
         float y0 = 0.0f, y1 = 0.0f;
         {
             float z0 = lane < h0 ? sb0[lane] : 0.0f;
             float z1 = lane + WAVE < h0 ? sb0[lane + WAVE] : 0.0f;
-            const float* wr0 = sw0 + (lane < h0 ? lane : 0) * 2 * D;
-            const float* wr1 = sw0 + (lane + WAVE < h0 ? lane + WAVE : 0) * 2 * D;
+            const float* wr0 = sw0 + (lane < h0 ? lane : 0) * S0;
+            const float* wr1 = sw0 + (lane + WAVE < h0 ? lane + WAVE : 0) * S0;
 #pragma unroll
             for (int q = 0; q < D; ++q) {
                 const float xq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xu), q));
@@ -67,7 +99,7 @@ __global__ __launch_bounds__(256) void tt_user_kernel(
         float v = 0.0f;
         {
             float z = lane < h1 ? sb1[lane] : 0.0f;
-            const float* wr = sw1 + (lane < h1 ? lane : 0) * h0;
+            const float* wr = sw1 + (lane < h1 ? lane : 0) * S1;
             const int q0 = h0 < WAVE ? h0 : WAVE;
             for (int q = 0; q < q0; ++q)
                 z += wr[q] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y0), q));
@@ -80,6 +112,9 @@ __global__ __launch_bounds__(256) void tt_user_kernel(
         float n2 = sqrtf(wave_sum_f32(v * v));
         if (n2 == 0.0f) n2 = 1.0f;
         if (lane < h1) out[u * h1 + lane] = v / n2;
+        len = nlen;
+        uidv = nuid;
+        hv = nhv;
     }
 }
 
@@ -122,7 +157,7 @@ int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* i
                     const float* b0, int h0, const float* w1, const float* b1, int h1,
                     float* out, nrk_stream_t stream) {
     clear_error();
-    NRK_REQUIRE(n >= 0 && seq_len >= 1, "bad sizes");
+    NRK_REQUIRE(n >= 0 && seq_len >= 1 && seq_len <= 64, "bad sizes (seq_len must be in [1, 64])");
     NRK_REQUIRE(n_user_rows > 0 && n_item_rows > 0, "empty embedding tables");
     if (!(dim == 16 || dim == 32 || dim == 64)) NRK_UNSUPPORTED("dim must be 16, 32 or 64");
     NRK_REQUIRE(h0 >= 1 && h0 <= 128, "h0 must be in [1, 128]");
@@ -131,7 +166,7 @@ int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* i
     if (n == 0) return NRK_OK;
     NRK_REQUIRE(user_table && item_table && uid && hist && hist_len && w0 && b0 && w1 && b1 && out,
                 "null pointer");
-    const size_t lds = sizeof(float) * ((size_t)h0 * 2 * dim + h0 + (size_t)h1 * h0 + h1);
+    const size_t lds = sizeof(float) * ((size_t)h0 * (2 * dim + 1) + h0 + (size_t)h1 * (h0 + 1) + h1);
     hipStream_t s = as_stream(stream);
     const int grid = (int)std::min<int64_t>((n + 3) / 4, 2048);
 #define NRK_TT_LAUNCH(DD)                                                                      \
