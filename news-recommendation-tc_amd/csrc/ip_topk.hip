@@ -518,6 +518,7 @@ __device__ __forceinline__ double exact_dot(const float* __restrict__ a, const f
 }
 
 constexpr int IP_SURV = 128;  // exact survivors per user held by the refine
+constexpr int IP_KRING = 256; // prefilter-kept rows awaiting an exact round (ring, power of two)
 
 // DS4 = dim / 4 when the candidate rows are staged through LDS (dim 16, 32,
 // 64): every 64-item round loads the rows with whole-row coalesced float4
@@ -534,6 +535,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
     int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
     double* __restrict__ out_e) {
     __shared__ Cand surv[4][IP_SURV];
+    __shared__ int32_t krow[DS4 > 0 ? 4 : 1][DS4 > 0 ? IP_KRING : 1];
     constexpr int RS = DS4 + 1;  // staged row stride in float4 (one float4 of padding)
     __shared__ float4 stage[DS4 > 0 ? 4 : 1][DS4 > 0 ? 64 * RS : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -611,11 +613,15 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         cnt += __popcll(bal);
     };
     if constexpr (DS4 > 0) {
-        // Software pipeline over 64-item rounds.  Round i issues, in this
-        // order: the fp32 rows of its kept items, the packed fp16 pieces of
-        // round i+1, the band entries of round i+2.  vmcnt retires in issue
-        // order, so waiting for round i's rows does not wait for round i+1's
-        // pieces, which stay in flight across round i's exact dot products.
+        // Two phases over the band.  (A) fp16 prefilter in 64-item rounds,
+        // software-pipelined: round i+1's packed fp16 pieces are in flight
+        // while round i is scored; the kept items' rows go to a per-wave LDS
+        // ring.  (B) whenever the ring holds 64 rows (and once at the end),
+        // one exact round: the rows staged through LDS with whole-row
+        // coalesced float4 pieces, each lane summing its own row sequentially
+        // (the oracle's order).  Most band items fail the prefilter, so the
+        // exact rounds (the expensive part) run on full 64-row chunks instead
+        // of once per prefilter round.
         uint4 pc[DSK > 0 ? 2 * DSK : 1];
         auto band_q = [&](int base) -> uint32_t {
             int idx = base + lane;
@@ -639,13 +645,54 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
                         pc[2 * st + hh] = *reinterpret_cast<const uint4*>(bp + st * 1024 + (il + 32 * hh) * 16);
             }
         };
+        int kc = 0, ko = 0;  // ring fill / read positions (wave-uniform)
+        auto exact_round = [&](int m) {
+            const int32_t rl = lane < m ? krow[wave][(ko + lane) & (IP_KRING - 1)] : -1;
+            float4 v[DS4];
+            bool okv[DS4];
+#pragma unroll
+            for (int it = 0; it < DS4; ++it) {
+                const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
+                const int r_item = __shfl(rl, item, WAVE);
+                okv[it] = r_item >= 0;
+                v[it] = reinterpret_cast<const float4*>(items + (int64_t)(okv[it] ? r_item : 0) * dim)[part];
+            }
+#pragma unroll
+            for (int it = 0; it < DS4; ++it) {
+                const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
+                stage[wave][item * RS + part] = okv[it] ? v[it] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double sd = 0.0;
+            bool keep = false;
+            if (rl >= 0) {
+                const float4* a4 = reinterpret_cast<const float4*>(uv);
+                const float4* b4 = &stage[wave][lane * RS];
+                double acc = 0.0;
+#pragma unroll
+                for (int t = 0; t < DS4; ++t) {
+                    const float4 x = a4[t], y = b4[t];
+                    acc += (double)x.x * (double)y.x;
+                    acc += (double)x.y * (double)y.y;
+                    acc += (double)x.z * (double)y.z;
+                    acc += (double)x.w * (double)y.w;
+                }
+                sd = acc + 0.0;
+                keep = sd >= thr;
+            }
+            __builtin_amdgcn_wave_barrier();  // the stage is rewritten next round
+            push(keep, sd, rl);
+            ko += m;
+        };
         int32_t row;
         bool inb;
         item_row(0, band_q(0), row, inb);
         pieces(row);
         uint32_t q1 = band_q(WAVE < nitem ? WAVE : 0);
         for (int base = 0; base < nitem; base += WAVE) {
-            // (1) fp16 prefilter of this round: every band item's scaled fp16
+            // (A) fp16 prefilter of this round: every band item's scaled fp16
             // score from its 64-B packed row, kept when it reaches the cut
             // (|fp16 score - exact| <= eps as in the screen)
             bool keep = inb;
@@ -662,56 +709,25 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
                     }
                 keep = acc >= pcut;
             }
-            // (2) this round's kept fp32 rows, whole-row coalesced float4
-            // pieces (64 / DS4 rows per instruction), unconditional loads
-            float4 v[DS4];
-            bool okv[DS4];
-#pragma unroll
-            for (int it = 0; it < DS4; ++it) {
-                const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
-                const int r_item = __shfl(row, item, WAVE);
-                okv[it] = __shfl((int)keep, item, WAVE) != 0;
-                // dropped items read row 0 (one shared line) instead of their own
-                v[it] = reinterpret_cast<const float4*>(items + (int64_t)(okv[it] ? r_item : 0) * dim)[part];
-            }
             const int32_t row_cur = row;
-            // (3) next round's rows and packed pieces, then the band entries
-            // of the round after it
+            // next round's rows and packed pieces, then the band entries of
+            // the round after it
             const int nb = base + WAVE;
             if (nb < nitem) {
                 item_row(nb, q1, row, inb);
                 pieces(row);
                 q1 = band_q(nb + WAVE < nitem ? nb + WAVE : nb);
             }
-            // (4) stage, then each lane sums its own row sequentially (the
-            // oracle's order)
-#pragma unroll
-            for (int it = 0; it < DS4; ++it) {
-                const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
-                stage[wave][item * RS + part] = okv[it] ? v[it] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+            const unsigned long long bal = __ballot(keep);
+            if (keep) krow[wave][(kc + __popcll(bal & ((1ull << lane) - 1ull))) & (IP_KRING - 1)] = row_cur;
+            kc += __popcll(bal);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            double sd = 0.0;
-            if (keep) {
-                const float4* a4 = reinterpret_cast<const float4*>(uv);
-                const float4* b4 = &stage[wave][lane * RS];
-                double acc = 0.0;
-#pragma unroll
-                for (int t = 0; t < DS4; ++t) {
-                    const float4 x = a4[t], y = b4[t];
-                    acc += (double)x.x * (double)y.x;
-                    acc += (double)x.y * (double)y.y;
-                    acc += (double)x.z * (double)y.z;
-                    acc += (double)x.w * (double)y.w;
-                }
-                sd = acc + 0.0;
-                keep = sd >= thr;
-            }
-            __builtin_amdgcn_wave_barrier();  // the stage is rewritten next round
-            push(keep, sd, row_cur);
+            // (B) exact rounds on full 64-row chunks
+            while (kc - ko >= WAVE) exact_round(WAVE);
         }
+        while (kc > ko) exact_round(kc - ko < WAVE ? kc - ko : WAVE);
     } else {
         for (int base = 0; base < nitem; base += WAVE) {
             const int idx = base + lane;
