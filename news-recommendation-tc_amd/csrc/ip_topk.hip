@@ -154,6 +154,12 @@ __device__ __forceinline__ float lds_rd(uint32_t a) {
 __device__ __forceinline__ void lds_wr(uint32_t a, uint32_t v) {
     asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
+// v0 at a, v1 at a + OFF (one address register)
+template <int OFF>
+__device__ __forceinline__ void lds_wr_pair(uint32_t a, uint32_t v0, uint32_t v1) {
+    asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %0, %2 offset:%c3" ::"v"(a), "v"(v0), "v"(v1), "n"(OFF)
+                 : "memory");
+}
 // 16 dwords at a + i * stride (i = 0..15), one wait for all of them.  Inline
 // asm: hipcc's waitcnt pass would drain the in-flight LDS-DMA (the ring
 // prefetch) in front of any compiler-visible LDS access.
@@ -393,27 +399,42 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && CL < 64) ? 2 : NW / 4) void ip
         }
     };
     const uint32_t lds0 = lds_base + lane * 16;
-    // all fragment reads and their wait in ONE asm statement (a separate wait
-    // statement lets the compiler copy an output before the data landed)
-    auto read_frags = [&](int t, u32x4 (&afr)[TB * DS]) {
+    // all fragment reads (and the flush-hint word) and their wait in ONE asm
+    // statement: one LDS round trip per tile, and a separate wait statement
+    // would let the compiler copy an output before the data landed
+    static_assert((TB * DS) % 8 == 0, "fragment groups of 8");
+    auto read_frags = [&](int t, u32x4 (&afr)[TB * DS], uint32_t& hraw) {
         const uint32_t base = lds0 + (uint32_t)((t % NSLOT) * TILE_BYTES);
+        u32x4* f = &afr[0];
+        asm volatile(
+            "ds_read_b32 %8, %10\n\t"
+            "ds_read_b128 %0, %9 offset:0\n\tds_read_b128 %1, %9 offset:1024\n\t"
+            "ds_read_b128 %2, %9 offset:2048\n\tds_read_b128 %3, %9 offset:3072\n\t"
+            "ds_read_b128 %4, %9 offset:4096\n\tds_read_b128 %5, %9 offset:5120\n\t"
+            "ds_read_b128 %6, %9 offset:6144\n\tds_read_b128 %7, %9 offset:7168\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]),
+              "=&v"(f[6]), "=&v"(f[7]), "=&v"(hraw)
+            : "v"(base), "v"(hint)
+            : "memory");
 #pragma unroll
-        for (int g = 0; g < TB * DS; g += 4) {
-            u32x4* f = &afr[g];
+        for (int g = 8; g < TB * DS; g += 8) {
+            f = &afr[g];
             asm volatile(
-                "ds_read_b128 %0, %4 offset:0\n\tds_read_b128 %1, %4 offset:1024\n\t"
-                "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
+                "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:1024\n\t"
+                "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
+                "ds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:5120\n\t"
+                "ds_read_b128 %6, %8 offset:6144\n\tds_read_b128 %7, %8 offset:7168\n\t"
                 "s_waitcnt lgkmcnt(0)"
-                : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3])
+                : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]),
+                  "=&v"(f[6]), "=&v"(f[7])
                 : "v"(base + 1024u * g)
                 : "memory");
         }
     };
     const int full_tiles = tail_blk / TB;  // tiles whose blocks are all full
-    auto tile = [&](int t, auto mask_c) {
+    auto tile = [&](int t, const u32x4 (&afr)[TB * DS], auto mask_c) {
         constexpr bool MASK = decltype(mask_c)::value;
-        u32x4 afr[TB * DS];
-        read_frags(t, afr);
         float m[TB];
 #pragma unroll
         for (int b = 0; b < TB; ++b) {
@@ -434,24 +455,25 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && CL < 64) ? 2 : NW / 4) void ip
             for (int r = 3; r < 15; r += 2) v = fmaxf(fmaxf(v, acc[r]), acc[r + 1]);
             m[b] = fmaxf(v, acc[15]);
         }
-        bool any = false;
+        uint32_t cm = 0;
 #pragma unroll
-        for (int b = 0; b < TB; ++b) any |= m[b] > tau;
-        if (__builtin_amdgcn_ballot_w64(any)) {
-            // both lanes of a user append in one go: lane 0 at n, lane 1 at
-            // n + (lane 0 appends)
+        for (int b = 0; b < TB; ++b) cm |= m[b] > tau ? (1u << b) : 0u;
+        if (__builtin_amdgcn_ballot_w64(cm != 0)) {
+            // both lanes of a user append in one go, branch-free: lane 0's
+            // entries at n + [0, c0), lane 1's at n + c0 + [0, c1); a block
+            // not taken is written to slot CL - 1, which a kept entry reaches
+            // only when all 2 TB blocks of the user are taken (no dump then)
+            const uint32_t pm = partner32(cm, h);
+            const int c_own = __popc(cm), c_par = __popc(pm);
+            const uint32_t base = (uint32_t)(n + (h ? c_par : 0));
+            constexpr uint32_t dump = (uint32_t)(CL - 1) * 128u;
 #pragma unroll
             for (int b = 0; b < TB; ++b) {
-                const bool c = m[b] > tau;
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(c);
-                const int c0 = (int)((bal >> q) & 1ull), c1 = (int)((bal >> (32 + q)) & 1ull);
-                const int pos = n + (h ? c0 : 0);
-                if (c) {
-                    lds_wr(ls + (uint32_t)pos * 128u, __float_as_uint(m[b]));
-                    lds_wr(li + (uint32_t)pos * 128u, (uint32_t)((t * TB + b) * 2 + h));
-                }
-                n += c0 + c1;
+                const uint32_t off = ((cm >> b) & 1u) ? (base + (uint32_t)__popc(cm & ((1u << b) - 1u))) * 128u
+                                                      : dump;
+                lds_wr_pair<CL * 32 * 4>(ls + off, __float_as_uint(m[b]), (uint32_t)((t * TB + b) * 2 + h));
             }
+            n += c_own + c_par;
         }
     };
 
@@ -462,10 +484,13 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && CL < 64) ? 2 : NW / 4) void ip
         // flight), list appends done; the barrier publishes everyone's
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(LPT * (NSLOT - 2)) : "memory");
         __builtin_amdgcn_s_barrier();
-        const int hv = (int)__builtin_amdgcn_readfirstlane((int)lds_rd(hint));
         issue_tile(t + NSLOT - 1);
-        if (t < full_tiles) tile(t, std::false_type{});
-        else tile(t, std::true_type{});
+        u32x4 afr[TB * DS];
+        uint32_t hraw;
+        read_frags(t, afr, hraw);
+        const int hv = (int)__builtin_amdgcn_readfirstlane((int)hraw);
+        if (t < full_tiles) tile(t, afr, std::false_type{});
+        else tile(t, afr, std::true_type{});
         // flush when a list cannot take the next tile's appends, or with the
         // other waves when one of them flushes at this tile (hint)
         const bool need = __builtin_amdgcn_ballot_w64(n > CAP) != 0;
