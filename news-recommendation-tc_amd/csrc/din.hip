@@ -1277,6 +1277,9 @@ int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int tabl
     clear_error();
     NRK_REQUIRE(att_w0 && prep && table, "null pointer");
     NRK_REQUIRE(n_item >= 1 && n_item <= 8, "n_item must be in [1, 8]");
+    // nrk_din_forward_segments is instantiated for 1, 2 and 4 item features only:
+    // refuse the others here rather than at the first forward call
+    if (n_item != 4 && n_item != 2 && n_item != 1) NRK_UNSUPPORTED("n_item must be 1, 2 or 4");
     NRK_REQUIRE(table_dtype == 0 || table_dtype == 1, "table_dtype must be 0 (f32) or 1 (bf16)");
     NRK_REQUIRE(n_table_rows >= 1, "n_table_rows must be >= 1");
     const int ID = n_item * DIN_E;

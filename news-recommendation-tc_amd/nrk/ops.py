@@ -236,6 +236,9 @@ class DinParams:
         self.row_base = torch.from_numpy(base).to(device)
         self.vocab = [t.shape[0] for t in tabs]
         self.n_user, self.n_item, self.n_ctx = len(user_feats), len(item_feats), len(ctx_feats)
+        if self.n_item not in (1, 2, 4):
+            # the attention kernels are instantiated for 1, 2 or 4 item features
+            raise NotImplementedError("DIN supports 1, 2 or 4 item features, got %d" % self.n_item)
         d = lambda k: torch.from_numpy(arr(k)).to(device).contiguous()  # noqa: E731
         self.att_w0 = d("activation_unit.mlp.0.weight")
         self.att_b0 = d("activation_unit.mlp.0.bias")

@@ -47,3 +47,13 @@ def test_argument_errors_raise_valueerror():
         _lib.check(rc, "nrk_ip_topk")
     rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, 33, 0, None, None, None, None, 0, None)
     assert rc == _lib.NRK_EUNSUPPORTED
+
+
+def test_din_prepare_refuses_unsupported_item_counts():
+    # the forward is instantiated for 1, 2 or 4 item features; prepare refuses
+    # the others before touching any pointer (fail at build time)
+    L = _lib.lib()
+    for n_item in (3, 5, 8):
+        rc = L.nrk_din_prepare(1, n_item, 1, 1, 10, 1, None)
+        assert rc == _lib.NRK_EUNSUPPORTED, n_item
+        assert b"n_item must be 1, 2 or 4" in L.nrk_last_error()
