@@ -96,7 +96,10 @@ def pmc_din_pass(default_config):
 
 
 def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+    # one write per line: ranks share the parent's stderr and run with -u, so
+    # print's separate text / newline writes could interleave between ranks
+    sys.stderr.write(" ".join(str(x) for x in a) + "\n")
+    sys.stderr.flush()
 
 
 def recall_workload(seed: int, n_users: int, n_items: int, dim: int, device):

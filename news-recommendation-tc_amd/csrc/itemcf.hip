@@ -25,27 +25,90 @@
 // workgroup, coalesced 16-element strips.
 #include "nrk_common.h"
 
+#include <climits>
+#include <cmath>
+
 namespace nrk {
 
 constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys per workgroup
 constexpr int64_t CF_HEAVY = 4096;               // top-n rows longer than this get a workgroup
+// LDS tile images of 4096 8-byte values read as thread-contiguous chunks of
+// 16: one pad slot per 16 keeps the chunk reads free of bank conflicts
+__device__ __forceinline__ int cf_pad(int i) { return i + (i >> 4); }
+constexpr int CF_SW = RS_TILE + RS_TILE / 16;
 
 // ------------------------------------------------------ pair offsets --
-// pair_off[u] = sum_{v<u} L_v^2 (exclusive), pair_off[n] = total.  One
-// workgroup of 1024 threads: contiguous chunks, block scan of chunk sums.
-__global__ __launch_bounds__(1024) void cf_pair_offsets_kernel(const int64_t* __restrict__ offsets,
-                                                               int64_t n, int64_t* __restrict__ pair_off) {
+// Exclusive int64 scans over users / queries (pair_off[u] = sum_{v<u} L_v^2,
+// the recall's candidate offsets): three launches -- per-tile totals, one
+// workgroup over the tile totals, per-tile scan + carry -- with every tile
+// of 4096 values staged in LDS by coalesced loads (one thread-contiguous
+// chunk of 16 per thread, padded against bank conflicts).  out may alias
+// the values (rc: in place); out[n] = total.
+struct ScanPairs {  // L_u^2 from the CSR offsets
+    const int64_t* offsets;
+    __device__ int64_t operator()(int64_t u) const {
+        const int64_t L = offsets[u + 1] - offsets[u];
+        return L * L;
+    }
+};
+struct ScanVals {
+    const int64_t* v;
+    __device__ int64_t operator()(int64_t u) const { return v[u]; }
+};
+
+// stage tile b's values, scan them in place (exclusive, tile-local); returns
+// the tile total (every thread)
+template <typename F>
+__device__ __forceinline__ int64_t scan_tile(F f, int64_t n, int64_t* sv, int64_t* part) {
+    const int tid = threadIdx.x;
+    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    for (int i = tid; i < RS_TILE; i += RS_THREADS) {
+        const int64_t e = t0 + i;
+        sv[cf_pad(i)] = e < n ? f(e) : 0;
+    }
+    __syncthreads();
+    int64_t s = 0;
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) s += sv[cf_pad(tid * RS_ITEMS + r)];
+    part[tid] = s;
+    __syncthreads();
+    for (int d = 1; d < RS_THREADS; d <<= 1) {
+        const int64_t v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int64_t run = part[tid] - s;
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const int k = cf_pad(tid * RS_ITEMS + r);
+        const int64_t v = sv[k];
+        sv[k] = run;
+        run += v;
+    }
+    const int64_t tot = part[RS_THREADS - 1];
+    __syncthreads();
+    return tot;
+}
+
+template <typename F>
+__global__ __launch_bounds__(RS_THREADS) void scan_totals_kernel(F f, int64_t n, int64_t* __restrict__ tot) {
+    __shared__ int64_t sv[CF_SW];
+    __shared__ int64_t part[RS_THREADS];
+    const int64_t t = scan_tile(f, n, sv, part);
+    if (threadIdx.x == 0) tot[blockIdx.x] = t;
+}
+
+// exclusive scan of the nb tile totals in place (one workgroup, chunked)
+__global__ __launch_bounds__(1024) void scan_top_kernel(int64_t* __restrict__ tot, int nb) {
     __shared__ int64_t part[1024];
     const int tid = threadIdx.x;
-    const int64_t chunk = (n + 1023) / 1024;
-    const int64_t a = tid * chunk, e = a + chunk < n ? a + chunk : n;
+    const int chunk = (nb + 1023) / 1024;
+    const int a = tid * chunk, e = a + chunk < nb ? a + chunk : nb;
     int64_t s = 0;
-    for (int64_t u = a; u < e; ++u) {
-        const int64_t L = offsets[u + 1] - offsets[u];
-        s += L * L;
-    }
+    for (int k = a; k < e; ++k) s += tot[k];
     part[tid] = s;
     __syncthreads();
     for (int d = 1; d < 1024; d <<= 1) {
@@ -54,19 +117,67 @@ __global__ __launch_bounds__(1024) void cf_pair_offsets_kernel(const int64_t* __
         part[tid] += v;
         __syncthreads();
     }
-    int64_t run = part[tid] - s;  // exclusive
-    for (int64_t u = a; u < e; ++u) {
-        pair_off[u] = run;
-        const int64_t L = offsets[u + 1] - offsets[u];
-        run += L * L;
+    int64_t run = part[tid] - s;
+    for (int k = a; k < e; ++k) {
+        const int64_t v = tot[k];
+        tot[k] = run;
+        run += v;
     }
-    if (tid == 1023) pair_off[n] = part[1023];
+    if (tid == 1023) tot[nb] = part[1023];
+}
+
+template <typename F>
+__global__ __launch_bounds__(RS_THREADS) void scan_apply_kernel(F f, int64_t n, const int64_t* __restrict__ tot,
+                                                                int nb, int64_t* __restrict__ out) {
+    __shared__ int64_t sv[CF_SW];
+    __shared__ int64_t part[RS_THREADS];
+    (void)scan_tile(f, n, sv, part);  // every value read before any is written (in-place safe)
+    const int64_t base = tot[blockIdx.x];
+    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    for (int i = threadIdx.x; i < RS_TILE; i += RS_THREADS) {
+        const int64_t e = t0 + i;
+        if (e < n) out[e] = base + sv[cf_pad(i)];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = tot[nb];
+}
+
+// tile totals buffer: nb + 1 int64
+static inline int64_t scan_tiles(int64_t n) { return (n + RS_TILE - 1) / RS_TILE; }
+
+// the nb + 1 tile totals live in a stream-ordered allocation (the C ABI of
+// these two entry points has no workspace argument)
+template <typename F>
+static int scan_exclusive(F f, int64_t n, int64_t* out, hipStream_t s) {
+    const int64_t nb = scan_tiles(n);
+    if (nb == 0) return hipMemsetAsync(out, 0, sizeof(int64_t), s) == hipSuccess ? NRK_OK : NRK_EHIP;
+    if (nb >= (1ll << 31)) return NRK_EINVAL;
+    int64_t* tot = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&tot), (size_t)(nb + 1) * sizeof(int64_t), s) != hipSuccess)
+        return NRK_EHIP;
+    scan_totals_kernel<F><<<(unsigned)nb, RS_THREADS, 0, s>>>(f, n, tot);
+    scan_top_kernel<<<1, 1024, 0, s>>>(tot, (int)nb);
+    scan_apply_kernel<F><<<(unsigned)nb, RS_THREADS, 0, s>>>(f, n, tot, (int)nb, out);
+    return hipFreeAsync(tot, s) == hipSuccess ? NRK_OK : NRK_EHIP;
 }
 
 // ------------------------------------------------------------- 1. pairs --
 struct CfParams {
     double loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha;
+    int64_t dt_zero;  // |dt| >= dt_zero -> pow(time_alpha, dt) is +0 (cf_dt_zero)
 };
+
+// Smallest |dt| from which time_alpha^|dt| lies below 2^-1100 for every dt
+// at or past it: any faithfully rounded pow returns +0 there, so the
+// kernels skip the pow (and exp(+0) = 1 exactly) -- bit-identical to
+// evaluating it.  Click timestamps are milliseconds (0.7^dt underflows from
+// dt ~ 2,100 ms on), so this is nearly every pair.  No shortcut unless
+// 0 < time_alpha < 1.
+static inline int64_t cf_dt_zero(double time_alpha) {
+    if (!(time_alpha > 0.0 && time_alpha < 1.0)) return INT64_MAX;
+    const double l2 = -std::log2(time_alpha);  // > 0
+    const double d = std::ceil(1100.0 / l2) + 1.0;
+    return d < 9.0e18 ? (int64_t)d : INT64_MAX;
+}
 
 __global__ __launch_bounds__(256) void cf_pairs_kernel(
     const int64_t* __restrict__ offsets, int64_t n_users, const int32_t* __restrict__ items,
@@ -76,6 +187,10 @@ __global__ __launch_bounds__(256) void cf_pairs_kernel(
     unsigned long long* __restrict__ cnt) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4;
+    // beta^dl for dl < 64 (the same device pow of the same arguments: same bits)
+    __shared__ double lwt[64];
+    if (threadIdx.x < 64) lwt[threadIdx.x] = pow(prm.loc_beta, (double)threadIdx.x);
+    __syncthreads();
     for (int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < n_users; u += nw) {
         const int64_t b = offsets[u];
         const int64_t L = offsets[u + 1] - b;
@@ -83,18 +198,19 @@ __global__ __launch_bounds__(256) void cf_pairs_kernel(
         // user_penalty = 1 / log_penalty(len) = 1 / log(L + 1) (item_cf.py:69-71)
         const double pen = 1.0 / log((double)(L + 1));
         for (int64_t l = lane; l < L; l += 64) atomicAdd(&cnt[items[b + l]], 1ull);
+        const bool small = L * L < (1ll << 31);  // 32-bit pair -> (l1, l2) division
         for (int64_t s = lane; s < L * L; s += 64) {
-            const int64_t l1 = s / L, l2 = s - l1 * L;
+            const int64_t l1 = small ? (int64_t)((uint32_t)s / (uint32_t)L) : s / L, l2 = s - l1 * L;
             const int32_t i = items[b + l1], j = items[b + l2];
             uint64_t key = sentinel;
             double wt = 0.0;
             if (i != j) {
                 const double la = l2 > l1 ? prm.loc_alpha : prm.loc_alpha_rev;
                 const int64_t dl = (l2 > l1 ? l2 - l1 : l1 - l2) - 1;
-                const double loc_w = la * pow(prm.loc_beta, (double)dl);
+                const double loc_w = la * (dl < 64 ? lwt[dl] : pow(prm.loc_beta, (double)dl));
                 const int64_t ti = ts[b + l1], tj = ts[b + l2];
                 const int64_t dt = ti > tj ? ti - tj : tj - ti;
-                const double click_w = exp(pow(prm.time_alpha, (double)dt));
+                const double click_w = dt >= prm.dt_zero ? 1.0 : exp(pow(prm.time_alpha, (double)dt));
                 const double created_w = exp(pow(prm.created_alpha, fabs(created[i] - created[j])));
                 wt = loc_w * click_w * created_w * pen;
                 key = ((uint64_t)(uint32_t)i << bj) | (uint32_t)j;
@@ -248,8 +364,37 @@ __device__ __forceinline__ SegSum seg_combine(SegSum a, SegSum b) {
     return SegSum{b.f ? b.v : a.v + b.v, a.f | b.f};
 }
 
-__device__ __forceinline__ bool cf_brk(const uint64_t* keys, int64_t e) {
-    return e == 0 || keys[e - 1] != keys[e];
+// The per-thread chunks below (thread t owns keys [16t, 16t + 16) of the
+// tile: the fixed association of the segmented sums) are read from LDS.  The
+// tile is staged by coalesced loads first -- chunk-strided global reads (a
+// 128-B stride across the lanes) re-fetched each line once per element:
+//   fl[i]  = run-break (key differs from the previous one, or e = 0) | sentinel << 1
+//            for keys t0 + i, i in [0, RS_TILE] (one past the tile: the
+//            last-of-run test of the tile's final key);
+//   sw[.]  = the weights, padded by one slot per 16 (conflict-free chunk reads).
+// Keys themselves are only read at run heads / ends (once per distinct key).
+constexpr int CF_FL = RS_TILE + 16;
+
+__device__ __forceinline__ void cf_stage_flags(const uint64_t* __restrict__ keys, int64_t n, int64_t t0,
+                                               uint64_t sentinel, uint8_t* fl) {
+    for (int i = threadIdx.x; i <= RS_TILE; i += RS_THREADS) {
+        const int64_t e = t0 + i;
+        uint8_t f = 0;
+        if (e < n) {
+            const uint64_t k = keys[e];
+            f = (uint8_t)(((e == 0 || keys[e - 1] != k) ? 1 : 0) | (k == sentinel ? 2 : 0));
+        }
+        fl[i] = f;
+    }
+}
+
+// this thread's 16 flags (one 16-B LDS read) + the next chunk's first
+__device__ __forceinline__ void cf_chunk_flags(const uint8_t* fl, int l0, uint8_t (&f)[RS_ITEMS + 1]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(fl + l0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) f[r] = (uint8_t)(w[r >> 2] >> (8 * (r & 3)));
+    f[RS_ITEMS] = fl[l0 + RS_ITEMS];
 }
 
 // 1. per tile: emitted-head count, the tile's segmented aggregate, and the
@@ -258,22 +403,36 @@ __global__ __launch_bounds__(RS_THREADS) void cf_tile_reduce(
     const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, const double* __restrict__ w,
     int64_t n, uint64_t sentinel, uint32_t* __restrict__ blkcnt, double* __restrict__ tail,
     int32_t* __restrict__ brk, double* __restrict__ ws) {
+    __shared__ __attribute__((aligned(16))) uint8_t fl[CF_FL];
+    __shared__ double sw[CF_SW];
     __shared__ double tv[RS_THREADS];
     __shared__ int tf[RS_THREADS];
     __shared__ uint32_t c;
     const int tid = threadIdx.x;
     if (tid == 0) c = 0;
-    const int64_t a = (int64_t)blockIdx.x * RS_TILE + (int64_t)tid * RS_ITEMS;
+    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    cf_stage_flags(keys, n, t0, sentinel, fl);
+#pragma unroll 4
+    for (int i = tid; i < RS_TILE; i += RS_THREADS) {
+        const int64_t e = t0 + i;
+        if (e < n) {
+            const double x = w[vals[e]];
+            ws[e] = x;
+            sw[cf_pad(i)] = x;
+        }
+    }
+    __syncthreads();
+    const int l0 = tid * RS_ITEMS;
+    const int64_t a = t0 + l0;
+    uint8_t f[RS_ITEMS + 1];
+    cf_chunk_flags(fl, l0, f);
     SegSum agg{0.0, 0};
     uint32_t my = 0;
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const int64_t e = a + r;
-        if (e >= n) break;
-        const double x = w[vals[e]];
-        ws[e] = x;
-        const bool b = cf_brk(keys, e);
-        if (b && keys[e] != sentinel) ++my;
-        agg = seg_combine(agg, SegSum{x, b ? 1 : 0});
+        if (a + r >= n) break;
+        const bool b = f[r] & 1;
+        if (f[r] == 1) ++my;  // a run head that is not the sentinel
+        agg = seg_combine(agg, SegSum{sw[cf_pad(l0 + r)], b ? 1 : 0});
     }
     tv[tid] = agg.v;
     tf[tid] = agg.f;
@@ -355,19 +514,30 @@ __global__ __launch_bounds__(RS_THREADS) void cf_emit(
     const unsigned long long* __restrict__ cnt, const int32_t* __restrict__ slots, int bj,
     int32_t* __restrict__ out_i, int32_t* __restrict__ out_j, double* __restrict__ out_v,
     int64_t* __restrict__ out_first) {
+    __shared__ __attribute__((aligned(16))) uint8_t fl[CF_FL];
+    __shared__ double sw[CF_SW];
     __shared__ double pv[RS_THREADS];
     __shared__ int pf[RS_THREADS];
     __shared__ uint32_t ph[RS_THREADS];
     const int tid = threadIdx.x;
-    const int64_t a = (int64_t)blockIdx.x * RS_TILE + (int64_t)tid * RS_ITEMS;
+    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    cf_stage_flags(keys, n, t0, sentinel, fl);
+#pragma unroll 4
+    for (int i = tid; i < RS_TILE; i += RS_THREADS) {
+        const int64_t e = t0 + i;
+        if (e < n) sw[cf_pad(i)] = ws[e];
+    }
+    __syncthreads();
+    const int l0 = tid * RS_ITEMS;
+    const int64_t a = t0 + l0;
+    uint8_t f[RS_ITEMS + 1];
+    cf_chunk_flags(fl, l0, f);
     SegSum agg{0.0, 0};
     uint32_t my = 0;
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const int64_t e = a + r;
-        if (e >= n) break;
-        const bool b = cf_brk(keys, e);
-        if (b && keys[e] != sentinel) ++my;
-        agg = seg_combine(agg, SegSum{ws[e], b ? 1 : 0});
+        if (a + r >= n) break;
+        if (f[r] == 1) ++my;
+        agg = seg_combine(agg, SegSum{sw[cf_pad(l0 + r)], (f[r] & 1) ? 1 : 0});
     }
     pv[tid] = agg.v;
     pf[tid] = agg.f;
@@ -397,10 +567,12 @@ __global__ __launch_bounds__(RS_THREADS) void cf_emit(
     for (int r = 0; r < RS_ITEMS; ++r) {
         const int64_t e = a + r;
         if (e >= n) break;
-        const uint64_t k = keys[e];
-        const bool b = cf_brk(keys, e);
-        run = seg_combine(run, SegSum{ws[e], b ? 1 : 0});
-        if (k == sentinel) continue;
+        const bool b = f[r] & 1;
+        run = seg_combine(run, SegSum{sw[cf_pad(l0 + r)], b ? 1 : 0});
+        if (f[r] & 2) continue;  // sentinel
+        const bool last = e + 1 == n || (f[r + 1] & 1);
+        if (!(b || last)) continue;
+        const uint64_t k = keys[e];  // run heads and ends only
         const int32_t i = (int32_t)(k >> bj), j = (int32_t)(k & jmask);
         if (b) {
             out_i[idx] = i;
@@ -408,7 +580,7 @@ __global__ __launch_bounds__(RS_THREADS) void cf_emit(
             out_first[idx] = slots ? slots[vals[e]] : vals[e];
             ++idx;
         }
-        if (e + 1 == n || keys[e + 1] != k) {  // last of the run: its sum
+        if (last) {  // last of the run: its sum
             const unsigned long long ci = cnt ? cnt[i] : 1ull, cj = cnt ? cnt[j] : 1ull;
             out_v[idx - 1] = cnt ? run.v / sqrt((double)(ci * cj)) : run.v;
         }
@@ -537,31 +709,6 @@ __global__ __launch_bounds__(256) void rc_count_kernel(const int64_t* __restrict
     }
 }
 
-// exclusive scan of n int64 counts -> off[0..n], one workgroup
-__global__ __launch_bounds__(1024) void rc_scan_kernel(const int64_t* __restrict__ cnt, int64_t n,
-                                                      int64_t* __restrict__ off) {
-    __shared__ int64_t part[1024];
-    const int tid = threadIdx.x;
-    const int64_t chunk = (n + 1023) / 1024;
-    const int64_t a = tid * chunk, e = a + chunk < n ? a + chunk : n;
-    int64_t s = 0;
-    for (int64_t u = a; u < e; ++u) s += cnt[u];
-    part[tid] = s;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int64_t v = tid >= d ? part[tid - d] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    int64_t run = part[tid] - s;
-    for (int64_t u = a; u < e; ++u) {  // (in place: cnt may alias off)
-        const int64_t c = cnt[u];
-        off[u] = run;
-        run += c;
-    }
-    if (tid == 1023) off[n] = part[1023];
-}
 
 struct RcParams {
     double loc_beta, created_alpha;
@@ -593,24 +740,39 @@ __global__ __launch_bounds__(256) void rc_cand_kernel(
         if (sl < 0) continue;
         const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
         int64_t c = cand_off[q];
-        // history of <= 64 clicks held one per lane: the in-history test is
-        // then L shuffles instead of L dependent global loads per neighbour
-        const int32_t hl = lane < L ? items[b + lane] : -1;
-        for (int64_t loc = 0; loc < L; ++loc) {
-            const int32_t i = items[b + loc];
-            const int n = nbr_cnt[i];
-            // position_weight(len(hist) - loc) (:92-95)
-            const double lw = pow(prm.loc_beta, (double)(L - loc));
-            for (int x0 = 0; x0 < n; x0 += 64) {  // uniform: the shuffles run converged
-                const int x = x0 + lane;
-                const int32_t j = x < n ? nbr_cols[(int64_t)i * prm.topn + x] : -2;
+        if (L <= 64) {
+            // history of <= 64 clicks held one per lane (the in-history test
+            // is L shuffles, not L dependent loads); the (loc, neighbour)
+            // candidates of all history positions are flattened over the
+            // wave -- lane f takes flat candidate f0 + f, its position loc
+            // found by a binary search of the lane-scanned neighbour counts
+            // (a row has <= topn neighbours, so one position per pass would
+            // leave most lanes idle).  Same values, same slots c + f.
+            const int32_t hl = lane < L ? items[b + lane] : -1;
+            const int nl = lane < L ? nbr_cnt[hl] : 0;
+            int inc = nl;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int t = __shfl_up(inc, d, 64);
+                if (lane >= d) inc += t;
+            }
+            const int total = __shfl(inc, 63, 64);
+            // position_weight(len(hist) - loc) (:92-95), lane loc
+            const double lwl = lane < L ? pow(prm.loc_beta, (double)(L - lane)) : 0.0;
+            for (int f0 = 0; f0 < total; f0 += 64) {  // uniform: the shuffles run converged
+                const int f = f0 + lane;
+                int loc = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1)
+                    if (__shfl(inc, loc + step - 1, 64) <= f) loc += step;
+                const int32_t i = __shfl(hl, loc, 64);
+                const int x = f - (__shfl(inc, loc, 64) - __shfl(nl, loc, 64));
+                const double lw = __shfl(lwl, loc, 64);
+                const bool ok = f < total;
+                const int32_t j = ok ? nbr_cols[(int64_t)i * prm.topn + x] : -2;
                 bool inh = false;
-                if (L <= 64) {
-                    for (int l = 0; l < (int)L; ++l) inh |= __shfl(hl, l, 64) == j;
-                } else if (x < n) {
-                    for (int64_t l = 0; l < L && !inh; ++l) inh = items[b + l] == j;
-                }
-                if (x >= n) continue;
+                for (int l = 0; l < (int)L; ++l) inh |= __shfl(hl, l, 64) == j;
+                if (!ok) continue;
                 const double wij = nbr_vals[(int64_t)i * prm.topn + x];
                 uint64_t key = sentinel;
                 double v = 0.0;
@@ -618,6 +780,37 @@ __global__ __launch_bounds__(256) void rc_cand_kernel(
                     // time_decay_weight(created_i, created_j) (:86-90)
                     const double cw = exp(pow(prm.created_alpha, fabs(created[i] - created[j])));
                     double content = 1.0;  // (:98-103)
+                    if (prm.ke > 0) {
+                        double e;
+                        if (rc_find(emb_cols + (int64_t)i * prm.ke, emb_vals + (int64_t)i * prm.ke, emb_cnt[i], j, e))
+                            content += e;
+                        if (rc_find(emb_cols + (int64_t)j * prm.ke, emb_vals + (int64_t)j * prm.ke, emb_cnt[j], i, e))
+                            content += e;
+                    }
+                    v = cw * lw * content * wij;
+                    key = ((uint64_t)q << prm.bj) | (uint32_t)j;
+                }
+                keys[c + f] = key;
+                vals[c + f] = (int32_t)(c + f);
+                contrib[c + f] = v;
+            }
+            continue;
+        }
+        // long histories: one position per pass, the in-history test by loads
+        for (int64_t loc = 0; loc < L; ++loc) {
+            const int32_t i = items[b + loc];
+            const int n = nbr_cnt[i];
+            const double lw = pow(prm.loc_beta, (double)(L - loc));
+            for (int x = lane; x < n; x += 64) {
+                const int32_t j = nbr_cols[(int64_t)i * prm.topn + x];
+                bool inh = false;
+                for (int64_t l = 0; l < L && !inh; ++l) inh = items[b + l] == j;
+                const double wij = nbr_vals[(int64_t)i * prm.topn + x];
+                uint64_t key = sentinel;
+                double v = 0.0;
+                if (!inh) {
+                    const double cw = exp(pow(prm.created_alpha, fabs(created[i] - created[j])));
+                    double content = 1.0;
                     if (prm.ke > 0) {
                         double e;
                         if (rc_find(emb_cols + (int64_t)i * prm.ke, emb_vals + (int64_t)i * prm.ke, emb_cnt[i], j, e))
@@ -922,7 +1115,11 @@ int nrk_itemcf_pair_offsets(const int64_t* offsets, int64_t n_users, int64_t* pa
     clear_error();
     NRK_REQUIRE(offsets && pair_off, "null pointer");
     NRK_REQUIRE(n_users >= 0, "n_users < 0");
-    cf_pair_offsets_kernel<<<1, 1024, 0, as_stream(stream)>>>(offsets, n_users, pair_off);
+    const int rc = scan_exclusive(ScanPairs{offsets}, n_users, pair_off, as_stream(stream));
+    if (rc != NRK_OK) {
+        set_error("nrk_itemcf_pair_offsets: scan workspace allocation / launch failed");
+        return rc;
+    }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -953,7 +1150,7 @@ int nrk_itemcf_sim(const int64_t* offsets, int64_t n_users, const int32_t* items
     const int nbits = 2 * bj;
     const uint64_t sentinel = (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
     (void)hipMemsetAsync(out_cnt, 0, sizeof(int64_t) * (size_t)n_items, s);
-    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha};
+    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha, cf_dt_zero(time_alpha)};
     const int64_t ugrid = (n_users + 3) / 4;
     if (n_users > 0)
         cf_pairs_kernel<<<(int)(ugrid < 65536 ? ugrid : 65536), 256, 0, s>>>(
@@ -1020,7 +1217,11 @@ int nrk_itemcf_recall_offsets(const int64_t* q_slot, int64_t n_query, const int6
         rc_count_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, s>>>(q_slot, n_query, offsets, items, nbr_cnt,
                                                                      cand_off);
     }
-    rc_scan_kernel<<<1, 1024, 0, s>>>(cand_off, n_query, cand_off);
+    const int rc = scan_exclusive(ScanVals{cand_off}, n_query, cand_off, s);
+    if (rc != NRK_OK) {
+        set_error("nrk_itemcf_recall_offsets: scan workspace allocation / launch failed");
+        return rc;
+    }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -1116,7 +1317,7 @@ int nrk_itemcf_pairs(const int64_t* offsets, int64_t n_users, const int32_t* ite
     const int bj = bits_for(n_items);
     const int nbits = 2 * bj;
     const uint64_t sentinel = (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
-    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha};
+    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha, cf_dt_zero(time_alpha)};
     const int64_t ugrid = (n_users + 3) / 4;
     cf_pairs_kernel<<<(int)(ugrid < 65536 ? ugrid : 65536), 256, 0, as_stream(stream)>>>(
         offsets, n_users, items, ts, created, pair_off, slot_base, prm, bj, sentinel, keys, slots, w,

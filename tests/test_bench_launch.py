@@ -3,6 +3,7 @@ shape has no torch.distributed launcher around it).  The dry run goes through
 the same launcher and rendezvous over gloo, without the GPU workload."""
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -22,10 +23,9 @@ def test_bench_gpus2_launches_two_ranks():
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout  # rank 0 only
     assert json.loads(lines[0])["n_gpus"] == 2
-    ranks = sorted(ln.split("]")[0] for ln in p.stderr.splitlines() if ln.startswith("[rank "))
-    assert ranks == ["[rank 0/2", "[rank 1/2"], p.stderr
-    pids = {ln.split("pid ")[1].split()[0] for ln in p.stderr.splitlines() if ln.startswith("[rank ")}
-    assert len(pids) == 2  # two distinct worker processes
+    found = re.findall(r"\[rank (\d+)/2\] local_rank \d+ pid (\d+)", p.stderr)
+    assert sorted(r for r, _ in found) == ["0", "1"], p.stderr
+    assert len({pid for _, pid in found}) == 2  # two distinct worker processes
 
 
 def test_bench_gpus1_stays_single_process():
