@@ -53,6 +53,7 @@ struct CatalogHdr {
     float scale;     // power of two applied before the fp16 conversion
     int32_t dim;
     int32_t dp;
+    float max_dnorm;  // max_j ||fp16(v_j * scale) / scale - v_j||_2 (rounded up)
 };
 
 // 2^(14 - e) where m = f * 2^e, f in [0.5, 1): maps max |x| into [2^13, 2^14)
@@ -121,6 +122,28 @@ __global__ void catalog_norm_kernel(const float* __restrict__ items, int64_t n_i
         atomicMax((unsigned int*)&hdr->max_norm, __float_as_uint(m));
         atomicMax((unsigned int*)&hdr->max_abs, __float_as_uint(a));
     }
+}
+
+// max_j of the fp16 rounding error norm of item j, exactly as catalog_pack
+// rounds it (for the screen's error bound eps)
+__global__ void catalog_dnorm_kernel(const float* __restrict__ items, int64_t n_items, int dim,
+                                     CatalogHdr* hdr) {
+    const float scale = hdr->scale;
+    double m = 0.0;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_items;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int d = 0; d < dim; ++d) {
+            const float f = items[r * dim + d];
+            const float x = (float)(_Float16)(f * scale);  // catalog_pack's rounding
+            const double e = (double)x / (double)scale - (double)f;
+            s += e * e;
+        }
+        m = fmax(m, sqrt(s));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, WAVE));
+    if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)&hdr->max_dnorm, __float_as_uint((float)(m * (1.0 + 1e-6))));
 }
 
 __global__ void catalog_hdr_kernel(CatalogHdr* hdr, int dim, int dp) {
@@ -355,14 +378,28 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && CL < 64) ? 2 : NW / 4) void ip
     uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
     const float su = pow2_scale(uabs);
     f16x8 ufrag[DS];
+    float du2 = 0.0f;  // ||fp16(u su) - u su||^2 (scaled units; each difference exact)
 #pragma unroll
     for (int s = 0; s < DS; ++s)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ufrag[s][e] = (_Float16)(uval[s][e] * su);
-    // |fp16 score - exact| <= (2^-10 + 2^-22 + (D-1) 2^-24 (1+2^-11)^2) ||u|| ||v||
-    // (+ subnormal terms, < 2^-30 relative after the power-of-two scaling).
-    const float ceps = 9.765625e-4f + 3.0517578e-5f + (float)DP * 1.1920929e-7f;
-    const float eps = (nrm2 == 0.0f) ? 0.0f : ceps * sqrtf(nrm2) * vmax * 1.0001f + 1e-30f;
+        for (int e = 0; e < 8; ++e) {
+            const float a = uval[s][e] * su;
+            ufrag[s][e] = (_Float16)a;
+            const float d = (float)ufrag[s][e] - a;
+            du2 += d * d;
+        }
+    du2 += __shfl_xor(du2, 32, WAVE);
+    // |fp16 score - exact| = |du.v + u.dv + du.dv + accumulation| with du, dv
+    // the actual fp16 rounding errors of this user and of the items:
+    //   <= ||du|| max||v|| + ||u|| max||dv|| + ||du|| max||dv||
+    //      + (2^-15 + D 2^-23) ||u|| max||v||  (fp32 accumulation of the exact
+    //        fp16 products in any order, with the round-1 bound's margins);
+    // ||du|| is measured here, max||dv|| by catalog_dnorm_kernel -- about
+    // 0.65x of round 1's worst case 2^-10 ||u|| max||v||.
+    const float nu = sqrtf(nrm2), ndu = sqrtf(du2) / su, dvmax = hdr->max_dnorm;
+    const float ceps = 3.0517578e-5f + (float)DP * 1.1920929e-7f;
+    const float eps = (nrm2 == 0.0f) ? 0.0f
+                                     : (ndu * vmax + nu * dvmax + ndu * dvmax + ceps * nu * vmax) * 1.0001f + 1e-30f;
     const float scl = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
     const float eps_s = eps * scl;
 
@@ -1074,6 +1111,8 @@ int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* cat
     }
     catalog_hdr_kernel<<<1, 1, 0, s>>>(hdr, dim, dp);
     if (total > 0) {
+        const int g2 = (int)std::min<int64_t>((n_items + 255) / 256, 2048);
+        catalog_dnorm_kernel<<<g2, 256, 0, s>>>(items, n_items, dim, hdr);
         const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
         catalog_pack_kernel<<<grid, 256, 0, s>>>(items, n_items, dim, dp, hdr,
                                                  reinterpret_cast<uint4*>(catalog));
