@@ -45,8 +45,8 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
-BUSY_FILE = os.path.join(REPO, "profiles", "r02_busy.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02e_traffic.json")
+BUSY_FILE = os.path.join(REPO, "profiles", "r02e_busy.json")
 
 
 def pmc_busy(kernels, default_config):
@@ -80,9 +80,12 @@ def pmc_traffic(kernels, default_config):
     ks = tf["kernels"]
     tot = 0.0
     for k in kernels:
-        if k not in ks:
+        # a name prefix ("nrk::ip_screen_kernel<32,") matches the one
+        # instantiation the default config runs
+        m = [v for name, v in ks.items() if name == k or name.startswith(k)]
+        if len(m) != 1:
             return None
-        tot += ks[k]["traffic_bytes_per_launch"]
+        tot += m[0]["traffic_bytes_per_launch"]
     return tot
 
 
@@ -549,7 +552,7 @@ def run_din(args, device, rank, world):
            "samples": n, "batch": B, "seq_len": T, "dtype": "fp32 math, bf16 tables",
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": din_traffic,
-                        "traffic_unit": "bytes per pass, every launch of one nrk_din_forward_segments call (profiles/r01_traffic.json din_pass)",
+                        "traffic_unit": "bytes per pass, every launch of one nrk_din_forward_segments call (profiles/r02e_traffic.json din_pass)",
                         "kernel": f"nrk_din_forward_segments ({n} samples in Dice batches of {B}, one call)",
                         "kernel_ms": round(pass_ms, 4),
                         "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * n,
@@ -795,15 +798,15 @@ def main(argv=None):
     flops = 2.0 * U * cat.n * D
     achieved = flops / (screen_ms * 1e-3) / 1e12
     default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and not catalog_mode
-    traffic = pmc_traffic(["nrk::ip_screen_kernel<32, 8>"], default_cfg)
+    traffic = pmc_traffic(["nrk::ip_screen_kernel<32,"], default_cfg)
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                 "traffic": round(traffic) if traffic else None,
-                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r01_traffic.json)",
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r02e_traffic.json)",
                 "kernel": "ip_screen_kernel<32> (fp16 MFMA 32x32x16)", "kernel_ms": round(screen_ms, 4),
                 "algorithmic_flop_per_launch": flops,
                 "busy": pmc_busy(["nrk::ip_screen_kernel", "nrk::ip_refine_kernel", "nrk::tt_user_kernel"], default_cfg),
-                "busy_source": "profiles/r02_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
+                "busy_source": "profiles/r02e_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
                                "SQ_WAIT_ANY, GRBM_GUI_ACTIVE passes; tools/pmc_busy.py)"}
 
     cpu = None
