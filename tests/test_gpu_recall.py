@@ -235,3 +235,41 @@ def test_catalog_shards_bound_full_size(ops):
     so, ro = oracle.ip_topk(users[sample].cpu().numpy(), items.cpu().numpy(), K, nthreads=8)
     assert np.array_equal(r[sample].cpu().numpy().astype(np.int64), ro)
     assert np.array_equal(s[sample].cpu().numpy(), so)
+
+
+@pytest.mark.parametrize("d", [16, 32, 64])
+def test_screen_eps_bounds_the_fp16_rounding(ops, d):
+    """The screen's per-user error bound (ucut.y, ip_topk.hip ip_screen_kernel:
+    ||du|| max||v|| + ||u|| max||dv|| + ||du|| max||dv|| + accumulation) must
+    cover |fp16 score - exact| for every (user, item): the fp16 scores are
+    re-derived here exactly (float16 rounding of the power-of-two scaled
+    rows, products summed in float64, so no accumulation error -- the
+    rounding part of the bound is what is tested).  Rows of very different
+    norms and a few tiny components stress both sides."""
+    rng = np.random.default_rng(7 + d)
+    U, I, K = 384, 20000, 31
+    users = (rng.standard_normal((U, d)) * np.exp(rng.standard_normal((U, 1)))).astype(np.float32)
+    items = (rng.standard_normal((I, d)) * np.exp(rng.standard_normal((I, 1)))).astype(np.float32)
+    items[::97, : d // 4] *= np.float32(1e-6)  # components deep below the fp16 normal range
+    cat = ops.Catalog(_dev(items))
+    ws = ops.ip_topk_workspace(U, cat, K, "cuda")
+    ops.ip_topk_screen(_dev(users), cat, K, ws)
+    torch.cuda.synchronize()
+    # workspace layout (ip_ws_layout): 256 B, candidate lists, then ucut float2 [U]
+    off = 256 + ((U * 2 * 48 * 8 + 255) // 256) * 256
+    eps = ws[off: off + U * 8].view(torch.float32).view(U, 2)[:, 1].double().cpu().numpy()
+
+    def p2(maxabs):  # pow2_scale: maps max|x| into [2^13, 2^14)
+        _, e = np.frexp(maxabs)
+        return np.ldexp(1.0, 14 - e)
+
+    su = p2(np.abs(users).max(1)).astype(np.float32)[:, None]
+    sv = np.float32(p2(np.abs(items).max()))
+    u16 = (users * su).astype(np.float16).astype(np.float64) / su
+    v16 = (items * sv).astype(np.float16).astype(np.float64) / np.float64(sv)
+    exact = users.astype(np.float64) @ items.astype(np.float64).T
+    err = np.abs(u16 @ v16.T - exact).max(1)
+    assert np.all(err <= eps), float((err / eps).max())
+    # and it is the tighter form: well under round 1's 2^-10 ||u|| max||v|| worst case
+    old = 9.765625e-4 * np.linalg.norm(users.astype(np.float64), axis=1) * np.linalg.norm(items, axis=1).max()
+    assert np.all(eps < 0.9 * old), float((eps / old).max())
