@@ -24,6 +24,9 @@ __global__ __launch_bounds__(256) void tt_user_kernel(
     float* sb0 = sw0 + h0 * S0;     // [h0]
     float* sw1 = sb0 + h0;          // [h1][S1]
     float* sb1 = sw1 + h1 * S1;     // [h1]
+    // per-wave broadcast rows for the two matvecs: [x (2D) | y0 (h0)]; every
+    // lane reads the same word (LDS broadcast) instead of a v_readlane per term
+    float* sx = sb1 + h1 + (threadIdx.x >> 6) * (2 * D + 128);
     for (int i = threadIdx.x; i < h0 * 2 * D; i += blockDim.x) sw0[(i / (2 * D)) * S0 + i % (2 * D)] = w0[i];
     for (int i = threadIdx.x; i < h0; i += blockDim.x) sb0[i] = b0[i];
     for (int i = threadIdx.x; i < h1 * h0; i += blockDim.x) sw1[(i / h0) * S1 + i % h0] = w1[i];
@@ -73,7 +76,13 @@ __global__ __launch_bounds__(256) void tt_user_kernel(
         for (int off = D; off < WAVE; off <<= 1) sum += __shfl_xor(sum, off, WAVE);
         // lane q < D holds x[q] = E_u[uid][q] and x[D + q] = mean[q]
         const float xm = sum / ((float)len + 1e-8f);
-        // layer 0: lane o (and o + 64) owns output o
+        // layer 0: lane o (and o + 64) owns output o; same fma order as a
+        // q-ascending dot (inputs broadcast from LDS)
+        if (lane < D) {
+            sx[lane] = xu;
+            sx[D + lane] = xm;
+        }
+        __builtin_amdgcn_wave_barrier();
         float y0 = 0.0f, y1 = 0.0f;
         {
             float z0 = lane < h0 ? sb0[lane] : 0.0f;
@@ -81,32 +90,27 @@ __global__ __launch_bounds__(256) void tt_user_kernel(
             const float* wr0 = sw0 + (lane < h0 ? lane : 0) * S0;
             const float* wr1 = sw0 + (lane + WAVE < h0 ? lane + WAVE : 0) * S0;
 #pragma unroll
-            for (int q = 0; q < D; ++q) {
-                const float xq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xu), q));
+            for (int q = 0; q < 2 * D; ++q) {
+                const float xq = sx[q];
                 z0 += wr0[q] * xq;
                 z1 += wr1[q] * xq;
-            }
-#pragma unroll
-            for (int q = 0; q < D; ++q) {
-                const float mq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xm), q));
-                z0 += wr0[D + q] * mq;
-                z1 += wr1[D + q] * mq;
             }
             y0 = fmaxf(z0, 0.0f);
             y1 = fmaxf(z1, 0.0f);
         }
         // layer 1: lane o < h1 owns output o
+        float* sy = sx + 2 * D;
+        if (lane < h0) sy[lane] = y0;
+        if (lane + WAVE < h0) sy[lane + WAVE] = y1;
+        __builtin_amdgcn_wave_barrier();
         float v = 0.0f;
         {
             float z = lane < h1 ? sb1[lane] : 0.0f;
             const float* wr = sw1 + (lane < h1 ? lane : 0) * S1;
-            const int q0 = h0 < WAVE ? h0 : WAVE;
-            for (int q = 0; q < q0; ++q)
-                z += wr[q] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y0), q));
-            for (int q = WAVE; q < h0; ++q)
-                z += wr[q] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y1), q - WAVE));
+            for (int q = 0; q < h0; ++q) z += wr[q] * sy[q];
             v = lane < h1 ? fmaxf(z, 0.0f) : 0.0f;
         }
+        __builtin_amdgcn_wave_barrier();  // sx / sy are rewritten for the next user
         const float nn = sqrtf(wave_sum_f32(v * v));
         v = v / fmaxf(nn, 1e-12f);
         float n2 = sqrtf(wave_sum_f32(v * v));
@@ -166,7 +170,8 @@ int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* i
     if (n == 0) return NRK_OK;
     NRK_REQUIRE(user_table && item_table && uid && hist && hist_len && w0 && b0 && w1 && b1 && out,
                 "null pointer");
-    const size_t lds = sizeof(float) * ((size_t)h0 * (2 * dim + 1) + h0 + (size_t)h1 * (h0 + 1) + h1);
+    const size_t lds = sizeof(float) * ((size_t)h0 * (2 * dim + 1) + h0 + (size_t)h1 * (h0 + 1) + h1 +
+                                        (size_t)4 * (2 * dim + 128));
     hipStream_t s = as_stream(stream);
     const int grid = (int)std::min<int64_t>((n + 3) / 4, 2048);
 #define NRK_TT_LAUNCH(DD)                                                                      \
