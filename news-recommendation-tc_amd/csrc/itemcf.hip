@@ -41,11 +41,14 @@ constexpr int CF_SW = RS_TILE + RS_TILE / 16;
 
 // ------------------------------------------------------ pair offsets --
 // Exclusive int64 scans over users / queries (pair_off[u] = sum_{v<u} L_v^2,
-// the recall's candidate offsets): three launches -- per-tile totals, one
-// workgroup over the tile totals, per-tile scan + carry -- with every tile
-// of 4096 values staged in LDS by coalesced loads (one thread-contiguous
-// chunk of 16 per thread, padded against bank conflicts).  out may alias
-// the values (rc: in place); out[n] = total.
+// the recall's candidate offsets): one workgroup of 1024 threads walks tiles
+// of 8,192 values -- coalesced loads into LDS, one thread-contiguous chunk of
+// 8 per thread, a wave shuffle scan + 16 wave totals, coalesced stores -- and
+// carries the running total.  No workspace (the C ABI of these two entry
+// points has none, and the library allocates nothing), in place when the
+// values alias out (every tile is loaded before it is written); out[n] = total.
+// Round 1's version read one 245-value chunk per thread, chunk-strided
+// (0.52 ms at 250k users).
 struct ScanPairs {  // L_u^2 from the CSR offsets
     const int64_t* offsets;
     __device__ int64_t operator()(int64_t u) const {
@@ -58,106 +61,61 @@ struct ScanVals {
     __device__ int64_t operator()(int64_t u) const { return v[u]; }
 };
 
-// stage tile b's values, scan them in place (exclusive, tile-local); returns
-// the tile total (every thread)
+constexpr int SCAN_PT = 8, SCAN_TILE = 1024 * SCAN_PT;
+
 template <typename F>
-__device__ __forceinline__ int64_t scan_tile(F f, int64_t n, int64_t* sv, int64_t* part) {
-    const int tid = threadIdx.x;
-    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
-    for (int i = tid; i < RS_TILE; i += RS_THREADS) {
-        const int64_t e = t0 + i;
-        sv[cf_pad(i)] = e < n ? f(e) : 0;
-    }
-    __syncthreads();
-    int64_t s = 0;
+__global__ __launch_bounds__(1024) void scan_exclusive_kernel(F f, int64_t n, int64_t* out) {  // out may alias f's values
+    __shared__ int64_t sv[SCAN_TILE + SCAN_TILE / 16];
+    __shared__ int64_t wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int64_t carry = 0;
+    for (int64_t t0 = 0; t0 < n; t0 += SCAN_TILE) {
+        int64_t v[SCAN_PT];
 #pragma unroll
-    for (int r = 0; r < RS_ITEMS; ++r) s += sv[cf_pad(tid * RS_ITEMS + r)];
-    part[tid] = s;
-    __syncthreads();
-    for (int d = 1; d < RS_THREADS; d <<= 1) {
-        const int64_t v = tid >= d ? part[tid - d] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    int64_t run = part[tid] - s;
+        for (int j = 0; j < SCAN_PT; ++j) {
+            const int64_t e = t0 + j * 1024 + tid;
+            v[j] = e < n ? f(e) : 0;
+        }
 #pragma unroll
-    for (int r = 0; r < RS_ITEMS; ++r) {
-        const int k = cf_pad(tid * RS_ITEMS + r);
-        const int64_t v = sv[k];
-        sv[k] = run;
-        run += v;
-    }
-    const int64_t tot = part[RS_THREADS - 1];
-    __syncthreads();
-    return tot;
-}
-
-template <typename F>
-__global__ __launch_bounds__(RS_THREADS) void scan_totals_kernel(F f, int64_t n, int64_t* __restrict__ tot) {
-    __shared__ int64_t sv[CF_SW];
-    __shared__ int64_t part[RS_THREADS];
-    const int64_t t = scan_tile(f, n, sv, part);
-    if (threadIdx.x == 0) tot[blockIdx.x] = t;
-}
-
-// exclusive scan of the nb tile totals in place (one workgroup, chunked)
-__global__ __launch_bounds__(1024) void scan_top_kernel(int64_t* __restrict__ tot, int nb) {
-    __shared__ int64_t part[1024];
-    const int tid = threadIdx.x;
-    const int chunk = (nb + 1023) / 1024;
-    const int a = tid * chunk, e = a + chunk < nb ? a + chunk : nb;
-    int64_t s = 0;
-    for (int k = a; k < e; ++k) s += tot[k];
-    part[tid] = s;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int64_t v = tid >= d ? part[tid - d] : 0;
+        for (int j = 0; j < SCAN_PT; ++j) sv[cf_pad(j * 1024 + tid)] = v[j];
         __syncthreads();
-        part[tid] += v;
+        int64_t c[SCAN_PT], sum = 0;
+#pragma unroll
+        for (int r = 0; r < SCAN_PT; ++r) {
+            c[r] = sv[cf_pad(tid * SCAN_PT + r)];
+            sum += c[r];
+        }
+        int64_t x = sum;  // inclusive over the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[wv] = x;
         __syncthreads();
+        int64_t wbase = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const int64_t t = wsum[w];
+            wbase += w < wv ? t : 0;
+            total += t;
+        }
+        int64_t run = carry + wbase + x - sum;
+#pragma unroll
+        for (int r = 0; r < SCAN_PT; ++r) {
+            sv[cf_pad(tid * SCAN_PT + r)] = run;
+            run += c[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SCAN_PT; ++j) {
+            const int64_t e = t0 + j * 1024 + tid;
+            if (e < n) out[e] = sv[cf_pad(j * 1024 + tid)];
+        }
+        carry += total;
+        __syncthreads();  // sv / wsum are rewritten by the next tile
     }
-    int64_t run = part[tid] - s;
-    for (int k = a; k < e; ++k) {
-        const int64_t v = tot[k];
-        tot[k] = run;
-        run += v;
-    }
-    if (tid == 1023) tot[nb] = part[1023];
-}
-
-template <typename F>
-__global__ __launch_bounds__(RS_THREADS) void scan_apply_kernel(F f, int64_t n, const int64_t* __restrict__ tot,
-                                                                int nb, int64_t* __restrict__ out) {
-    __shared__ int64_t sv[CF_SW];
-    __shared__ int64_t part[RS_THREADS];
-    (void)scan_tile(f, n, sv, part);  // every value read before any is written (in-place safe)
-    const int64_t base = tot[blockIdx.x];
-    const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
-    for (int i = threadIdx.x; i < RS_TILE; i += RS_THREADS) {
-        const int64_t e = t0 + i;
-        if (e < n) out[e] = base + sv[cf_pad(i)];
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = tot[nb];
-}
-
-// tile totals buffer: nb + 1 int64
-static inline int64_t scan_tiles(int64_t n) { return (n + RS_TILE - 1) / RS_TILE; }
-
-// the nb + 1 tile totals live in a stream-ordered allocation (the C ABI of
-// these two entry points has no workspace argument)
-template <typename F>
-static int scan_exclusive(F f, int64_t n, int64_t* out, hipStream_t s) {
-    const int64_t nb = scan_tiles(n);
-    if (nb == 0) return hipMemsetAsync(out, 0, sizeof(int64_t), s) == hipSuccess ? NRK_OK : NRK_EHIP;
-    if (nb >= (1ll << 31)) return NRK_EINVAL;
-    int64_t* tot = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void**>(&tot), (size_t)(nb + 1) * sizeof(int64_t), s) != hipSuccess)
-        return NRK_EHIP;
-    scan_totals_kernel<F><<<(unsigned)nb, RS_THREADS, 0, s>>>(f, n, tot);
-    scan_top_kernel<<<1, 1024, 0, s>>>(tot, (int)nb);
-    scan_apply_kernel<F><<<(unsigned)nb, RS_THREADS, 0, s>>>(f, n, tot, (int)nb, out);
-    return hipFreeAsync(tot, s) == hipSuccess ? NRK_OK : NRK_EHIP;
+    if (tid == 0) out[n] = carry;
 }
 
 // ------------------------------------------------------------- 1. pairs --
@@ -1115,11 +1073,7 @@ int nrk_itemcf_pair_offsets(const int64_t* offsets, int64_t n_users, int64_t* pa
     clear_error();
     NRK_REQUIRE(offsets && pair_off, "null pointer");
     NRK_REQUIRE(n_users >= 0, "n_users < 0");
-    const int rc = scan_exclusive(ScanPairs{offsets}, n_users, pair_off, as_stream(stream));
-    if (rc != NRK_OK) {
-        set_error("nrk_itemcf_pair_offsets: scan workspace allocation / launch failed");
-        return rc;
-    }
+    scan_exclusive_kernel<ScanPairs><<<1, 1024, 0, as_stream(stream)>>>(ScanPairs{offsets}, n_users, pair_off);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -1217,11 +1171,7 @@ int nrk_itemcf_recall_offsets(const int64_t* q_slot, int64_t n_query, const int6
         rc_count_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, s>>>(q_slot, n_query, offsets, items, nbr_cnt,
                                                                      cand_off);
     }
-    const int rc = scan_exclusive(ScanVals{cand_off}, n_query, cand_off, s);
-    if (rc != NRK_OK) {
-        set_error("nrk_itemcf_recall_offsets: scan workspace allocation / launch failed");
-        return rc;
-    }
+    scan_exclusive_kernel<ScanVals><<<1, 1024, 0, s>>>(ScanVals{cand_off}, n_query, cand_off);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
