@@ -115,7 +115,8 @@ int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
  *   k > n_lists * m leaves the cut unchanged.  New: no reference
  *   counterpart (a Faiss search is single-index). */
 int nrk_ip_topk_bound(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
-                      int m, float* out_bound, void* workspace, size_t workspace_bytes, nrk_stream_t stream);
+                      int k, int m, float* out_bound, void* workspace, size_t workspace_bytes,
+                      nrk_stream_t stream);
 int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, int m, int k, void* workspace,
                             size_t workspace_bytes, nrk_stream_t stream);
 

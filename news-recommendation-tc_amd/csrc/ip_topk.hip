@@ -1,44 +1,55 @@
 // ip_topk.hip -- brute-force user x item inner-product top-K on gfx950.
 //
 // Replaces faiss.IndexFlatIP.add/.search (src/recall/youtubednn_recaller.py
-// :493-494, :520).  Contract (= IndexFlatIP): exact inner product, score desc,
-// ties -> lower row.  "Exact" is the fp64 sum of the fp32 products,
-// accumulated in dimension order (the oracle's definition, oracle/nrk_oracle.c).
+// :493-494, :520; the second Faiss site src/similarity/embedding.py:46-50).
+// Contract (= IndexFlatIP): exact inner product, score desc, ties -> lower
+// row, -1 / -FLT_MAX padding when k exceeds the catalog.  "Exact" is the fp64
+// sum of the fp32 products accumulated in dimension order (the oracle's
+// definition, oracle/nrk_oracle.c).  Any k >= 1 up to IP_KMAX.
 //
-// Design (MI355X-first, see DESIGN.md "ip_topk"):
-//   1. ip_screen   -- the one dense contraction on MFMA: fp16 32x32x16 tiles
+// Design (MI355X-first):
+//   1. ip_scan    -- the one dense contraction on MFMA: fp16 32x32x16 tiles
 //      (power-of-two scaled, so the only error is fp16 rounding), items
-//      (A operand) streamed through LDS from a catalog pre-packed in
-//      fragment order, 32 users per wave (B operand) held in registers.
-//      Each lane owns one user x one 16-item half of every 32-item block.
-//      Per block the lane takes the max of its 16 scores and appends
-//      (half-block max, half-block id) to its LDS list, branch-free: the
-//      entry is always written and kept only if it beats the lane threshold
-//      tau = theta - 2*eps, theta = K-th largest listed half-block max (a
-//      lower bound of the K-th largest score: K distinct half-blocks each
-//      hold an item >= theta), eps bounds |fp16 score - exact|
-//      (eps = c(D) * ||u|| * max_j ||v_j||).  A full list is compacted by a
-//      register bitonic sort (all lanes at once, no serial LDS chains).
-//   2. ip_refine   -- one wave per user: fp64 exact rescoring of every item
-//      of the flagged half-blocks, keep items with exact score >= cut + eps
-//      (typically K + a few), wave bitonic sort on (score desc, row asc).
-//   3. ip_fallback -- users whose candidate band overflowed (dense exact or
-//      near ties, e.g. duplicated catalog rows): exact fp64 radix-select over
-//      the whole catalog.  Never taken on non-degenerate data.
+//      (A operand) streamed through an LDS ring by LDS-DMA, UG x 32 users per
+//      wave (B operands) in registers, so one LDS fragment read feeds UG
+//      MFMAs.  Each lane owns one 16-item half of every 32-item block for
+//      each of its users and takes the half-block max.  A half-block max that
+//      reaches the lane's cut tau is appended (score, half-block id) to the
+//      user's list in HBM; tau = theta - 2 eps, theta = the smaller of the two
+//      lanes' j-th largest maxima (2(j+1) >= k, so k distinct half-blocks each
+//      hold an item >= theta: a lower bound of the k-th score), kept as a
+//      sorted register list per lane.  No per-user lists in LDS and no list
+//      compaction in the scan: the LDS holds only the catalog ring.
+//   2. ip_select  -- one wave per user: theta = the exact k-th largest
+//      appended maximum (bit-wise radix select), the band = appended entries
+//      >= theta - 2 eps (every half-block that can hold a top-k item).
+//   3. ip_refine  -- one wave per user: fp64 exact rescoring of every item of
+//      the band (fp16 prefilter first), keep items with exact score >=
+//      cut + eps, wave bitonic sort on (score desc, row asc).
+//   4. ip_fallback -- users whose lists or band overflowed (dense exact or
+//      near ties, e.g. duplicated catalog rows), and every user when k >
+//      IP_KFAST: exact fp64 radix-select over the whole catalog, then a
+//      workgroup bitonic sort of the k winners.
 #include "nrk_common.h"
 
 #include <float.h>
+#include <math.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 namespace nrk {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int IP_CW = 48;  // candidate entries per (user, half) slot of the workspace
-constexpr int IP_KMAX = 32;
+constexpr int IP_KFAST = 128;   // largest k on the screen path
+constexpr int IP_KMAX = 2048;   // largest k at all (exact path above IP_KFAST)
+constexpr int IP_SEL = 256;     // appended maxima >= theta_lb held by the select
+constexpr int IP_BQ = 288;      // largest band (k = 128); the refine holds SV + 32 entries
+constexpr int IP_KRING = 256;   // prefilter-kept rows awaiting an exact round (ring, power of two)
 constexpr size_t CATALOG_HDR = 256;
 
 __host__ __device__ static inline int pad_dim(int d) {
@@ -70,7 +81,7 @@ static inline size_t catalog_body_bytes(int64_t n_items, int dp) {
 
 // --------------------------------------------------------- catalog build --
 // Thread -> one 16-byte fragment: block b, k-step s, lane l:
-//   8 bf16 of item 32b + (l & 31), dims 16s + 8(l >> 5) + [0, 8).
+//   8 fp16 of item 32b + (l & 31), dims 16s + 8(l >> 5) + [0, 8).
 __global__ void catalog_pack_kernel(const float* __restrict__ items, int64_t n_items, int dim,
                                     int dp, const CatalogHdr* __restrict__ hdr,
                                     uint4* __restrict__ out) {
@@ -153,56 +164,11 @@ __global__ void catalog_hdr_kernel(CatalogHdr* hdr, int dim, int dp) {
 }
 
 // ------------------------------------------------------------- screening --
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-
+// theta - two_eps rounded toward -inf (one ulp below the fp32 result)
 __device__ __forceinline__ float round_down_sub(float theta, float two_eps) {
     float c = theta - two_eps;
     return __uint_as_float(c > 0.0f ? __float_as_uint(c) - 1u
                                     : (c == 0.0f ? 0x80000001u : __float_as_uint(c) + 1u));
-}
-
-// ---- per-user candidate lists ---------------------------------------------
-// Each wave owns 32 users; user q's list lives in LDS as two SoA planes
-// (scores f32, half-block ids u32), entry j at plane + (j * 32 + q) * 4, so
-// the 32 lanes of a half-wave touch 128 consecutive bytes.  Both lanes of a
-// user (h = 0, 1: the two 16-item halves of every 32-item block) append to
-// the same list and keep identical copies of its count n, cut tau and theta.
-constexpr int SC_CL = 64;  // entries per user list (default variant)
-
-__device__ __forceinline__ float lds_rd(uint32_t a) {
-    float v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-    return v;
-}
-__device__ __forceinline__ void lds_wr(uint32_t a, uint32_t v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-// v0 at a, v1 at a + OFF (one address register)
-template <int OFF>
-__device__ __forceinline__ void lds_wr_pair(uint32_t a, uint32_t v0, uint32_t v1) {
-    asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %0, %2 offset:%c3" ::"v"(a), "v"(v0), "v"(v1), "n"(OFF)
-                 : "memory");
-}
-// 16 dwords at a + i * stride (i = 0..15), one wait for all of them.  Inline
-// asm: hipcc's waitcnt pass would drain the in-flight LDS-DMA (the ring
-// prefetch) in front of any compiler-visible LDS access.
-template <int STRIDE>
-__device__ __forceinline__ void lds_rd16(uint32_t a, uint32_t (&o)[16]) {
-    asm volatile(
-        "ds_read_b32 %0, %16 offset:%c17*0\n\tds_read_b32 %1, %16 offset:%c17*1\n\t"
-        "ds_read_b32 %2, %16 offset:%c17*2\n\tds_read_b32 %3, %16 offset:%c17*3\n\t"
-        "ds_read_b32 %4, %16 offset:%c17*4\n\tds_read_b32 %5, %16 offset:%c17*5\n\t"
-        "ds_read_b32 %6, %16 offset:%c17*6\n\tds_read_b32 %7, %16 offset:%c17*7\n\t"
-        "ds_read_b32 %8, %16 offset:%c17*8\n\tds_read_b32 %9, %16 offset:%c17*9\n\t"
-        "ds_read_b32 %10, %16 offset:%c17*10\n\tds_read_b32 %11, %16 offset:%c17*11\n\t"
-        "ds_read_b32 %12, %16 offset:%c17*12\n\tds_read_b32 %13, %16 offset:%c17*13\n\t"
-        "ds_read_b32 %14, %16 offset:%c17*14\n\tds_read_b32 %15, %16 offset:%c17*15\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]),
-          "=&v"(o[6]), "=&v"(o[7]), "=&v"(o[8]), "=&v"(o[9]), "=&v"(o[10]), "=&v"(o[11]),
-          "=&v"(o[12]), "=&v"(o[13]), "=&v"(o[14]), "=&v"(o[15])
-        : "v"(a), "n"(STRIDE)
-        : "memory");
 }
 
 // value of lane l ^ 32 (v_permlane32_swap: lanes 32-63 of vdst <-> lanes
@@ -215,220 +181,126 @@ __device__ __forceinline__ float partner32f(float v, int h) {
     return __uint_as_float(partner32(__float_as_uint(v), h));
 }
 
-// Register bitonic sort of 32 floats, descending (per lane).
-__device__ __forceinline__ void sort32_desc(float (&x)[32]) {
+// Sorted (descending) register list: insert v (v = -inf inserts nothing).
+// new[i] = max(t[i], min(t[i-1], v)) -- independent per element.  The scan
+// fills the first MT - (jk + 1) slots with +inf, so t[MT - 1] is always the
+// (jk + 1)-th largest inserted value (no run-time index into the list).
+template <int MT>
+__device__ __forceinline__ void top_insert(float (&t)[MT], float v) {
 #pragma unroll
-    for (int kl = 1; kl <= 5; ++kl) {
-#pragma unroll
-        for (int jl = kl - 1; jl >= 0; --jl) {
-#pragma unroll
-            for (int i = 0; i < 32; ++i) {
-                const int p = i ^ (1 << jl);
-                if (p > i) {
-                    const bool desc = ((i >> kl) & 1) == 0;
-                    const float a = x[i], b = x[p];
-                    const float hi = fmaxf(a, b), lo = fminf(a, b);
-                    x[i] = desc ? hi : lo;
-                    x[p] = desc ? lo : hi;
-                }
-            }
-        }
-    }
+    for (int i = MT - 1; i >= 1; --i) t[i] = fmaxf(t[i], fminf(t[i - 1], v));
+    t[0] = fmaxf(t[0], v);
 }
 
-// Compact user q's list (both lanes of the user run this in lock step):
-// theta = k-th largest listed half-block max (a lower bound of the user's
-// k-th largest score: k distinct half-blocks each hold an item with
-// fp16 score >= theta), keep the entries >= cut = theta - 2 eps.  Lane h
-// sorts entries [32h, 32h + 32); the top 32 of the union is max(own[i],
-// partner[31 - i]) (one bitonic merge step), sorted again to read the k-th.
-// A user whose kept band does not leave room for the next tile's appends
-// (dense exact ties) stops appending and is redone by the exact fallback.
-template <int CL>
-__device__ __forceinline__ void user_flush(uint32_t ls, uint32_t li, int h, int& n, float& tau,
-                                           float& theta, bool& ovf, int k, float eps, int cap) {
-    const uint32_t as = ls + (uint32_t)h * (32u * 32u * 4u), ai = li + (uint32_t)h * (32u * 32u * 4u);
-    uint32_t raw[16];
-    float x[32];
-    const int nv = n - 32 * h;  // valid entries in this lane's half
-    lds_rd16<128>(as, raw);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = i < nv ? __uint_as_float(raw[i]) : -INFINITY;
-    lds_rd16<128>(as + 16 * 128, raw);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[16 + i] = 16 + i < nv ? __uint_as_float(raw[i]) : -INFINITY;
-    sort32_desc(x);
-    float z[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) z[i] = fmaxf(x[i], partner32f(x[31 - i], h));
-    // z is bitonic: merge it descending
-#pragma unroll
-    for (int jl = 4; jl >= 0; --jl) {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            const int p = i ^ (1 << jl);
-            if (p > i) {
-                const float a = z[i], b = z[p];
-                z[i] = fmaxf(a, b);
-                z[p] = fminf(a, b);
-            }
-        }
-    }
-    float th = z[0];
-#pragma unroll
-    for (int j = 1; j < 32; ++j) th = (j == k - 1) ? z[j] : th;
-    const float cut = (th == -INFINITY) ? -INFINITY : round_down_sub(th, 2.0f * eps);
-    // re-read (score, id) in list order and compact: lane 0's kept entries go
-    // to [0, c0), lane 1's to [c0, c0 + c1); a dropped entry is written to
-    // slot SC_CL - 1, which no kept entry reaches unless the user overflows.
-    uint32_t s[32], id[32];
-    lds_rd16<128>(as, raw);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s[i] = raw[i];
-    lds_rd16<128>(as + 16 * 128, raw);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s[16 + i] = raw[i];
-    lds_rd16<128>(ai, raw);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) id[i] = raw[i];
-    lds_rd16<128>(ai + 16 * 128, raw);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) id[16 + i] = raw[i];
-    uint32_t keepm = 0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i)
-        keepm |= (i < nv && __uint_as_float(s[i]) >= cut) ? (1u << i) : 0u;
-    const int c_own = __popc(keepm);
-    const int c_par = (int)partner32((uint32_t)c_own, h);
-    int pos = h ? c_par : 0;
-    const uint32_t ls0 = ls - (uint32_t)0, dump = (uint32_t)(CL - 1) * 128u;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        const bool kp = (keepm >> i) & 1u;
-        const uint32_t off = kp ? (uint32_t)pos * 128u : dump;
-        lds_wr(ls0 + off, s[i]);
-        lds_wr(li + off, id[i]);
-        pos += kp ? 1 : 0;
-    }
-    const int nn = c_own + c_par;
-    theta = th;
-    if (nn > cap) {
-        ovf = true;
-        tau = INFINITY;
-        n = 0;
-    } else {
-        n = nn;
-        tau = fmaxf(tau, cut);
-    }
-}
-
-// Screen: 8 waves (2 per SIMD) x 32 users per workgroup share one LDS ring of
-// catalog tiles.  Per tile every wave runs TB x DS MFMAs, takes each lane's
-// half-block max and, when any lane beats its user's cut, appends those
-// maxima to the user lists (branch per tile).  Lists are compacted when one
-// is nearly full; a flush requested by any wave is joined by the others at
-// the same tile (they all meet at the per-tile barrier anyway), through an
-// LDS hint word.
-template <int DP, int NW, int NSL = 3, int CL = SC_CL>
-__global__ __launch_bounds__(NW * 64, (NW == 4 && CL < 64) ? 2 : NW / 4) void ip_screen_kernel(
-    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog,
-    int n_items, int dim, int k, uint2* __restrict__ cand, int32_t* __restrict__ cand_cnt,
-    float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
-    int32_t* __restrict__ ovf_count) {
+// Per-user screen record (uinfo): theta_lb (scaled), eps (scaled), the
+// exact power-of-two scale scl = su * catalog scale, eps (unscaled).
+//
+// Scan: NW waves x UG x 32 users per workgroup share one NSL-slot LDS ring of
+// catalog tiles (8 KB, or one 16-KB block at dim 256).  Per tile every wave
+// reads the tile's A fragments once and runs TB x DS x UG MFMAs.
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false>
+__global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
+    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
+    int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
+    float4* __restrict__ uinfo) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
     constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : 8192 / BLOCK_BYTES;
     constexpr int TILE_BYTES = TB * BLOCK_BYTES;
-    constexpr int LPT = TILE_BYTES / (NW * 64 * 16);  // 1-KB LDS-DMA pieces per wave per tile
+    constexpr int LPT = TILE_BYTES / (NW * 1024);  // 1-KB LDS-DMA pieces per wave per tile
     static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
-    constexpr int NSLOT = NSL;
-    constexpr int WLIST = 2 * CL * 32 * 4;  // one wave's score + id planes
-    constexpr int CAP = CL - 2 * TB;        // list size that still takes one tile of appends
-    constexpr int LDS = NSLOT * TILE_BYTES + NW * WLIST + 16;
-    static_assert(LDS <= 163840, "LDS budget");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[LDS];
+    static_assert(!FULLREAD || (TB * DS) % 8 == 0, "fragment groups of 8");
+    static_assert(NSL >= 2, "ring");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NSL * TILE_BYTES];
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
-    const int user = blockIdx.x * (NW * 32) + wave * 32 + q;
-    const bool active = user < n_users;
+    const int ubase = blockIdx.x * (NW * 32 * UG) + wave * (32 * UG);
 
     const int nblk = (n_items + 31) >> 5;
     const int ntile = (nblk + TB - 1) / TB;
     const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk * BLOCK_BYTES);
-    const float vmax = hdr->max_norm;
-    const float sv_scale = hdr->scale;
+    const float vmax = hdr->max_norm, sv_scale = hdr->scale, dvmax = hdr->max_dnorm;
+    const int jk = (k + 1) / 2 - 1;  // list position whose pair-min bounds the k-th: 2 (jk + 1) >= k
 
-    // B operand: 32 users x DP dims, fp16 (scaled by a power of two); lane
-    // holds user q, dims 16s + 8h + [0, 8) for k-step s.
-    float uval[DS][8];
-    float nrm2 = 0.0f, uabs = 0.0f;
-    const float* urow = users + (size_t)(active ? user : 0) * dim;
+    // B operands: 32 users x DP dims per group, fp16 (scaled by a power of
+    // two); lane holds user q of the group, dims 16s + 8h + [0, 8).
+    f16x8 ufrag[UG][DS];
+    float eps_s[UG], eps_u[UG], scl[UG], tau[UG];
+    float t[UG][MT];
+    int cnt[UG];
+    bool live[UG];
 #pragma unroll
-    for (int s = 0; s < DS; ++s)
+    for (int g = 0; g < UG; ++g) {
+        const int user = ubase + g * 32 + q;
+        const bool active = user < n_users;
+        float uval[DS][8];
+        float nrm2 = 0.0f, uabs = 0.0f;
+        const float* urow = users + (size_t)(active ? user : 0) * dim;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int d = 16 * s + 8 * h + e;
-            const float f = (active && d < dim) ? urow[d] : 0.0f;
-            uval[s][e] = f;
-            nrm2 += f * f;
-            uabs = fmaxf(uabs, fabsf(f));
-        }
-    nrm2 += __shfl_xor(nrm2, 32, WAVE);
-    uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
-    const float su = pow2_scale(uabs);
-    f16x8 ufrag[DS];
-    float du2 = 0.0f;  // ||fp16(u su) - u su||^2 (scaled units; each difference exact)
+        for (int s = 0; s < DS; ++s)
 #pragma unroll
-    for (int s = 0; s < DS; ++s)
+            for (int e = 0; e < 8; ++e) {
+                const int d = 16 * s + 8 * h + e;
+                const float f = (active && d < dim) ? urow[d] : 0.0f;
+                uval[s][e] = f;
+                nrm2 += f * f;
+                uabs = fmaxf(uabs, fabsf(f));
+            }
+        nrm2 += __shfl_xor(nrm2, 32, WAVE);
+        uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
+        const float su = pow2_scale(uabs);
+        float du2 = 0.0f;  // ||fp16(u su) - u su||^2 (scaled units; each difference exact)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float a = uval[s][e] * su;
-            ufrag[s][e] = (_Float16)a;
-            const float d = (float)ufrag[s][e] - a;
-            du2 += d * d;
-        }
-    du2 += __shfl_xor(du2, 32, WAVE);
-    // |fp16 score - exact| = |du.v + u.dv + du.dv + accumulation| with du, dv
-    // the actual fp16 rounding errors of this user and of the items:
-    //   <= ||du|| max||v|| + ||u|| max||dv|| + ||du|| max||dv||
-    //      + (2^-15 + D 2^-23) ||u|| max||v||  (fp32 accumulation of the exact
-    //        fp16 products in any order, with the round-1 bound's margins);
-    // ||du|| is measured here, max||dv|| by catalog_dnorm_kernel -- about
-    // 0.65x of round 1's worst case 2^-10 ||u|| max||v||.
-    const float nu = sqrtf(nrm2), ndu = sqrtf(du2) / su, dvmax = hdr->max_dnorm;
-    const float ceps = 3.0517578e-5f + (float)DP * 1.1920929e-7f;
-    const float eps = (nrm2 == 0.0f) ? 0.0f
-                                     : (ndu * vmax + nu * dvmax + ndu * dvmax + ceps * nu * vmax) * 1.0001f + 1e-30f;
-    const float scl = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
-    const float eps_s = eps * scl;
+        for (int s = 0; s < DS; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float a = uval[s][e] * su;
+                ufrag[g][s][e] = (_Float16)a;
+                const float d = (float)ufrag[g][s][e] - a;
+                du2 += d * d;
+            }
+        du2 += __shfl_xor(du2, 32, WAVE);
+        // |fp16 score - exact| = |du.v + u.dv + du.dv + accumulation| with du, dv
+        // the actual fp16 rounding errors of this user and of the items:
+        //   <= ||du|| max||v|| + ||u|| max||dv|| + ||du|| max||dv||
+        //      + (2^-15 + D 2^-23) ||u|| max||v||  (fp32 accumulation of the exact
+        //        fp16 products in any order);
+        // ||du|| is measured here, max||dv|| by catalog_dnorm_kernel.
+        const float nu = sqrtf(nrm2), ndu = sqrtf(du2) / su;
+        const float ceps = 3.0517578e-5f + (float)DP * 1.1920929e-7f;
+        const float eps = (nrm2 == 0.0f) ? 0.0f
+                                         : (ndu * vmax + nu * dvmax + ndu * dvmax + ceps * nu * vmax) * 1.0001f + 1e-30f;
+        scl[g] = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
+        eps_s[g] = eps * scl[g];
+        eps_u[g] = eps;
+        // zero users (all scores exactly 0) are answered by the refine directly
+        live[g] = active && nrm2 > 0.0f;
+        tau[g] = live[g] ? -FLT_MAX : INFINITY;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) t[g][i] = (live[g] && i >= MT - 1 - jk) ? -INFINITY : INFINITY;
+        cnt[g] = 0;
+    }
+    uint2* dst[UG];
+#pragma unroll
+    for (int g = 0; g < UG; ++g) {
+        const int user = ubase + g * 32 + q;
+        dst[g] = app + ((size_t)(user < n_users ? user : 0) * 2 + h) * (size_t)m2;
+    }
 
-    // zero users (all scores exactly 0) are answered by the refine directly
-    const bool live = active && nrm2 > 0.0f;
-    int n = 0;
-    float tau = live ? -INFINITY : INFINITY, theta = -INFINITY;
-    bool ovf = false;
-
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
-    const uint32_t lst = lds_base + NSLOT * TILE_BYTES + wave * WLIST;
-    const uint32_t ls = lst + q * 4;                       // score plane, entry j at + j * 128
-    const uint32_t li = lst + CL * 32 * 4 + q * 4;      // id plane
-    const uint32_t hint = lds_base + NSLOT * TILE_BYTES + NW * WLIST;
-    if (tid == 0) lds_wr(hint, 0xFFFFFFFFu);
-
     const int body_bytes = nblk * BLOCK_BYTES;
     const int tail_blk = n_items >> 5;  // first block holding a row >= n_items
-    // Tile t -> ring slot t % NSLOT by LDS-DMA (global_load_lds_dwordx4: one
+    // Tile t -> ring slot t % NSL by LDS-DMA (global_load_lds_dwordx4: one
     // 1-KB piece per wave-instruction, no VGPR staging); tiles past the end
     // re-load the last piece (keeps the per-wave vmcnt accounting uniform,
     // the data is never used).
-    auto issue_tile = [&](int t) {
-        uint8_t* slot = smem + (t % NSLOT) * TILE_BYTES;
+    auto issue_tile = [&](int tt) {
+        uint8_t* slot = smem + (tt % NSL) * TILE_BYTES;
 #pragma unroll
         for (int p = 0; p < LPT; ++p) {
             const int piece = p * NW + wave;
-            int off = t * TILE_BYTES + piece * 1024;
+            int off = tt * TILE_BYTES + piece * 1024;
             off = off < body_bytes ? off : body_bytes - 1024;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(catalog + off + lane * 16),
@@ -436,27 +308,15 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && CL < 64) ? 2 : NW / 4) void ip
         }
     };
     const uint32_t lds0 = lds_base + lane * 16;
-    // all fragment reads (and the flush-hint word) and their wait in ONE asm
-    // statement: one LDS round trip per tile, and a separate wait statement
+    // all fragment reads and their wait in inline asm: hipcc's waitcnt pass
+    // would otherwise drain the in-flight LDS-DMA (the ring prefetch) in
+    // front of a compiler-visible LDS access, and a separate wait statement
     // would let the compiler copy an output before the data landed
-    static_assert((TB * DS) % 8 == 0, "fragment groups of 8");
-    auto read_frags = [&](int t, u32x4 (&afr)[TB * DS], uint32_t& hraw) {
-        const uint32_t base = lds0 + (uint32_t)((t % NSLOT) * TILE_BYTES);
-        u32x4* f = &afr[0];
-        asm volatile(
-            "ds_read_b32 %8, %10\n\t"
-            "ds_read_b128 %0, %9 offset:0\n\tds_read_b128 %1, %9 offset:1024\n\t"
-            "ds_read_b128 %2, %9 offset:2048\n\tds_read_b128 %3, %9 offset:3072\n\t"
-            "ds_read_b128 %4, %9 offset:4096\n\tds_read_b128 %5, %9 offset:5120\n\t"
-            "ds_read_b128 %6, %9 offset:6144\n\tds_read_b128 %7, %9 offset:7168\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]),
-              "=&v"(f[6]), "=&v"(f[7]), "=&v"(hraw)
-            : "v"(base), "v"(hint)
-            : "memory");
+    auto read_frags = [&](int tt, u32x4 (&afr)[TB * DS]) {
+        const uint32_t base = lds0 + (uint32_t)((tt % NSL) * TILE_BYTES);
 #pragma unroll
-        for (int g = 8; g < TB * DS; g += 8) {
-            f = &afr[g];
+        for (int g = 0; g < TB * DS; g += 8) {
+            u32x4* f = &afr[g];
             asm volatile(
                 "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:1024\n\t"
                 "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
@@ -469,94 +329,277 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && CL < 64) ? 2 : NW / 4) void ip
                 : "memory");
         }
     };
+    // one block's DS fragments (FULLREAD = false: fewer live registers,
+    // one LDS round trip per block)
+    auto read_block = [&](int tt, int b, u32x4 (&af)[DS]) {
+        const uint32_t base = lds0 + (uint32_t)((tt % NSL) * TILE_BYTES + b * DS * 1024);
+        if constexpr (DS == 1) {
+            asm volatile("ds_read_b128 %0, %1 offset:0\n\ts_waitcnt lgkmcnt(0)" : "=&v"(af[0]) : "v"(base) : "memory");
+        } else {
+#pragma unroll
+            for (int s2 = 0; s2 < DS; s2 += 2)
+                asm volatile("ds_read_b128 %0, %2 offset:0\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                             : "=&v"(af[s2]), "=&v"(af[s2 + 1])
+                             : "v"(base + 1024u * s2)
+                             : "memory");
+        }
+    };
     const int full_tiles = tail_blk / TB;  // tiles whose blocks are all full
-    auto tile = [&](int t, const u32x4 (&afr)[TB * DS], auto mask_c) {
+    float pend[UG];  // IE = 2: the lane's largest max since its group's last insert
+#pragma unroll
+    for (int g = 0; g < UG; ++g) pend[g] = -INFINITY;
+    auto tile = [&](int tt, const u32x4 (&afr)[FULLREAD ? TB * DS : 1], auto mask_c) {
         constexpr bool MASK = decltype(mask_c)::value;
-        float m[TB];
+        float mx[UG][TB];
 #pragma unroll
         for (int b = 0; b < TB; ++b) {
-            f32x16 acc = f32x16{};
+            u32x4 afb[DS];
+            if constexpr (FULLREAD) {
+#pragma unroll
+                for (int s = 0; s < DS; ++s) afb[s] = afr[b * DS + s];
+            } else {
+                read_block(tt, b, afb);
+            }
+            // the UG independent accumulation chains interleaved, so one
+            // group's reduction overlaps the other's MFMAs
+            f32x16 acc[UG];
+#pragma unroll
+            for (int g = 0; g < UG; ++g) acc[g] = f32x16{};
 #pragma unroll
             for (int s = 0; s < DS; ++s)
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afr[b * DS + s]),
-                                                             ufrag[s], acc, 0, 0, 0);
-            if constexpr (MASK) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = (t * TB + b) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (row >= n_items) acc[r] = -INFINITY;
+                for (int g = 0; g < UG; ++g)
+                    acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[s]), ufrag[g][s],
+                                                                    acc[g], 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < UG; ++g) {
+                if constexpr (MASK) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = (tt * TB + b) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (row >= n_items) acc[g][r] = -INFINITY;
+                    }
+                }
+                float v = fmaxf(fmaxf(acc[g][0], acc[g][1]), acc[g][2]);
+#pragma unroll
+                for (int r = 3; r < 15; r += 2) v = fmaxf(fmaxf(v, acc[g][r]), acc[g][r + 1]);
+                mx[g][b] = fmaxf(v, acc[g][15]);
+            }
+        }
+        // the lane's largest max of the tile, per user group
+        float vt[UG];
+#pragma unroll
+        for (int g = 0; g < UG; ++g) {
+            vt[g] = mx[g][0];
+#pragma unroll
+            for (int b = 1; b < TB; ++b) vt[g] = fmaxf(vt[g], mx[g][b]);
+        }
+        // appends: every half-block max >= tau reaches the user's HBM list
+        // (the count runs past the capacity -- the select then sends the user
+        // to the exact fallback -- and extra entries land on the last slots).
+        // TAPP: a lane whose tile max passes stores ALL TB maxima of its
+        // tile (one or two 16-B stores, one branch per group instead of one
+        // per block); the others are true half-block maxima below the tau of
+        // their tile, so the select's thresholds (>= theta_lb, >= cut, both
+        // above every tau) never take them.
+        bool any_app = false;
+        if constexpr (TAPP) {
+#pragma unroll
+            for (int g = 0; g < UG; ++g) any_app |= vt[g] >= tau[g];
+        } else {
+#pragma unroll
+            for (int g = 0; g < UG; ++g)
+#pragma unroll
+                for (int b = 0; b < TB; ++b) any_app |= mx[g][b] >= tau[g];
+        }
+        if (__builtin_amdgcn_ballot_w64(any_app)) {
+#pragma unroll
+            for (int g = 0; g < UG; ++g) {
+                if constexpr (TAPP) {
+                    if (vt[g] >= tau[g]) {
+                        uint2* pd = dst[g] + min(cnt[g], m2 - TB);
+                        const uint32_t id0 = (uint32_t)(tt * TB * 2 + h);
+                        if constexpr (TB == 1) {
+                            pd[0] = make_uint2(__float_as_uint(mx[g][0]), id0);
+                        } else {
+#pragma unroll
+                            for (int b = 0; b < TB; b += 2)
+                                *reinterpret_cast<uint4*>(pd + b) =
+                                    make_uint4(__float_as_uint(mx[g][b]), id0 + 2u * b, __float_as_uint(mx[g][b + 1]),
+                                               id0 + 2u * (b + 1));
+                        }
+                        cnt[g] += TB;
+                    }
+                } else {
+#pragma unroll
+                    for (int b = 0; b < TB; ++b) {
+                        const bool a = mx[g][b] >= tau[g];
+                        if (a)
+                            dst[g][min(cnt[g], m2 - 1)] =
+                                make_uint2(__float_as_uint(mx[g][b]), (uint32_t)((tt * TB + b) * 2 + h));
+                        cnt[g] += a ? 1 : 0;
+                    }
                 }
             }
-            float v = fmaxf(fmaxf(acc[0], acc[1]), acc[2]);
-#pragma unroll
-            for (int r = 3; r < 15; r += 2) v = fmaxf(fmaxf(v, acc[r]), acc[r + 1]);
-            m[b] = fmaxf(v, acc[15]);
         }
-        uint32_t cm = 0;
+        // threshold: the lane's largest max since the last insert enters its
+        // top list (a subset of the half-block maxima: the (jk + 1)-th largest
+        // stays a lower bound), then tau = (min over the user's two lanes) -
+        // 2 eps.  Every inserted value exceeded the lane's list minimum at
+        // its own tile, >= the tau it was tested against, so it was appended.
+        // IE = 2: group g inserts at tiles tt % 2 == g % 2 only.
 #pragma unroll
-        for (int b = 0; b < TB; ++b) cm |= m[b] > tau ? (1u << b) : 0u;
-        if (__builtin_amdgcn_ballot_w64(cm != 0)) {
-            // both lanes of a user append in one go, branch-free: lane 0's
-            // entries at n + [0, c0), lane 1's at n + c0 + [0, c1); a block
-            // not taken is written to slot CL - 1, which a kept entry reaches
-            // only when all 2 TB blocks of the user are taken (no dump then)
-            const uint32_t pm = partner32(cm, h);
-            const int c_own = __popc(cm), c_par = __popc(pm);
-            const uint32_t base = (uint32_t)(n + (h ? c_par : 0));
-            constexpr uint32_t dump = (uint32_t)(CL - 1) * 128u;
-#pragma unroll
-            for (int b = 0; b < TB; ++b) {
-                const uint32_t off = ((cm >> b) & 1u) ? (base + (uint32_t)__popc(cm & ((1u << b) - 1u))) * 128u
-                                                      : dump;
-                lds_wr_pair<CL * 32 * 4>(ls + off, __float_as_uint(m[b]), (uint32_t)((t * TB + b) * 2 + h));
+        for (int g = 0; g < UG; ++g) {
+            float v = vt[g];
+            if constexpr (IE == 2) {
+                pend[g] = fmaxf(pend[g], v);
+                if ((tt & 1) != (g & 1) && tt + 1 < ntile) continue;
+                v = pend[g];
+                pend[g] = -INFINITY;
             }
-            n += c_own + c_par;
+            const bool in = v > t[g][MT - 1];
+            if (__builtin_amdgcn_ballot_w64(in)) {
+                top_insert<MT>(t[g], in ? v : -INFINITY);
+                const float lb = fminf(t[g][MT - 1], partner32f(t[g][MT - 1], h));
+                const float c = lb - 2.0f * eps_s[g];
+                const uint32_t cb = __float_as_uint(c);
+                uint32_t rb = c > 0.0f ? cb - 1u : cb + 1u;  // one ulp toward -inf
+                rb = c == 0.0f ? 0x80000001u : rb;
+                float tv = lb == -INFINITY ? -FLT_MAX : __uint_as_float(rb);
+                tau[g] = live[g] ? tv : INFINITY;
+            }
         }
     };
 
 #pragma unroll
-    for (int p = 0; p < NSLOT - 1; ++p) issue_tile(p);
-    for (int t = 0; t < ntile; ++t) {
-        // own pieces of tile t landed (the next NSLOT-2 tiles' stay in
-        // flight), list appends done; the barrier publishes everyone's
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(LPT * (NSLOT - 2)) : "memory");
+    for (int p = 0; p < NSL - 1; ++p) issue_tile(p);
+    for (int tt = 0; tt < ntile; ++tt) {
+        // own pieces of tile tt landed (the next NSL-2 tiles' stay in
+        // flight; appends issued since only make the wait conservative); the
+        // barrier publishes everyone's pieces and retires slot (tt-1) % NSL
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * (NSL - 2)) : "memory");
         __builtin_amdgcn_s_barrier();
-        issue_tile(t + NSLOT - 1);
-        u32x4 afr[TB * DS];
-        uint32_t hraw;
-        read_frags(t, afr, hraw);
-        const int hv = (int)__builtin_amdgcn_readfirstlane((int)hraw);
-        if (t < full_tiles) tile(t, afr, std::false_type{});
-        else tile(t, afr, std::true_type{});
-        // flush when a list cannot take the next tile's appends, or with the
-        // other waves when one of them flushes at this tile (hint)
-        const bool need = __builtin_amdgcn_ballot_w64(n > CAP) != 0;
-        const bool soon = __builtin_amdgcn_ballot_w64(n > CAP - 2 * TB) != 0;
-        if (soon && lane == 0) lds_wr(hint, (uint32_t)(t + 1));
-        if (need || (hv == t && __builtin_amdgcn_ballot_w64(n > CL / 2) != 0))
-            user_flush<CL>(ls, li, h, n, tau, theta, ovf, k, eps_s, CAP);
+        issue_tile(tt + NSL - 1);
+        u32x4 afr[FULLREAD ? TB * DS : 1];
+        if constexpr (FULLREAD) read_frags(tt, afr);
+        if (tt < full_tiles) tile(tt, afr, std::false_type{});
+        else tile(tt, afr, std::true_type{});
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
-    user_flush<CL>(ls, li, h, n, tau, theta, ovf, k, eps_s, CAP);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
 
-    if (!active) return;
+#pragma unroll
+    for (int g = 0; g < UG; ++g) {
+        const float lb = fminf(t[g][MT - 1], partner32f(t[g][MT - 1], h));
+        const int user = ubase + g * 32 + q;
+        if (user < n_users) {
+            acnt[(size_t)user * 2 + h] = cnt[g];
+            if (h == 0) uinfo[user] = make_float4(live[g] ? lb : -INFINITY, eps_s[g], scl[g], eps_u[g]);
+        }
+    }
+}
+
+// ordered uint32 key of a float (monotone; -inf > 0, padding key 0 below all)
+__device__ __forceinline__ uint32_t fkey(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+    return __uint_as_float((k >> 31) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// Select: one wave per user.  theta = the exact k-th largest appended max:
+// the entries >= theta_lb (at least 2 (jk + 1) >= k of them: every value a
+// lane's final top list holds entered it at a position <= jk, above the tau
+// of that moment, so it was appended) are held one key per lane slot and
+// theta is built bit by bit (count of keys >= candidate by ballots).  The
+// band = every appended entry >= cut = theta - 2 eps (rounded down); an
+// item with exact score >= cut + eps has an fp16 score >= cut, so its
+// half-block max was >= every tau of the scan and was appended.
+__global__ __launch_bounds__(256) void ip_select_kernel(
+    int64_t n_users, int k, int m2, int bandcap, const uint2* __restrict__ app,
+    const int32_t* __restrict__ acnt, const float4* __restrict__ uinfo, uint2* __restrict__ cand,
+    int32_t* __restrict__ cand_cnt, float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag,
+    int32_t* __restrict__ ovf_list, int32_t* __restrict__ ovf_count) {
+    __shared__ uint32_t sel[4][IP_SEL];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t u = (int64_t)blockIdx.x * 4 + wave;
+    if (u >= n_users) return;
+    const int a0 = acnt[2 * u], a1 = acnt[2 * u + 1];
+    const float4 inf = uinfo[u];
+    bool ovf = a0 > m2 || a1 > m2;
+    const int n = ovf ? 0 : a0 + a1;
+    const uint2* s0 = app + (size_t)(2 * u) * m2;
+    const uint2* s1 = s0 + m2;
+    auto entry = [&](int e) -> uint2 { return e < a0 ? s0[e] : s1[e - a0]; };
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    // pass 1: keys of the entries >= theta_lb
+    int c = 0;
+    for (int b0 = 0; b0 < n; b0 += WAVE) {
+        const int e = b0 + lane;
+        const float v = e < n ? __uint_as_float(entry(e).x) : -INFINITY;
+        const bool kp = e < n && v >= inf.x;
+        const unsigned long long bal = __ballot(kp);
+        const int pos = c + __popcll(bal & lt);
+        if (kp && pos < IP_SEL) sel[wave][pos] = fkey(v);
+        c += __popcll(bal);
+    }
+    if (c > IP_SEL) ovf = true;
+    float theta = -INFINITY;
+    if (!ovf && c >= k) {
+        wave_sync_lds();
+        const int ec = (c + WAVE - 1) / WAVE;
+        uint32_t key[IP_SEL / WAVE];
+#pragma unroll
+        for (int e = 0; e < IP_SEL / WAVE; ++e) {
+            const int i = e * WAVE + lane;
+            key[e] = (e < ec && i < c) ? sel[wave][i] : 0u;
+        }
+        uint32_t x = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t cd = x | (1u << bit);
+            int cc = 0;
+#pragma unroll
+            for (int e = 0; e < IP_SEL / WAVE; ++e)
+                if (e < ec) cc += __popcll(__ballot(key[e] >= cd));
+            if (cc >= k) x = cd;
+        }
+        theta = fkey_inv(x);
+    }
     float cut = theta;
-    if (eps_s != 0.0f && theta != -INFINITY) cut = round_down_sub(theta, 2.0f * eps_s);
-    // lane 0 writes list entries [0, min(n, IP_CW)), lane 1 the rest
-    const int j0 = h ? IP_CW : 0, j1 = h ? n : (n < IP_CW ? n : IP_CW);
-    uint2* dst = cand + ((size_t)user * 2 + h) * IP_CW;
-    for (int j = j0; j < j1; ++j) {
-        const float sc = lds_rd(ls + (uint32_t)j * 128u);
-        const uint32_t id = __float_as_uint(lds_rd(li + (uint32_t)j * 128u));
-        dst[j - j0] = make_uint2(__float_as_uint(sc), id);
+    if (inf.y != 0.0f && theta != -INFINITY) cut = round_down_sub(theta, 2.0f * inf.y);
+    // pass 2: the band (append order)
+    int nb = 0;
+    uint2* bd = cand + (size_t)u * bandcap;
+    for (int b0 = 0; b0 < n; b0 += WAVE) {
+        const int e = b0 + lane;
+        uint2 ent = make_uint2(0u, 0u);
+        if (e < n) ent = entry(e);
+        const bool kp = e < n && __uint_as_float(ent.x) >= cut;
+        const unsigned long long bal = __ballot(kp);
+        const int pos = nb + __popcll(bal & lt);
+        if (kp && pos < bandcap) bd[pos] = ent;
+        nb += __popcll(bal);
     }
-    cand_cnt[user * 2 + h] = j1 > j0 ? j1 - j0 : 0;
-    if (h == 0) {
-        // unscaled cut and eps for the refinement (exact power-of-two rescale)
-        ucut[user] = make_float2(cut == -INFINITY ? -INFINITY : cut / scl, eps);
-        ovf_flag[user] = ovf ? 1 : 0;
-        if (ovf) ovf_list[atomicAdd(ovf_count, 1)] = user;
+    if (nb > bandcap) ovf = true;
+    if (lane == 0) {
+        cand_cnt[u] = ovf ? 0 : nb;
+        ucut[u] = make_float2(cut == -INFINITY ? -INFINITY : cut / inf.z, inf.w);
+        ovf_flag[u] = ovf ? 1 : 0;
+        if (ovf) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
     }
+}
+
+// k > IP_KFAST: every user takes the exact path
+__global__ void ip_all_exact_kernel(int64_t n_users, int32_t* __restrict__ cand_cnt,
+                                    int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
+                                    int32_t* __restrict__ ovf_count) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_users;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        cand_cnt[u] = 0;
+        ovf_flag[u] = 1;
+        ovf_list[u] = (int32_t)u;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ovf_count = (int32_t)n_users;
 }
 
 // ------------------------------------------------------------ refinement --
@@ -579,27 +622,26 @@ __device__ __forceinline__ double exact_dot(const float* __restrict__ a, const f
     return s + 0.0;
 }
 
-constexpr int IP_SURV = 128;  // exact survivors per user held by the refine
-constexpr int IP_KRING = 256; // prefilter-kept rows awaiting an exact round (ring, power of two)
-
 // DS4 = dim / 4 when the candidate rows are staged through LDS (dim 16, 32,
 // 64): every 64-item round loads the rows with whole-row coalesced float4
 // pieces (64 / DS4 rows per instruction) into a padded per-wave LDS stage,
 // then each lane sums its own row sequentially (the oracle's order).
-// DS4 = 0: the generic per-lane gather.
-template <int DS4>
+// DS4 = 0: the generic per-lane gather.  SV = exact survivors held per user
+// (SV / 64 per lane in the final sort).
+template <int DS4, int SV>
 __global__ __launch_bounds__(256) void ip_refine_kernel(
     const float* __restrict__ users, int64_t n_users, const float* __restrict__ items,
     const uint8_t* __restrict__ catalog, int64_t n_items, int dim, int k, int64_t row_offset,
-    const uint2* __restrict__ cand,
-    const int32_t* __restrict__ cand_cnt, const float2* __restrict__ ucut,
-    const int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
+    const uint2* __restrict__ cand, int bandcap, const int32_t* __restrict__ cand_cnt,
+    const float2* __restrict__ ucut, const int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
     int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
     double* __restrict__ out_e) {
-    __shared__ Cand surv[4][IP_SURV];
+    constexpr int SE = SV / WAVE;
+    __shared__ Cand surv[4][SV];
     __shared__ int32_t krow[DS4 > 0 ? 4 : 1][DS4 > 0 ? IP_KRING : 1];
     constexpr int RS = DS4 + 1;  // staged row stride in float4 (one float4 of padding)
     __shared__ float4 stage[DS4 > 0 ? 4 : 1][DS4 > 0 ? 64 * RS : 1];
+    __shared__ uint32_t bandq[4][SV + 32];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users || ovf_flag[u]) return;
@@ -609,30 +651,31 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
     for (int d = lane; d < dim; d += WAVE) nz += fabsf(uv[d]);
     nz = wave_sum_f32(nz);
     if (nz == 0.0f) {
-        if (lane < k) {
-            const bool ok = lane < n_items;
-            out_s[u * k + lane] = ok ? 0.0f : -FLT_MAX;
-            out_r[u * k + lane] = ok ? (int32_t)(lane + row_offset) : -1;
-            if (out_e) out_e[u * k + lane] = ok ? 0.0 : -INFINITY;
+        for (int i = lane; i < k; i += WAVE) {
+            const bool ok = i < n_items;
+            out_s[u * k + i] = ok ? 0.0f : -FLT_MAX;
+            out_r[u * k + i] = ok ? (int32_t)(i + row_offset) : -1;
+            if (out_e) out_e[u * k + i] = ok ? 0.0 : -INFINITY;
         }
         return;
     }
-    const int n0 = cand_cnt[2 * u], n1 = cand_cnt[2 * u + 1];
+    const int nbd = cand_cnt[u];
+    const uint2* bd = cand + (size_t)u * bandcap;
     const float2 ce = ucut[u];
     double thr = -INFINITY;
     if (ce.x != -INFINITY) {
         thr = (double)ce.x + (double)ce.y;
         thr = thr - fabs(thr) * 1e-15 - 1e-300;  // round down
     }
-    // The screen's cut in its scaled fp16 units (exact power-of-two rescale):
+    // The cut in the screen's scaled fp16 units (exact power-of-two rescale):
     // |fp16 score - exact| <= eps, so every item with exact >= cut + eps has
     // an fp16 score >= cut.  Used twice: (a) band entries (half-blocks) whose
-    // listed fp16 max is below it are dropped -- none on one GPU (the final
-    // flush kept only entries >= cut), most of the band on a catalog shard
-    // after nrk_ip_topk_apply_bound raised the cut to the global bound; (b)
-    // the fp16 prefilter (DS4 > 0): every band item's fp16 score recomputed
-    // from its 64-B packed row, only items reaching the cut are fetched in
-    // fp32 for the exact score.
+    // listed fp16 max is below it are dropped -- none on one GPU (the select
+    // kept only entries >= cut), most of the band on a catalog shard after
+    // nrk_ip_topk_apply_bound raised the cut to the global bound; (b) the
+    // fp16 prefilter (DS4 > 0): every band item's fp16 score recomputed from
+    // its 64-B packed row, only items reaching the cut are fetched in fp32
+    // for the exact score.
     constexpr int DSK = DS4 / 4;  // 16-dim k-steps of the packed layout
     const bool pre = catalog != nullptr && ce.x != -INFINITY;
     float ush[DS4 > 0 ? 4 * DS4 : 1];
@@ -650,28 +693,24 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         }
         pcut = ce.x * (su * hdr->scale);
     }
-    // (a) compact the band of both halves into LDS (list order kept)
-    __shared__ uint32_t bandq[4][2 * IP_CW];
+    // (a) compact the band into LDS (list order kept)
     int nband = 0;
-    for (int b0 = 0; b0 < n0 + n1; b0 += WAVE) {
+    for (int b0 = 0; b0 < nbd; b0 += WAVE) {
         const int e = b0 + lane;
         uint2 ent = make_uint2(0u, 0u);
-        if (e < n0 + n1)
-            ent = e < n0 ? cand[(size_t)(2 * u) * IP_CW + e] : cand[(size_t)(2 * u + 1) * IP_CW + (e - n0)];
-        const bool kp = e < n0 + n1 && (!pre || __uint_as_float(ent.x) >= pcut);
+        if (e < nbd) ent = bd[e];
+        const bool kp = e < nbd && (!pre || __uint_as_float(ent.x) >= pcut);
         const unsigned long long bal = __ballot(kp);
         if (kp) bandq[wave][nband + __popcll(bal & ((1ull << lane) - 1ull))] = ent.y;
         nband += __popcll(bal);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync_lds();
     const int nitem = nband * 16;
     int cnt = 0;
     auto push = [&](bool keep, double s, int32_t row) {
         const unsigned long long bal = __ballot(keep);
         const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
-        if (keep && pos < IP_SURV) surv[wave][pos] = Cand{s, row};
+        if (keep && pos < SV) surv[wave][pos] = Cand{s, row};
         cnt += __popcll(bal);
     };
     if constexpr (DS4 > 0) {
@@ -681,9 +720,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         // ring.  (B) whenever the ring holds 64 rows (and once at the end),
         // one exact round: the rows staged through LDS with whole-row
         // coalesced float4 pieces, each lane summing its own row sequentially
-        // (the oracle's order).  Most band items fail the prefilter, so the
-        // exact rounds (the expensive part) run on full 64-row chunks instead
-        // of once per prefilter round.
+        // (the oracle's order).
         uint4 pc[DSK > 0 ? 2 * DSK : 1];
         auto band_q = [&](int base) -> uint32_t {
             int idx = base + lane;
@@ -724,9 +761,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
                 const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
                 stage[wave][item * RS + part] = okv[it] ? v[it] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_sync_lds();
             double sd = 0.0;
             bool keep = false;
             if (rl >= 0) {
@@ -783,9 +818,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
             const unsigned long long bal = __ballot(keep);
             if (keep) krow[wave][(kc + __popcll(bal & ((1ull << lane) - 1ull))) & (IP_KRING - 1)] = row_cur;
             kc += __popcll(bal);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_sync_lds();
             // (B) exact rounds on full 64-row chunks
             while (kc - ko >= WAVE) exact_round(WAVE);
         }
@@ -798,8 +831,8 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
             int32_t row = 0;
             if (idx < nitem) {
                 const int bb = idx >> 4, r = idx & 15;
-                const uint32_t q = bandq[wave][bb];
-                const int64_t rr = (int64_t)(q >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (q & 1);
+                const uint32_t qv = bandq[wave][bb];
+                const int64_t rr = (int64_t)(qv >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (qv & 1);
                 if (rr < n_items) row = (int32_t)rr;
                 keep = rr < n_items;
                 if (keep) {
@@ -810,23 +843,21 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
             push(keep, sd, row);
         }
     }
-    if (cnt > IP_SURV) {  // dense exact ties: hand the user to the exact fallback
+    if (cnt > SV) {  // dense exact ties: hand the user to the exact fallback
         if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
         return;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    Cand x[2];
+    wave_sync_lds();
+    Cand x[SE];
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < SE; ++e) {
         const int idx = e * 64 + lane;
         if (idx < cnt) x[e] = surv[wave][idx];
         else { x[e].s = -INFINITY; x[e].row = INT32_MAX; }
     }
-    wave_bitonic_sort<2>(x);
+    wave_bitonic_sort<SE>(x);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < SE; ++e) {
         const int idx = e * 64 + lane;
         if (idx < k) {
             const bool ok = x[e].row != INT32_MAX;
@@ -843,13 +874,18 @@ __device__ __forceinline__ uint64_t okey(double s) {
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 
+// One workgroup per listed user: the k-th largest exact key by an 8-bit
+// radix select over the whole catalog (8 histogram passes), then the items
+// above it plus the first ties in row order (k winners in all), ordered by
+// an LDS bitonic sort of ns = next_pow2(max(k, 64)) entries (dynamic LDS).
 __global__ __launch_bounds__(256) void ip_fallback_kernel(
     const float* __restrict__ users, const float* __restrict__ items, int64_t n_items, int dim,
-    int k, int64_t row_offset, const int32_t* __restrict__ ovf_list,
+    int k, int ns, int64_t row_offset, const int32_t* __restrict__ ovf_list,
     const int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
     double* __restrict__ out_e) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    Cand* sel = reinterpret_cast<Cand*>(dyn);
     __shared__ unsigned int hist[256];
-    __shared__ Cand sel[64];
     __shared__ int sel_n;
     __shared__ unsigned long long s_prefix;
     __shared__ int s_krem;
@@ -857,8 +893,8 @@ __global__ __launch_bounds__(256) void ip_fallback_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int cnt = *ovf_count;
     const int kk = (int)(n_items < k ? n_items : k);
-    for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
-        const int64_t u = ovf_list[q];
+    for (int qi = blockIdx.x; qi < cnt; qi += gridDim.x) {
+        const int64_t u = ovf_list[qi];
         const float* uv = users + u * dim;
         unsigned long long prefix = 0, mask = 0;
         int krem = kk;
@@ -916,101 +952,128 @@ __global__ __launch_bounds__(256) void ip_fallback_kernel(
             __syncthreads();
         }
         __syncthreads();
-        if (wave == 0) {
-            Cand x[1];
-            if (lane < sel_n) x[0] = sel[lane];
-            else { x[0].s = -INFINITY; x[0].row = INT32_MAX; }
-            wave_bitonic_sort<1>(x);
-            if (lane < k) {
-                const bool ok = lane < kk;
-                out_s[u * k + lane] = ok ? (float)x[0].s : -FLT_MAX;
-                out_r[u * k + lane] = ok ? (int32_t)(x[0].row + row_offset) : -1;
-                if (out_e) out_e[u * k + lane] = ok ? x[0].s : -INFINITY;
+        const int nsel = sel_n;
+        for (int i = nsel + tid; i < ns; i += 256) sel[i] = Cand{-INFINITY, INT32_MAX};
+        __syncthreads();
+        // bitonic sort of sel[0, ns), best first
+        for (int sz = 2; sz <= ns; sz <<= 1) {
+            for (int st = sz >> 1; st > 0; st >>= 1) {
+                for (int i = tid; i < ns / 2; i += 256) {
+                    const int lo = 2 * st * (i / st) + (i % st), hi = lo + st;
+                    const bool up = (lo & sz) == 0;
+                    const Cand a = sel[lo], b = sel[hi];
+                    if (up ? better(b, a) : better(a, b)) {
+                        sel[lo] = b;
+                        sel[hi] = a;
+                    }
+                }
+                __syncthreads();
             }
+        }
+        for (int i = tid; i < k; i += 256) {
+            const bool ok = i < kk;
+            out_s[u * k + i] = ok ? (float)sel[i].s : -FLT_MAX;
+            out_r[u * k + i] = ok ? (int32_t)(sel[i].row + row_offset) : -1;
+            if (out_e) out_e[u * k + i] = ok ? sel[i].s : -INFINITY;
         }
         __syncthreads();
     }
 }
 
 // ----------------------------------------------------------------- merge --
+// One wave per user.  E = 1, 2, 4: the n_lists * k_in entries in registers
+// (E per lane); E = 0: in the wave's dynamic-LDS region of NS entries.
 template <int E>
 __global__ __launch_bounds__(256) void topk_merge_kernel(
     const double* __restrict__ in_e, const int32_t* __restrict__ in_r, int n_lists,
-    int64_t stride, int64_t n_users, int k_in, int k_out, float* __restrict__ out_s,
+    int64_t stride, int64_t n_users, int k_in, int k_out, int ns, float* __restrict__ out_s,
     int32_t* __restrict__ out_r, double* __restrict__ out_e) {
-    const int lane = threadIdx.x & 63;
-    const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users) return;
-    Cand x[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int idx = e * 64 + lane;
+    auto load = [&](int idx) -> Cand {
+        Cand c{-INFINITY, INT32_MAX};
         const int l = idx / k_in, j = idx - l * k_in;
-        x[e].s = -INFINITY;
-        x[e].row = INT32_MAX;
         if (l < n_lists) {
             const int64_t o = l * stride + u * k_in + j;
             const int32_t r = in_r[o];
-            if (r >= 0) {
-                x[e].s = in_e[o];
-                x[e].row = r;
-            }
+            if (r >= 0) c = Cand{in_e[o], r};
         }
-    }
-    wave_bitonic_sort<E>(x);
+        return c;
+    };
+    auto store = [&](int idx, const Cand& c) {
+        const bool ok = c.row != INT32_MAX;
+        out_s[u * k_out + idx] = ok ? (float)c.s : -FLT_MAX;
+        out_r[u * k_out + idx] = ok ? c.row : -1;
+        if (out_e) out_e[u * k_out + idx] = ok ? c.s : -INFINITY;
+    };
+    if constexpr (E > 0) {
+        Cand x[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int idx = e * 64 + lane;
-        if (idx < k_out) {
-            const bool ok = x[e].row != INT32_MAX;
-            out_s[u * k_out + idx] = ok ? (float)x[e].s : -FLT_MAX;
-            out_r[u * k_out + idx] = ok ? x[e].row : -1;
-            if (out_e) out_e[u * k_out + idx] = ok ? x[e].s : -INFINITY;
-        }
+        for (int e = 0; e < E; ++e) x[e] = load(e * 64 + lane);
+        wave_bitonic_sort<E>(x);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (e * 64 + lane < k_out) store(e * 64 + lane, x[e]);
+    } else {
+        Cand* x = reinterpret_cast<Cand*>(dyn) + (size_t)wave * ns;
+        for (int i = lane; i < ns; i += WAVE) x[i] = load(i);
+        wave_lds_sort(x, ns);
+        for (int i = lane; i < k_out; i += WAVE) store(i, x[i]);
     }
 }
 
 // ------------------------------------------------- catalog-shard bound --
-constexpr int IP_BOUND_MMAX = 32;
-
-// Per user, the m largest listed half-block maxima of this shard's band as
-// exact lower bounds: a half-block whose fp16 max is x (scaled units, scl =
-// su * catalog scale) holds an item with exact score >= x / scl - eps.
-// Distinct half-blocks are distinct items, so any k of these values bound k
-// distinct items from below.  Descending, -inf padded (fp32, rounded down).
-template <int MM>
-__global__ void ip_bound_kernel(const float* __restrict__ users, int64_t n_users, int dim,
-                                const CatalogHdr* __restrict__ hdr, const uint2* __restrict__ cand,
-                                const int32_t* __restrict__ cand_cnt, const float2* __restrict__ ucut,
-                                int m, float* __restrict__ out) {
-    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Per user, the m largest band maxima of this shard as exact lower bounds: a
+// half-block whose fp16 max is x (scaled units, scl = su * catalog scale)
+// holds an item with exact score >= x / scl - eps.  Distinct half-blocks are
+// distinct items, so any k of these values bound k distinct items from
+// below.  Descending, -inf padded (fp32, rounded down).  One wave per user;
+// E = 1, 2, 4: the band in registers, E = 0: in dynamic LDS (ns per wave).
+template <int E>
+__global__ __launch_bounds__(256) void ip_bound_kernel(const float* __restrict__ users, int64_t n_users, int dim,
+                                                       const CatalogHdr* __restrict__ hdr,
+                                                       const uint2* __restrict__ cand, int bandcap,
+                                                       const int32_t* __restrict__ cand_cnt,
+                                                       const float2* __restrict__ ucut, int m, int ns,
+                                                       float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users) return;
-    float best[MM];
+    const int nb = cand_cnt[u];
+    const float* uv = users + u * dim;
+    float ua = 0.0f;
+    for (int d = lane; d < dim; d += WAVE) ua = fmaxf(ua, fabsf(uv[d]));
 #pragma unroll
-    for (int j = 0; j < MM; ++j) best[j] = -INFINITY;
-    const int n0 = cand_cnt[2 * u], n1 = cand_cnt[2 * u + 1];
-    if (n0 + n1 > 0) {
-        const float* uv = users + u * dim;
-        float ua = 0.0f;
-        for (int d = 0; d < dim; ++d) ua = fmaxf(ua, fabsf(uv[d]));
-        const double inv = 1.0 / ((double)pow2_scale(ua) * (double)hdr->scale);  // exact power of two
-        const double eps = (double)ucut[u].y;
-        for (int e = 0; e < n0 + n1; ++e) {
-            const uint2 c = e < n0 ? cand[(size_t)(2 * u) * IP_CW + e] : cand[(size_t)(2 * u + 1) * IP_CW + (e - n0)];
-            const double t = (double)__uint_as_float(c.x) * inv - eps;
-            float v = (float)t;
-            if ((double)v > t) v = nextafterf(v, -INFINITY);
-            // insertion into the descending top-m
-#pragma unroll
-            for (int j = 0; j < MM; ++j) {
-                const bool in = j < m && v > best[j];
-                const float o = best[j];
-                best[j] = in ? v : o;
-                v = in ? o : v;
-            }
+    for (int o = 32; o > 0; o >>= 1) ua = fmaxf(ua, __shfl_xor(ua, o, WAVE));
+    const double inv = 1.0 / ((double)pow2_scale(ua) * (double)hdr->scale);  // exact power of two
+    const double eps = (double)ucut[u].y;
+    auto load = [&](int i) -> Cand {
+        Cand c{-INFINITY, INT32_MAX};
+        if (i < nb) {
+            const double tv = (double)__uint_as_float(cand[(size_t)u * bandcap + i].x) * inv - eps;
+            float v = (float)tv;
+            if ((double)v > tv) v = nextafterf(v, -INFINITY);
+            c = Cand{(double)v, i};
         }
+        return c;
+    };
+    if constexpr (E > 0) {
+        Cand x[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[e] = load(e * 64 + lane);
+        wave_bitonic_sort<E>(x);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (e * 64 + lane < m) out[u * m + e * 64 + lane] = (float)x[e].s;
+    } else {
+        Cand* x = reinterpret_cast<Cand*>(dyn) + (size_t)wave * ns;
+        for (int i = lane; i < ns; i += WAVE) x[i] = load(i);
+        wave_lds_sort(x, ns);
+        for (int i = lane; i < m; i += WAVE) out[u * m + i] = (float)x[i].s;
     }
-    for (int j = 0; j < m; ++j) out[u * m + j] = best[j];
 }
 
 // G = the k-th largest of the n_lists * m bounds of the user (lists laid out
@@ -1018,27 +1081,43 @@ __global__ void ip_bound_kernel(const float* __restrict__ users, int64_t n_users
 // lower bound of the user's k-th exact score over the whole catalog.  Raise
 // the shard's cut to G - eps (rounded down to fp32): the refine then keeps
 // exact >= cut + eps <= G, and the band / prefilter tests use the raised cut.
-// One wave per user: one value per lane, wave bitonic sort (n_lists * m <= 64).
+// One wave per user (values in registers for E = 1, 2, 4, in LDS for E = 0).
+template <int E>
 __global__ __launch_bounds__(256) void ip_apply_bound_kernel(float2* __restrict__ ucut, int64_t n_users,
                                                              const float* __restrict__ vals, int n_lists,
-                                                             int m, int k) {
-    const int lane = threadIdx.x & 63;
-    const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                             int m, int k, int ns) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users) return;
-    Cand x[1];
-    x[0].row = lane;
-    x[0].s = -(double)INFINITY;
-    if (lane < n_lists * m) {
-        const int l = lane / m, j = lane - l * m;
-        x[0].s = (double)vals[((int64_t)l * n_users + u) * m + j];
+    auto load = [&](int i) -> Cand {
+        Cand c{-(double)INFINITY, i};
+        if (i < n_lists * m) {
+            const int l = i / m, j = i - l * m;
+            c.s = (double)vals[((int64_t)l * n_users + u) * m + j];
+        }
+        return c;
+    };
+    double G = -(double)INFINITY;
+    if constexpr (E > 0) {
+        Cand x[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[e] = load(e * 64 + lane);
+        wave_bitonic_sort<E>(x);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if ((k - 1) / 64 == e) G = __shfl(x[e].s, (k - 1) % 64, WAVE);
+    } else {
+        Cand* x = reinterpret_cast<Cand*>(dyn) + (size_t)wave * ns;
+        for (int i = lane; i < ns; i += WAVE) x[i] = load(i);
+        wave_lds_sort(x, ns);
+        G = x[k - 1].s;
     }
-    wave_bitonic_sort<1>(x);
-    const double G = __shfl(x[0].s, k - 1, WAVE);
     if (lane != 0 || !(G > -(double)INFINITY)) return;
     float2 c = ucut[u];
-    const double t = G - (double)c.y;
-    float f = (float)t;
-    if ((double)f > t) f = nextafterf(f, -INFINITY);
+    const double tt = G - (double)c.y;
+    float f = (float)tt;
+    if ((double)f > tt) f = nextafterf(f, -INFINITY);
     if (f > c.x) {
         c.x = f;
         ucut[u] = c;
@@ -1046,36 +1125,129 @@ __global__ __launch_bounds__(256) void ip_apply_bound_kernel(float2* __restrict_
 }
 
 // ------------------------------------------------------------- workspace --
+// [hdr 256 B: ovf_count] [ucut f2] [cand_cnt] [ovf_flag] [ovf_list] [uinfo f4]
+// [acnt 2 per user] [cand: bandcap per user] [app: 2 x m2 per user]
+// ucut .. acnt depend on n_users only (nrk_ip_topk_apply_bound has no k).
 struct IpWs {
-    uint2* cand;
+    int32_t* ovf_count;
     float2* ucut;
     int32_t* cnt;
     int32_t* ovf_flag;
     int32_t* ovf_list;
-    int32_t* ovf_count;
+    float4* uinfo;
+    int32_t* acnt;
+    uint2* cand;
+    uint2* app;
+    int bandcap, m2;
     size_t bytes;
 };
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static IpWs ip_ws_layout(void* base, int64_t n_users) {
+// band entries kept per user (k + the entries within 2 eps of theta)
+static inline int ip_bandcap(int k) {
+    const int b = ((2 * k + 32 + 31) / 32) * 32;
+    return std::min(IP_BQ, std::max(96, b));
+}
+// appended maxima per (user, half): about twice the expected record count
+// of a lane's top-(jk+1) over its nblk half-blocks (random catalog order),
+// never more than nblk (a lane appends at most one entry per block)
+// (per half-block appends); the tile-append scan (k <= 32) stores whole
+// tiles of TB maxima per passing tile, so there it is TB x the tile count
+static inline int ip_m2(int64_t n_items, int k, int dim) {
+    if (k > IP_KFAST) return 0;
+    const int64_t nblk = std::max<int64_t>(1, n_blocks_of(n_items));
+    const double mt = (double)((k + 1) / 2);
+    const double est = mt * (1.0 + log(std::max(1.0, (double)nblk / mt)));
+    int64_t m2 = (((int64_t)(2.0 * est) + 64 + 63) / 64) * 64;
+    m2 = std::min<int64_t>(m2, ((nblk + 63) / 64) * 64);
+    if (mt <= 16) {
+        const int dp = pad_dim(dim);
+        const int64_t tb = 64 * dp >= 8192 ? 1 : 8192 / (64 * dp);
+        const int64_t ntile = (nblk + tb - 1) / tb;
+        const double et = mt * (1.0 + log(std::max(1.0, (double)ntile / mt)));
+        int64_t mt2 = ((tb * ((int64_t)(2.0 * et) + 16) + 63) / 64) * 64;
+        mt2 = std::min<int64_t>(mt2, ((ntile * tb + 63) / 64) * 64);
+        m2 = std::max(m2, mt2);
+    }
+    return (int)m2;
+}
+
+static IpWs ip_ws_layout(void* base, int64_t n_users, int64_t n_items, int k, int dim) {
     IpWs w;
+    w.bandcap = ip_bandcap(k);
+    w.m2 = ip_m2(n_items, k, dim);
     uint8_t* p = reinterpret_cast<uint8_t*>(base);
     size_t off = 0;
     w.ovf_count = reinterpret_cast<int32_t*>(p + off);
     off += 256;
-    w.cand = reinterpret_cast<uint2*>(p + off);
-    off += align256((size_t)n_users * 2 * IP_CW * sizeof(uint2));
     w.ucut = reinterpret_cast<float2*>(p + off);
     off += align256((size_t)n_users * sizeof(float2));
     w.cnt = reinterpret_cast<int32_t*>(p + off);
-    off += align256((size_t)n_users * 2 * sizeof(int32_t));
+    off += align256((size_t)n_users * sizeof(int32_t));
     w.ovf_flag = reinterpret_cast<int32_t*>(p + off);
     off += align256((size_t)n_users * sizeof(int32_t));
     w.ovf_list = reinterpret_cast<int32_t*>(p + off);
     off += align256((size_t)n_users * sizeof(int32_t));
+    w.uinfo = reinterpret_cast<float4*>(p + off);
+    off += align256((size_t)n_users * sizeof(float4));
+    w.acnt = reinterpret_cast<int32_t*>(p + off);
+    off += align256((size_t)n_users * 2 * sizeof(int32_t));
+    w.cand = reinterpret_cast<uint2*>(p + off);
+    off += align256((size_t)n_users * w.bandcap * sizeof(uint2));
+    w.app = reinterpret_cast<uint2*>(p + off);
+    off += align256((size_t)n_users * 2 * (size_t)w.m2 * sizeof(uint2));
     w.bytes = off;
     return w;
+}
+
+static inline int next_pow2(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// scan variants: (DP, waves per workgroup, ring slots, user groups per wave,
+// register list length, waves per SIMD)
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false>
+static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
+                          const IpWs& w, hipStream_t s) {
+    const int per_wg = NW * 32 * UG;
+    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<(n_users + per_wg - 1) / per_wg, NW * 64, 0, s>>>(
+        users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo);
+}
+
+template <int DP, int MT>
+static void launch_scan(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
+                        const IpWs& w, hipStream_t s) {
+    constexpr int UG = (DP <= 128 && MT <= 32) ? 2 : 1;
+    constexpr int WPE = (DP >= 128 || MT >= 32) ? 2 : 4;
+    if constexpr (DP == 32 && MT == 16) {
+        // dev A/B switch (tools/screen_time.py): NRK_SCAN_VARIANT
+        static const int var = [] { const char* e = getenv("NRK_SCAN_VARIANT"); return e ? atoi(e) : 0; }();
+        switch (var) {
+            case 1: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 2: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 3: launch_scan_v<DP, 8, 3, 2, MT, 4, false>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 4: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 5: launch_scan_v<DP, 8, 3, 2, MT, 4, true, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            default: break;
+        }
+    }
+    // 8 waves (two per SIMD) share a 3-slot ring; 2 workgroups per CU.  k <= 32
+    // appends whole tiles (TAPP).  Config 2: 7.5 ms against 7.9 for 4-wave
+    // workgroups with a 4-slot ring (tools/scan_ab.sh)
+    constexpr int NW = (UG == 2) ? 8 : 4, NSL = (UG == 2) ? 3 : 4;
+    launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 1, MT == 16>(users, n_users, cat, n_items, dim, k, w, s);
+}
+
+template <int DP>
+static void launch_scan_k(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
+                          const IpWs& w, hipStream_t s) {
+    const int mt = (k + 1) / 2;
+    if (mt <= 16) launch_scan<DP, 16>(users, n_users, cat, n_items, dim, k, w, s);
+    else if (mt <= 32) launch_scan<DP, 32>(users, n_users, cat, n_items, dim, k, w, s);
+    else launch_scan<DP, 64>(users, n_users, cat, n_items, dim, k, w, s);
 }
 
 }  // namespace nrk
@@ -1122,11 +1294,9 @@ int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* cat
 }
 
 size_t nrk_ip_topk_workspace_bytes(int64_t n_users, int64_t n_items, int dim, int k) {
-    (void)n_items;
     (void)dim;
-    (void)k;
-    if (n_users < 0) return 0;
-    return ip_ws_layout(nullptr, n_users).bytes;
+    if (n_users < 0 || n_items < 0 || k < 1) return 0;
+    return ip_ws_layout(nullptr, n_users, n_items, k, dim).bytes;
 }
 
 static int ip_check(const float* users, int64_t n_users, const float* items, const void* catalog,
@@ -1135,11 +1305,11 @@ static int ip_check(const float* users, int64_t n_users, const float* items, con
     NRK_REQUIRE(n_items < (1ll << 30) && n_users < (1ll << 30), "n_items / n_users must be < 2^30");
     NRK_REQUIRE(dim > 0 && dim <= 256, "dim must be in [1, 256]");
     NRK_REQUIRE(k >= 1, "k must be >= 1");
-    if (k > IP_KMAX) NRK_UNSUPPORTED("k > 32 is not compiled");
+    if (k > IP_KMAX) NRK_UNSUPPORTED("k > 2048 is not compiled");
     if (n_users == 0) return NRK_OK;
     NRK_REQUIRE(users && workspace, "null pointer");
     NRK_REQUIRE(n_items == 0 || (items && catalog), "items/catalog null");
-    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users).bytes, "workspace too small");
+    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users, n_items, k, dim).bytes, "workspace too small");
     return NRK_OK;
 }
 
@@ -1150,7 +1320,7 @@ int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog,
     int rc = ip_check(users, n_users, (const float*)catalog, catalog, n_items, dim, k, workspace,
                       workspace_bytes);
     if (rc != NRK_OK || n_users == 0) return rc;
-    const IpWs w = ip_ws_layout(workspace, n_users);
+    const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
     hipStream_t s = as_stream(stream);
     if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
         set_error("nrk_ip_topk_screen: hipMemsetAsync failed");
@@ -1160,38 +1330,26 @@ int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog,
     const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
     if (n_items == 0) {
         // nothing to search: every output row is padding
-        (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * 2 * sizeof(int32_t), s);
+        (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * sizeof(int32_t), s);
         (void)hipMemsetAsync(w.ovf_flag, 0, (size_t)n_users * sizeof(int32_t), s);
+        (void)hipMemsetAsync(w.ucut, 0xFF, (size_t)n_users * sizeof(float2), s);  // NaN cut: no band
+    } else if (k > IP_KFAST) {
+        const int grid = (int)std::min<int64_t>((n_users + 255) / 256, 4096);
+        ip_all_exact_kernel<<<grid, 256, 0, s>>>(n_users, w.cnt, w.ovf_flag, w.ovf_list, w.ovf_count);
     } else {
-#define NRK_SCREEN(DPV, NWV)                                                               \
-    ip_screen_kernel<DPV, NWV><<<(int)((n_users + 32 * NWV - 1) / (32 * NWV)), 64 * NWV, 0, s>>>( \
-        users, (int)n_users, cat, (int)n_items, dim, k, w.cand, w.cnt, w.ucut, w.ovf_flag,       \
-        w.ovf_list, w.ovf_count)
-        // 4 waves (128 users) per workgroup, a 2-tile LDS-DMA ring and 62-entry
-        // lists: 79.9 KB of LDS, so two workgroups share a CU and each one's
-        // per-tile barrier / DMA wait is covered by the other (9.5 ms at config
-        // 2 against 10.3 ms for one 8-wave workgroup with a 3-tile ring;
-        // tools/screen_variants.sh).  NRK_SCREEN_VARIANT=0 selects the latter.
-        static const int var = [] { const char* e = getenv("NRK_SCREEN_VARIANT"); return e ? atoi(e) : 1; }();
-#define NRK_SCREEN_V(DPV, NWV, NSV, CLV)                                                                   \
-    ip_screen_kernel<DPV, NWV, NSV, CLV><<<(int)((n_users + 32 * NWV - 1) / (32 * NWV)), 64 * NWV, 0, s>>>( \
-        users, (int)n_users, cat, (int)n_items, dim, k, w.cand, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,        \
-        w.ovf_count)
-        if (var == 1 && dp <= 64) {  // D = 128 (config 5): the 8-wave form measured 0.8% faster
-            switch (dp) {
-                case 16: NRK_SCREEN_V(16, 4, 2, 62); break;
-                case 32: NRK_SCREEN_V(32, 4, 2, 62); break;
-                default: NRK_SCREEN_V(64, 4, 2, 62); break;
-            }
-        } else switch (dp) {
-            case 16: NRK_SCREEN(16, 8); break;
-            case 32: NRK_SCREEN(32, 8); break;
-            case 64: NRK_SCREEN(64, 8); break;
-            case 128: NRK_SCREEN(128, 8); break;
-            default: NRK_SCREEN(256, 4); break;
+        const int nu = (int)n_users, ni = (int)n_items;
+        switch (dp) {
+            case 16: launch_scan_k<16>(users, nu, cat, ni, dim, k, w, s); break;
+            case 32: launch_scan_k<32>(users, nu, cat, ni, dim, k, w, s); break;
+            case 64: launch_scan_k<64>(users, nu, cat, ni, dim, k, w, s); break;
+            case 128: launch_scan_k<128>(users, nu, cat, ni, dim, k, w, s); break;
+            default: launch_scan_k<256>(users, nu, cat, ni, dim, k, w, s); break;
         }
-#undef NRK_SCREEN_V
-#undef NRK_SCREEN
+
+        ip_select_kernel<<<(int)((n_users + 3) / 4), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt,
+                                                                 w.uinfo, w.cand, w.cnt, w.ucut, w.ovf_flag,
+                                                                 w.ovf_list, w.ovf_count);
+
     }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
@@ -1206,23 +1364,38 @@ int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
     int rc = ip_check(users, n_users, items, items, n_items, dim, k, workspace, workspace_bytes);
     if (rc != NRK_OK || n_users == 0) return rc;
     NRK_REQUIRE(out_scores && out_rows, "null output");
-    const IpWs w = ip_ws_layout(workspace, n_users);
+    const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
     hipStream_t s = as_stream(stream);
     const int g2 = (int)((n_users + 3) / 4);
-#define NRK_REFINE(DS4)                                                                        \
-    ip_refine_kernel<DS4><<<g2, 256, 0, s>>>(users, n_users, items,                             \
-                                             reinterpret_cast<const uint8_t*>(catalog), n_items, \
-                                             dim, k, row_offset,                                 \
-                                             w.cand, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,      \
-                                             w.ovf_count, out_scores, out_rows, out_exact)
-    if (dim == 32) NRK_REFINE(8);
-    else if (dim == 16) NRK_REFINE(4);
-    else if (dim == 64) NRK_REFINE(16);
-    else NRK_REFINE(0);
+    const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
+#define NRK_REFINE(DS4, SV)                                                                                  \
+    ip_refine_kernel<DS4, SV><<<g2, 256, 0, s>>>(users, n_users, items, cat, n_items, dim, k, row_offset,   \
+                                                 w.cand, w.bandcap, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,   \
+                                                 w.ovf_count, out_scores, out_rows, out_exact)
+#define NRK_REFINE_SV(DS4)                          \
+    do {                                            \
+        if (k <= 64) NRK_REFINE(DS4, 128);          \
+        else NRK_REFINE(DS4, 256);                  \
+    } while (0)
+    if (k <= IP_KFAST || n_items == 0) {
+        if (dim == 32) NRK_REFINE_SV(8);
+        else if (dim == 16) NRK_REFINE_SV(4);
+        else if (dim == 64) NRK_REFINE_SV(16);
+        else NRK_REFINE_SV(0);
+    }
+#undef NRK_REFINE_SV
 #undef NRK_REFINE
-    if (n_items > 0)
-        ip_fallback_kernel<<<256, 256, 0, s>>>(users, items, n_items, dim, k, row_offset, w.ovf_list,
-                                               w.ovf_count, out_scores, out_rows, out_exact);
+    if (n_items > 0) {
+        const int ns = next_pow2(std::max(k, 64));
+        const size_t lds = (size_t)ns * sizeof(Cand);
+        (void)hipFuncSetAttribute((const void*)ip_fallback_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        const int grid = (int)std::min<int64_t>(n_users, k > IP_KFAST ? 2048 : 256);
+
+        ip_fallback_kernel<<<grid, 256, lds, s>>>(users, items, n_items, dim, k, ns, row_offset, w.ovf_list,
+                                                  w.ovf_count, out_scores, out_rows, out_exact);
+
+    }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -1239,28 +1412,35 @@ int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const v
 }
 
 int nrk_ip_topk_bound(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
-                      int m, float* out_bound, void* workspace, size_t workspace_bytes, nrk_stream_t stream) {
+                      int k, int m, float* out_bound, void* workspace, size_t workspace_bytes,
+                      nrk_stream_t stream) {
     clear_error();
-    int rc = ip_check(users, n_users, (const float*)catalog, catalog, n_items, dim, 1, workspace,
+    int rc = ip_check(users, n_users, (const float*)catalog, catalog, n_items, dim, k, workspace,
                       workspace_bytes);
     if (rc != NRK_OK) return rc;
-    NRK_REQUIRE(m >= 1 && m <= IP_BOUND_MMAX, "m must be in [1, 32]");
+    if (k > IP_KFAST) NRK_UNSUPPORTED("the screen bound needs k <= 128");
+    NRK_REQUIRE(m >= 1 && m <= 256, "m must be in [1, 256]");
     if (n_users == 0) return NRK_OK;
     NRK_REQUIRE(out_bound != nullptr, "null pointer");
-    const IpWs w = ip_ws_layout(workspace, n_users);
+    const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
     hipStream_t s = as_stream(stream);
     if (n_items == 0) {
         // empty shard: no bound (the screen wrote no band)
-        (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * 2 * sizeof(int32_t), s);
+        (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * sizeof(int32_t), s);
     }
     const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(
         reinterpret_cast<const uint8_t*>(catalog) + catalog_body_bytes(n_items, pad_dim(dim)));
-    const int grid = (int)((n_users + 255) / 256);
-    if (m <= 8)
-        ip_bound_kernel<8><<<grid, 256, 0, s>>>(users, n_users, dim, hdr, w.cand, w.cnt, w.ucut, m, out_bound);
-    else
-        ip_bound_kernel<IP_BOUND_MMAX><<<grid, 256, 0, s>>>(users, n_users, dim, hdr, w.cand, w.cnt, w.ucut, m,
-                                                            out_bound);
+    const int grid = (int)((n_users + 3) / 4);
+    const int need = std::max(w.bandcap, m);
+#define NRK_BOUND(E, NS)                                                                                    \
+    ip_bound_kernel<E><<<grid, 256, (E) ? 0 : 4 * (NS) * sizeof(Cand), s>>>(users, n_users, dim, hdr, w.cand, \
+                                                                           w.bandcap, w.cnt, w.ucut, m, NS,  \
+                                                                           out_bound)
+    if (need <= 64) NRK_BOUND(1, 64);
+    else if (need <= 128) NRK_BOUND(2, 128);
+    else if (need <= 256) NRK_BOUND(4, 256);
+    else NRK_BOUND(0, next_pow2(need));
+#undef NRK_BOUND
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -1269,15 +1449,23 @@ int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, i
                             size_t workspace_bytes, nrk_stream_t stream) {
     clear_error();
     NRK_REQUIRE(n_users >= 0 && n_users < (1ll << 30), "n_users out of range");
-    NRK_REQUIRE(n_lists >= 1 && m >= 1 && n_lists * m <= 64, "need 1 <= n_lists * m <= 64");
-    NRK_REQUIRE(k >= 1 && k <= IP_KMAX, "k must be in [1, 32]");
+    NRK_REQUIRE(n_lists >= 1 && m >= 1 && n_lists * m <= 512, "need 1 <= n_lists * m <= 512");
+    NRK_REQUIRE(k >= 1 && k <= IP_KFAST, "k must be in [1, 128]");
     if (n_users == 0) return NRK_OK;
     NRK_REQUIRE(bounds && workspace, "null pointer");
-    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users).bytes, "workspace too small");
-    const IpWs w = ip_ws_layout(workspace, n_users);
+    // ucut's place depends on n_users only
+    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users, 0, 1, 1).bytes, "workspace too small");
+    const IpWs w = ip_ws_layout(workspace, n_users, 0, 1, 1);
     if (k > n_lists * m) return NRK_OK;  // fewer values than k: no bound, cut unchanged
-    ip_apply_bound_kernel<<<(int)((n_users + 3) / 4), 256, 0, as_stream(stream)>>>(w.ucut, n_users, bounds,
-                                                                                 n_lists, m, k);
+    const int tot = n_lists * m, grid = (int)((n_users + 3) / 4);
+    hipStream_t s = as_stream(stream);
+#define NRK_APPLY(E, NS) \
+    ip_apply_bound_kernel<E><<<grid, 256, (E) ? 0 : 4 * (NS) * sizeof(Cand), s>>>(w.ucut, n_users, bounds, n_lists, m, k, NS)
+    if (tot <= 64) NRK_APPLY(1, 64);
+    else if (tot <= 128) NRK_APPLY(2, 128);
+    else if (tot <= 256) NRK_APPLY(4, 256);
+    else NRK_APPLY(0, next_pow2(tot));
+#undef NRK_APPLY
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -1289,20 +1477,21 @@ int nrk_topk_merge(const double* in_exact, const int32_t* in_rows, int n_lists, 
     NRK_REQUIRE(n_lists >= 1 && k_in >= 1 && k_out >= 1 && n_users >= 0, "bad sizes");
     NRK_REQUIRE(list_stride >= n_users * (int64_t)k_in, "list_stride too small");
     const int tot = n_lists * k_in;
-    if (tot > 512) NRK_UNSUPPORTED("n_lists * k_in > 512");
+    if (tot > 1024) NRK_UNSUPPORTED("n_lists * k_in > 1024");
     NRK_REQUIRE(k_out <= tot, "k_out > n_lists * k_in");
     if (n_users == 0) return NRK_OK;
     NRK_REQUIRE(in_exact && in_rows && out_scores && out_rows, "null pointer");
     hipStream_t s = as_stream(stream);
     const int grid = (int)((n_users + 3) / 4);
-    if (tot <= 64)
-        topk_merge_kernel<1><<<grid, 256, 0, s>>>(in_exact, in_rows, n_lists, list_stride, n_users, k_in, k_out, out_scores, out_rows, out_exact);
-    else if (tot <= 128)
-        topk_merge_kernel<2><<<grid, 256, 0, s>>>(in_exact, in_rows, n_lists, list_stride, n_users, k_in, k_out, out_scores, out_rows, out_exact);
-    else if (tot <= 256)
-        topk_merge_kernel<4><<<grid, 256, 0, s>>>(in_exact, in_rows, n_lists, list_stride, n_users, k_in, k_out, out_scores, out_rows, out_exact);
-    else
-        topk_merge_kernel<8><<<grid, 256, 0, s>>>(in_exact, in_rows, n_lists, list_stride, n_users, k_in, k_out, out_scores, out_rows, out_exact);
+#define NRK_MERGE(E, NS)                                                                                    \
+    topk_merge_kernel<E><<<grid, 256, (E) ? 0 : 4 * (NS) * sizeof(Cand), s>>>(in_exact, in_rows, n_lists,      \
+                                                                              list_stride, n_users, k_in, k_out, \
+                                                                              NS, out_scores, out_rows, out_exact)
+    if (tot <= 64) NRK_MERGE(1, 64);
+    else if (tot <= 128) NRK_MERGE(2, 128);
+    else if (tot <= 256) NRK_MERGE(4, 256);
+    else NRK_MERGE(0, next_pow2(tot));
+#undef NRK_MERGE
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

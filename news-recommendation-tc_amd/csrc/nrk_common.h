@@ -76,7 +76,10 @@ __device__ __forceinline__ Cand shfl_xor_cand(const Cand& c, int m) {
 template <int E>
 __device__ __forceinline__ void wave_bitonic_sort(Cand (&x)[E]) {
     const int lane = threadIdx.x & (WAVE - 1);
-    constexpr int LOGN = (E == 1 ? 6 : E == 2 ? 7 : E == 4 ? 8 : 9);
+    // fully unrolled: E = 8 already costs minutes of compile time per
+    // instantiation, so larger sorts go through wave_lds_sort
+    static_assert(E == 1 || E == 2 || E == 4, "E must be 1, 2 or 4 (wave_lds_sort beyond)");
+    constexpr int LOGN = (E == 1 ? 6 : E == 2 ? 7 : 8);
 #pragma unroll
     for (int kl = 1; kl <= LOGN; ++kl) {
         const int k = 1 << kl;
@@ -113,6 +116,34 @@ __device__ __forceinline__ void wave_bitonic_sort(Cand (&x)[E]) {
                     x[e].row = take ? yr : x[e].row;
                 }
             }
+        }
+    }
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-cooperative bitonic sort of n candidates (a power of two) held in
+// this wave's LDS region, best first.  Run-time loops (nothing unrolled):
+// the large-list path of the merge / bound / fusion kernels.
+__device__ inline void wave_lds_sort(Cand* x, int n) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    wave_sync_lds();
+    for (int sz = 2; sz <= n; sz <<= 1) {
+        for (int st = sz >> 1; st > 0; st >>= 1) {
+            for (int i = lane; i < n / 2; i += WAVE) {
+                const int lo = 2 * st * (i / st) + (i % st), hi = lo + st;
+                const bool up = (lo & sz) == 0;
+                const Cand a = x[lo], b = x[hi];
+                if (up ? better(b, a) : better(a, b)) {
+                    x[lo] = b;
+                    x[hi] = a;
+                }
+            }
+            wave_sync_lds();
         }
     }
 }

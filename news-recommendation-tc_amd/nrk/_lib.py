@@ -34,7 +34,7 @@ SIGNATURES = {
     "nrk_ip_topk": (INT, [P, I64, P, P, I64, INT, INT, I64, P, P, P, P, SZ, P]),
     "nrk_ip_topk_screen": (INT, [P, I64, P, I64, INT, INT, P, SZ, P]),
     "nrk_ip_topk_finish": (INT, [P, I64, P, P, I64, INT, INT, I64, P, P, P, P, SZ, P]),
-    "nrk_ip_topk_bound": (INT, [P, I64, P, I64, INT, INT, P, P, SZ, P]),
+    "nrk_ip_topk_bound": (INT, [P, I64, P, I64, INT, INT, INT, P, P, SZ, P]),
     "nrk_ip_topk_apply_bound": (INT, [I64, P, INT, INT, INT, P, SZ, P]),
     "nrk_topk_merge": (INT, [P, P, INT, I64, I64, INT, INT, P, P, P, P]),
     "nrk_row_normalize": (INT, [P, I64, INT, P, P, P]),

@@ -52,7 +52,7 @@ class HipShard:
         """fp16 MFMA screen; returns this shard's m largest exact lower
         bounds per user (fp32 [U, m])."""
         self.ops.ip_topk_screen(users, self.cat, self.k, self.ws)
-        return self.ops.ip_topk_bound(users, self.cat, m, self.ws)
+        return self.ops.ip_topk_bound(users, self.cat, self.k, m, self.ws)
 
     def finish(self, users, bounds=None):
         """Exact refine -> (exact f64 [U, k], global rows i32 [U, k]) of this
@@ -68,12 +68,12 @@ class HipShard:
 
 def bound_width(k: int, world: int) -> int:
     """Bounds per user and shard for the exchange: world * m >= k values
-    (so the k-th largest exists) with a little slack, world * m <= 64; 0 =
-    no exchange (one rank, or too many ranks for one wave's sort)."""
+    (so the k-th largest exists) with a little slack, world * m <= 512; 0 =
+    no exchange (one rank, or too many ranks for nrk_ip_topk_apply_bound)."""
     if world <= 1:
         return 0
-    m = min(32, -(-k // world) + 1)
-    return m if world * m <= 64 and world * m >= k else 0
+    m = min(256, -(-k // world) + 1)
+    return m if world * m <= 512 and world * m >= k else 0
 
 
 def _default_merge(exact_lists, row_lists, k):

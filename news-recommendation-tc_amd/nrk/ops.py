@@ -82,6 +82,10 @@ def tt_item_fwd(item_table, ids):
 
 
 # ------------------------------------------------------------------ top-k --
+IP_KFAST = 128   # k on the MFMA screen path (csrc/ip_topk.hip); larger k takes the exact path
+IP_KMAX = 2048   # largest k compiled
+
+
 class Catalog:
     """The search index: fp32 rows (kept for exact rescoring) + packed bf16
     copy in MFMA fragment order.  = faiss.IndexFlatIP(d).add(items)."""
@@ -108,8 +112,8 @@ def ip_topk(users, catalog: Catalog, k: int, row_offset: int = 0, exact: bool = 
     _need(users, torch.float32, name="users")
     if users.dim() != 2 or users.shape[1] != catalog.d:
         raise ValueError(f"users must be [n, {catalog.d}]")
-    if not (1 <= k <= 32):
-        raise ValueError("k must be in [1, 32]")
+    if not (1 <= k <= IP_KMAX):
+        raise ValueError(f"k must be in [1, {IP_KMAX}]")
     n = users.shape[0]
     dev = users.device
     s = torch.empty((n, k), dtype=torch.float32, device=dev)
@@ -135,8 +139,8 @@ def topk_merge(exact_lists, row_lists, k_out):
     _need(exact_lists, torch.float64, name="exact_lists")
     _need(row_lists, torch.int32, tuple(exact_lists.shape), "row_lists")
     G, n, k_in = exact_lists.shape
-    if G * k_in > 512 or k_out > G * k_in:
-        raise ValueError("need G*k_in <= 512 and k_out <= G*k_in")
+    if G * k_in > 1024 or k_out > G * k_in:
+        raise ValueError("need G*k_in <= 1024 and k_out <= G*k_in")
     dev = exact_lists.device
     s = torch.empty((n, k_out), dtype=torch.float32, device=dev)
     r = torch.empty((n, k_out), dtype=torch.int32, device=dev)
@@ -164,14 +168,15 @@ def ip_topk_finish(users, catalog: Catalog, k: int, workspace, out_scores, out_r
               workspace.numel(), _stream())
 
 
-def ip_topk_bound(users, catalog: Catalog, m: int, workspace):
-    """After ip_topk_screen: per user the m largest exact lower bounds of
-    this shard (fp32 [n, m], descending, -inf padded), each bounding a
-    distinct item's exact score."""
+def ip_topk_bound(users, catalog: Catalog, k: int, m: int, workspace):
+    """After ip_topk_screen (same k): per user the m largest exact lower
+    bounds of this shard (fp32 [n, m], descending, -inf padded), each
+    bounding a distinct item's exact score."""
     _dev(users, workspace)
     n = users.shape[0]
     out = torch.empty((n, m), dtype=torch.float32, device=users.device)
-    _lib.call("nrk_ip_topk_bound", _ptr(users), n, _ptr(catalog.packed), catalog.n, catalog.d, int(m), _ptr(out),
+    _lib.call("nrk_ip_topk_bound", _ptr(users), n, _ptr(catalog.packed), catalog.n, catalog.d, int(k), int(m),
+              _ptr(out),
               _ptr(workspace), workspace.numel(), _stream())
     return out
 

@@ -45,8 +45,15 @@ def test_argument_errors_raise_valueerror():
     assert b"k must be" in L.nrk_last_error()
     with pytest.raises(ValueError):
         _lib.check(rc, "nrk_ip_topk")
-    rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, 33, 0, None, None, None, None, 0, None)
+    rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, 2049, 0, None, None, None, None, 0, None)
     assert rc == _lib.NRK_EUNSUPPORTED
+    # k = 61 (RecallEnsemble's 2 * topk + 1) and 129 (exact path) are accepted; the null
+    # pointers are what fails
+    for k in (61, 129):
+        rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, k, 0, None, None, None, None, 0, None)
+        assert rc == _lib.NRK_EINVAL and b"null pointer" in L.nrk_last_error()
+    # the workspace grows with k (band + appended maxima) but not beyond the screen path
+    assert L.nrk_ip_topk_workspace_bytes(1000, 364047, 32, 101) > L.nrk_ip_topk_workspace_bytes(1000, 364047, 32, 31)
 
 
 def test_din_prepare_refuses_unsupported_item_counts():

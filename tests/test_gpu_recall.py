@@ -108,6 +108,72 @@ def test_ip_topk_ties_overflow_fallback(ops):
     assert np.array_equal(s, so)
 
 
+@pytest.mark.parametrize(
+    "n_users,n_items,d,k",
+    [
+        (300, 5000, 32, 61),    # RecallEnsemble's recall(uid, 2 * 30) -> k + 1 = 61 (fusion.py:478)
+        (257, 20000, 32, 101),
+        (130, 7000, 32, 128),   # largest k on the screen path
+        (66, 3001, 16, 64),
+        (70, 4000, 64, 77),
+        (40, 1500, 250, 65),    # EmbeddingSimilarity width
+        (33, 2500, 32, 129),    # exact path (k > 128)
+        (20, 1200, 32, 700),
+        (9, 500, 32, 600),      # k > n_items: -1 / -FLT_MAX padding
+    ],
+)
+def test_ip_topk_large_k_vs_oracle(ops, n_users, n_items, d, k):
+    """k beyond round 2's cap of 32: the screen path up to k = 128, the exact
+    path above it; bit-exact rows and scores."""
+    rng = np.random.default_rng(n_users + n_items + d + k)
+    users = _unit(rng.standard_normal((n_users, d)))
+    users[0] = 0.0  # zero user: all-tie row
+    items = _unit(rng.standard_normal((n_items, d)))
+    s, r, e = _run_topk(ops, users, items, k)
+    so, ro, eo = oracle.ip_topk(users, items, k, exact=True)
+    assert np.array_equal(r, ro)
+    assert np.array_equal(s, so)
+    assert np.array_equal(e[ro >= 0], eo[ro >= 0])
+
+
+@pytest.mark.parametrize("k", [61, 101, 200])
+def test_ip_topk_large_k_ties(ops, k):
+    """Tie stress at large k: duplicated catalog rows, quantised vectors,
+    users equal to catalog rows (exact ties across the k-th place)."""
+    rng = np.random.default_rng(k)
+    base = _unit(rng.standard_normal((40, 32)))
+    items = np.concatenate([base[rng.integers(0, 40, size=3000)],
+                            _unit(np.round(rng.standard_normal((3000, 32)) * 2) / 2)]).astype(np.float32)
+    users = _unit(rng.standard_normal((96, 32)))
+    users[:4] = 0.0
+    users[4:24] = base[rng.integers(0, 40, size=20)]
+    s, r, _ = _run_topk(ops, users, items, k)
+    so, ro = oracle.ip_topk(users, items, k)
+    assert np.array_equal(r, ro)
+    assert np.array_equal(s, so)
+
+
+def test_recall_ensemble_style_call(golden):
+    """RecallEnsemble.recall calls recall(user_id, topk=topk * 2)
+    (fusion.py:478): at BASELINE's top-30 that is a (60 + 1)-deep search
+    through YoutubeDNNRecaller.recall, one user at a time."""
+    from nrk.recall.youtubednn_recaller import YoutubeDNNRecaller
+
+    g = golden("youtubednn_small")
+    ue, ie = g["user_embeddings"], g["item_embeddings"]
+    rec = YoutubeDNNRecaller.from_embeddings(ue, ie, user_index_2_rawid=g["user_index_2_rawid"],
+                                             item_index_2_rawid=g["item_index_2_rawid"])
+    users = [int(u) for u in g["recall_users"][:12]]
+    so, ro = oracle.ip_topk(ue.astype(np.float32), ie.astype(np.float32), 61)
+    u2i = {int(r): i for i, r in enumerate(g["user_index_2_rawid"])}
+    i2r = {i: int(r) for i, r in enumerate(g["item_index_2_rawid"])}
+    want = oracle.youtubednn_recall(so, ro, u2i, i2r, users, 60)
+    for u in users:
+        got = rec.recall(u, topk=60)
+        assert [a for a, _ in got] == [a for a, _ in want[u]]
+        assert [b for _, b in got] == [b for _, b in want[u]]
+
+
 def test_recall_lists_match_reference(golden):
     """YoutubeDNNRecaller.recall semantics end to end (drop rank 0, row->raw quirk)."""
     from nrk.recall.youtubednn_recaller import YoutubeDNNRecaller
@@ -255,8 +321,8 @@ def test_screen_eps_bounds_the_fp16_rounding(ops, d):
     ws = ops.ip_topk_workspace(U, cat, K, "cuda")
     ops.ip_topk_screen(_dev(users), cat, K, ws)
     torch.cuda.synchronize()
-    # workspace layout (ip_ws_layout): 256 B, candidate lists, then ucut float2 [U]
-    off = 256 + ((U * 2 * 48 * 8 + 255) // 256) * 256
+    # workspace layout (ip_ws_layout): 256 B header, then ucut float2 [U]
+    off = 256
     eps = ws[off: off + U * 8].view(torch.float32).view(U, 2)[:, 1].double().cpu().numpy()
 
     def p2(maxabs):  # pow2_scale: maps max|x| into [2^13, 2^14)

@@ -37,5 +37,5 @@ for _ in range(reps):
     t_s += ev[0].elapsed_time(ev[1])
     t_f += ev[1].elapsed_time(ev[2])
 chk = int((r.long() * torch.arange(1, K + 1, device=dev)).sum().item())
-print(f"variant {os.environ.get('NRK_SCREEN_VARIANT', '0')}: screen {t_s / reps:.3f} ms, finish {t_f / reps:.3f} ms, "
+print(f"variant {os.environ.get('NRK_SCAN_VARIANT', '0')}: screen {t_s / reps:.3f} ms, finish {t_f / reps:.3f} ms, "
       f"rows checksum {chk}")
