@@ -56,6 +56,15 @@ int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* i
 
 /* Item tower.  Replaces get_item_embedding (:184-188) + numpy re-norm
  * (:485-489): out[r] = renorm(normalize(E_i[ids[r]])). */
+/* The user tower at any depth (youtubednn_hidden_units of any length,
+ * youtubednn_recaller.py:105-112): weights packed per layer as W_l
+ * [widths[l], in_l] row-major then b_l [widths[l]] (in_0 = 2 * dim), 1 to 8
+ * layers of width <= 256, the last equal to dim.  Same outputs as
+ * nrk_tt_user_fwd for two layers. */
+int nrk_tt_user_fwd_layers(const float* user_table, int64_t n_user_rows, const float* item_table,
+                           int64_t n_item_rows, int dim, const int32_t* uid, const int32_t* hist,
+                           const int32_t* hist_len, int64_t n, int seq_len, const float* weights, int n_layers,
+                           const int* widths, float* out, nrk_stream_t stream);
 int nrk_tt_item_fwd(const float* item_table, int64_t n_item_rows, int dim, const int32_t* ids,
                     int64_t n, float* out, nrk_stream_t stream);
 
@@ -334,17 +343,26 @@ int nrk_gather_rows(const void* src, int64_t n_rows, int row_words, const int32_
  * strategy: 0 weighted_sum, 1 weighted_avg, 2 max_score, 3 harmonic_mean,
  * 4 diversity_weighted, 5 rrf (:189-265).  norm: 0 local (per list min-max,
  * :71-98), 1 global (gmin / gmax from nrk_fuse_minmax, :100-134), 2 z-score
- * (zmean / zstd per method, :136-187).  Optional seen_off / seen: per-user
- * item codes removed after the merge (:320-326).  Output: the top-k items
- * by (merged score desc, first appearance asc) -- the reference's stable
- * sort of its insertion-ordered dict -- -1 padded, and the count per user.
- * At most 256 entries per user and 16 methods. */
+ * (zmean / zstd per method, :136-187; device exp), 3 pre-normalised (the
+ * caller passes the normalised scores: the Python wrapper computes the
+ * z-score sigmoid with numpy exactly as the reference does).  Optional
+ * seen_off / seen: per-user item codes removed after the merge (:320-326).
+ * Output: the top-k items by (merged score desc, first appearance asc) --
+ * the reference's stable sort of its insertion-ordered dict -- -1 padded,
+ * and the count per user.  nrk_fuse takes users of at most 256 entries: a
+ * user with more gets out_cnt = -1 (padded output); nrk_fuse_wide takes any
+ * user of at most max_entries (<= 2048) entries, any topk. */
 int nrk_fuse_minmax(const double* score, int64_t n, double* out_minmax, nrk_stream_t stream);
 int nrk_fuse(const int64_t* offsets, int64_t n_users, const int32_t* item, const double* score,
              const int32_t* method, const int32_t* rank, int n_methods, const double* weight, int strategy,
              int norm, double gmin, double gmax, const double* zmean, const double* zstd, const int64_t* seen_off,
              const int32_t* seen, int topk, int32_t* out_item, double* out_score, int32_t* out_cnt,
              nrk_stream_t stream);
+int nrk_fuse_wide(const int64_t* offsets, int64_t n_users, const int32_t* item, const double* score,
+                  const int32_t* method, const int32_t* rank, int n_methods, const double* weight, int strategy,
+                  int norm, double gmin, double gmax, const double* zmean, const double* zstd,
+                  const int64_t* seen_off, const int32_t* seen, int max_entries, int topk, int32_t* out_item,
+                  double* out_score, int32_t* out_cnt, nrk_stream_t stream);
 
 /* ---------------------------------------------------------------------- */
 /* Ranker context features                                                */

@@ -198,7 +198,8 @@ __device__ __forceinline__ void top_insert(float (&t)[MT], float v) {
 // Scan: NW waves x UG x 32 users per workgroup share one NSL-slot LDS ring of
 // catalog tiles (8 KB, or one 16-KB block at dim 256).  Per tile every wave
 // reads the tile's A fragments once and runs TB x DS x UG MFMAs.
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false>
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false,
+          int DBG = 0>
 __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
     int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     float pend[UG];  // IE = 2: the lane's largest max since its group's last insert
 #pragma unroll
     for (int g = 0; g < UG; ++g) pend[g] = -INFINITY;
-    auto tile = [&](int tt, const u32x4 (&afr)[FULLREAD ? TB * DS : 1], auto mask_c) {
+    auto tile = [&](int tt, const u32x4 (&afr)[FULLREAD ? TB * DS : 1], auto mask_c, int) {
         constexpr bool MASK = decltype(mask_c)::value;
         float mx[UG][TB];
 #pragma unroll
@@ -393,6 +394,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             vt[g] = mx[g][0];
 #pragma unroll
             for (int b = 1; b < TB; ++b) vt[g] = fmaxf(vt[g], mx[g][b]);
+        }
+        if constexpr (DBG == 1) {  // dev floor measurement: MFMA + max only
+#pragma unroll
+            for (int g = 0; g < UG; ++g) pend[g] = fmaxf(pend[g], vt[g]);
+            return;
         }
         // appends: every half-block max >= tau reaches the user's HBM list
         // (the count runs past the capacity -- the select then sends the user
@@ -442,38 +448,52 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                 }
             }
         }
-        // threshold: the lane's largest max since the last insert enters its
-        // top list (a subset of the half-block maxima: the (jk + 1)-th largest
-        // stays a lower bound), then tau = (min over the user's two lanes) -
-        // 2 eps.  Every inserted value exceeded the lane's list minimum at
-        // its own tile, >= the tau it was tested against, so it was appended.
-        // IE = 2: group g inserts at tiles tt % 2 == g % 2 only.
+        // threshold: maxima enter the lane's top list (a subset of the
+        // half-block maxima: the (jk + 1)-th largest stays a lower bound),
+        // then tau = (min over the user's two lanes) - 2 eps.  Every inserted
+        // value exceeded the lane's list minimum, >= the tau of its tile, so
+        // it was appended.
+        //   IE = 1: every tile, per group, the lane's tile max when some lane
+        //           of the wave has one that enters (branchy);
+        //   IE = 2: no branch: group IG (alternating by tile, from the tile
+        //           loop) inserts the lane's largest max since its last
+        //           insert (pend), -inf (a no-op) when it does not enter.
+        auto retau = [&](int g) {
+            const float lb = fminf(t[g][MT - 1], partner32f(t[g][MT - 1], h));
+            const float c = lb - 2.0f * eps_s[g];
+            const uint32_t cb = __float_as_uint(c);
+            uint32_t rb = c > 0.0f ? cb - 1u : cb + 1u;  // one ulp toward -inf
+            rb = c == 0.0f ? 0x80000001u : rb;
+            const float tv = lb == -INFINITY ? -FLT_MAX : __uint_as_float(rb);
+            tau[g] = live[g] ? tv : INFINITY;
+        };
+        if constexpr (IE == 1) {
 #pragma unroll
-        for (int g = 0; g < UG; ++g) {
-            float v = vt[g];
-            if constexpr (IE == 2) {
-                pend[g] = fmaxf(pend[g], v);
-                if ((tt & 1) != (g & 1) && tt + 1 < ntile) continue;
-                v = pend[g];
-                pend[g] = -INFINITY;
+            for (int g = 0; g < UG; ++g) {
+                const float v = vt[g];
+                const bool in = v > t[g][MT - 1];
+                if (__builtin_amdgcn_ballot_w64(in)) {
+                    top_insert<MT>(t[g], in ? v : -INFINITY);
+                    retau(g);
+                }
             }
-            const bool in = v > t[g][MT - 1];
-            if (__builtin_amdgcn_ballot_w64(in)) {
-                top_insert<MT>(t[g], in ? v : -INFINITY);
-                const float lb = fminf(t[g][MT - 1], partner32f(t[g][MT - 1], h));
-                const float c = lb - 2.0f * eps_s[g];
-                const uint32_t cb = __float_as_uint(c);
-                uint32_t rb = c > 0.0f ? cb - 1u : cb + 1u;  // one ulp toward -inf
-                rb = c == 0.0f ? 0x80000001u : rb;
-                float tv = lb == -INFINITY ? -FLT_MAX : __uint_as_float(rb);
-                tau[g] = live[g] ? tv : INFINITY;
+        } else {
+#pragma unroll
+            for (int g = 0; g < UG; ++g) pend[g] = fmaxf(pend[g], vt[g]);
+            // group (tt & 1) (UG = 2) / every other tile (UG = 1): a uniform branch
+#pragma unroll
+            for (int g = 0; g < UG; ++g) {
+                if ((tt & 1) == g) {
+                    const float v = pend[g];
+                    pend[g] = -INFINITY;
+                    top_insert<MT>(t[g], v > t[g][MT - 1] ? v : -INFINITY);
+                    retau(g);
+                }
             }
         }
     };
 
-#pragma unroll
-    for (int p = 0; p < NSL - 1; ++p) issue_tile(p);
-    for (int tt = 0; tt < ntile; ++tt) {
+    auto step = [&](int tt, int ig_c) {
         // own pieces of tile tt landed (the next NSL-2 tiles' stay in
         // flight; appends issued since only make the wait conservative); the
         // barrier publishes everyone's pieces and retires slot (tt-1) % NSL
@@ -482,9 +502,12 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         issue_tile(tt + NSL - 1);
         u32x4 afr[FULLREAD ? TB * DS : 1];
         if constexpr (FULLREAD) read_frags(tt, afr);
-        if (tt < full_tiles) tile(tt, afr, std::false_type{});
-        else tile(tt, afr, std::true_type{});
-    }
+        if (tt < full_tiles) tile(tt, afr, std::false_type{}, ig_c);
+        else tile(tt, afr, std::true_type{}, ig_c);
+    };
+#pragma unroll
+    for (int p = 0; p < NSL - 1; ++p) issue_tile(p);
+    for (int tt = 0; tt < ntile; ++tt) step(tt, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
 
 #pragma unroll
@@ -494,6 +517,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         if (user < n_users) {
             acnt[(size_t)user * 2 + h] = cnt[g];
             if (h == 0) uinfo[user] = make_float4(live[g] ? lb : -INFINITY, eps_s[g], scl[g], eps_u[g]);
+            if (DBG == 1 && pend[g] == 12345.0f) acnt[(size_t)user * 2 + h] = 7;
         }
     }
 }
@@ -1209,11 +1233,11 @@ static inline int next_pow2(int x) {
 
 // scan variants: (DP, waves per workgroup, ring slots, user groups per wave,
 // register list length, waves per SIMD)
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false>
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false, int DBG = 0>
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
     const int per_wg = NW * 32 * UG;
-    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<(n_users + per_wg - 1) / per_wg, NW * 64, 0, s>>>(
+    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP, DBG><<<(n_users + per_wg - 1) / per_wg, NW * 64, 0, s>>>(
         users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo);
 }
 
@@ -1226,11 +1250,14 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
         // dev A/B switch (tools/screen_time.py): NRK_SCAN_VARIANT
         static const int var = [] { const char* e = getenv("NRK_SCAN_VARIANT"); return e ? atoi(e) : 0; }();
         switch (var) {
-            case 1: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 1: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 2: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 3: launch_scan_v<DP, 8, 3, 2, MT, 4, false>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 4: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 5: launch_scan_v<DP, 8, 3, 2, MT, 4, true, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 3: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 4: launch_scan_v<DP, 8, 4, 2, MT, 3, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 5: launch_scan_v<DP, 8, 3, 2, MT, 3, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 6: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 7: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 8: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
             default: break;
         }
     }
@@ -1238,7 +1265,7 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
     // appends whole tiles (TAPP).  Config 2: 7.5 ms against 7.9 for 4-wave
     // workgroups with a 4-slot ring (tools/scan_ab.sh)
     constexpr int NW = (UG == 2) ? 8 : 4, NSL = (UG == 2) ? 3 : 4;
-    launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 1, MT == 16>(users, n_users, cat, n_items, dim, k, w, s);
+    launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 2, MT == 16>(users, n_users, cat, n_items, dim, k, w, s);
 }
 
 template <int DP>

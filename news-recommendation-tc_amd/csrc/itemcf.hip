@@ -33,6 +33,7 @@ namespace nrk {
 constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys per workgroup
+constexpr int CF_WIDE_MAX = 2048;  // largest topn / topk (wide LDS path above 64)
 constexpr int64_t CF_HEAVY = 4096;               // top-n rows longer than this get a workgroup
 // LDS tile images of 4096 8-byte values read as thread-contiguous chunks of
 // 16: one pad slot per 16 keeps the chunk reads free of bank conflicts
@@ -973,6 +974,151 @@ __global__ __launch_bounds__(1024) void cf_topn_heavy_kernel(const int64_t* __re
     }
 }
 
+// ----------------------------------------------------- wide top-k (k > 64) --
+// The reference has no limit on itemcf_sim_item_topk / the recall topk
+// (itemcf_recaller.py:41-54, :125) or on rank_and_recommend's topk.  Above
+// the 64-lane register paths: one wave per row keeps a running top-K
+// (K = next_pow2(k)) best-first in LDS; each chunk of up to K new entries
+// lands behind it and the 2K are re-sorted by an LDS bitonic sort on
+// (score desc, first asc) -- a total order, so the result does not depend on
+// the chunking.
+__device__ inline void cf_lds_sort(CfEnt* x, int n) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    wave_sync_lds();
+    for (int sz = 2; sz <= n; sz <<= 1) {
+        for (int st = sz >> 1; st > 0; st >>= 1) {
+            for (int i = lane; i < n / 2; i += WAVE) {
+                const int lo = 2 * st * (i / st) + (i % st), hi = lo + st;
+                const bool up = (lo & sz) == 0;
+                const CfEnt a = x[lo], b = x[hi];
+                const bool b_first = cf_better(b.s, b.f, a.s, a.f);
+                if (up ? b_first : !b_first && (a.s != b.s || a.f != b.f)) {
+                    x[lo] = b;
+                    x[hi] = a;
+                }
+            }
+            wave_sync_lds();
+        }
+    }
+}
+
+template <class Get>
+__device__ inline void cf_wave_topk(CfEnt* buf, int K, int64_t n, Get get) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    for (int i = lane; i < 2 * K; i += WAVE) buf[i] = CfEnt{-INFINITY, INT64_MAX, -1};
+    for (int64_t c0 = 0; c0 < n; c0 += K) {
+        wave_sync_lds();
+        for (int i = lane; i < K; i += WAVE) buf[K + i] = c0 + i < n ? get(c0 + i) : CfEnt{-INFINITY, INT64_MAX, -1};
+        cf_lds_sort(buf, 2 * K);
+    }
+    wave_sync_lds();
+}
+
+__global__ __launch_bounds__(64) void cf_topn_wide_kernel(const int64_t* __restrict__ row_off, int64_t n_rows,
+                                                        const int32_t* __restrict__ cols,
+                                                        const double* __restrict__ vals,
+                                                        const int64_t* __restrict__ first, int topn, int K,
+                                                        int32_t* __restrict__ out_cols, double* __restrict__ out_vals,
+                                                        int32_t* __restrict__ out_cnt) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    CfEnt* buf = reinterpret_cast<CfEnt*>(dyn);
+    const int lane = threadIdx.x;
+    for (int64_t row = blockIdx.x; row < n_rows; row += gridDim.x) {
+        const int64_t a = row_off[row], n = row_off[row + 1] - a;
+        cf_wave_topk(buf, K, n, [&](int64_t i) { return CfEnt{vals[a + i], first[a + i], cols[a + i]}; });
+        const int64_t m = n < topn ? n : topn;
+        for (int i = lane; i < topn; i += WAVE) {
+            const bool ok = i < m;
+            out_cols[row * topn + i] = ok ? buf[i].c : -1;
+            out_vals[row * topn + i] = ok ? buf[i].s : 0.0;
+        }
+        if (lane == 0) out_cnt[row] = (int32_t)m;
+        wave_sync_lds();
+    }
+}
+
+// rc_topk_kernel for topk > 64 (same outputs): candidates by the wave top-K,
+// then the hot fill (:116-122) appended in hot order -- every fill score
+// -x - 100 is below every candidate's (products of positive weights) and
+// the fill scores decrease with x, so no re-sort is needed.
+__global__ __launch_bounds__(64) void rc_topk_wide_kernel(
+    const int64_t* __restrict__ q_slot, int64_t nq, const int64_t* __restrict__ offsets,
+    const int32_t* __restrict__ items, const int32_t* __restrict__ hot, int n_hot,
+    const int32_t* __restrict__ eq, const int32_t* __restrict__ ej, const double* __restrict__ ev,
+    const int64_t* __restrict__ ef, const int64_t* __restrict__ n_emit, int topk, int K,
+    int32_t* __restrict__ out_items, double* __restrict__ out_scores, int32_t* __restrict__ out_src,
+    int32_t* __restrict__ out_cnt) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    CfEnt* buf = reinterpret_cast<CfEnt*>(dyn);
+    const int lane = threadIdx.x;
+    const int64_t ne = *n_emit;
+    for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const int64_t sl = q_slot[q];
+        int32_t* oi = out_items + q * topk;
+        double* os = out_scores + q * topk;
+        int32_t* osrc = out_src + q * topk;
+        if (sl < 0) {  // cold start: [(hot[i], -i) for i < topk] (:68-70)
+            const int m = n_hot < topk ? n_hot : topk;
+            for (int i = lane; i < topk; i += WAVE) {
+                oi[i] = i < m ? hot[i] : -1;
+                os[i] = i < m ? -(double)i : 0.0;
+                osrc[i] = i < m ? 2 : -1;
+            }
+            if (lane == 0) out_cnt[q] = m;
+            continue;
+        }
+        const int64_t a = rc_lower(eq, ne, q), e = rc_lower(eq, ne, q + 1), n = e - a;
+        cf_wave_topk(buf, K, n, [&](int64_t i) { return CfEnt{ev[a + i], ef[a + i], ej[a + i]}; });
+        const int mc = (int)(n < topk ? n : topk);
+        for (int i = lane; i < mc; i += WAVE) {
+            oi[i] = buf[i].c;
+            os[i] = buf[i].s;
+            osrc[i] = 0;
+        }
+        int got = 0;
+        if (mc < topk) {
+            const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
+            int need = topk - mc;
+            for (int x0 = 0; x0 < n_hot && need > 0; x0 += WAVE) {
+                const int x = x0 + lane;
+                bool ok = false;
+                int32_t hv = -1;
+                if (x < n_hot) {
+                    hv = hot[x];
+                    ok = true;
+                    for (int64_t l = 0; l < L && ok; ++l) ok = items[b + l] != hv;
+                    if (ok && n > 0) {  // binary search in the query's candidate js (sorted)
+                        int64_t lo = a, hi = e;
+                        while (lo < hi) {
+                            const int64_t mid = (lo + hi) >> 1;
+                            if (ej[mid] < hv) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        ok = !(lo < e && ej[lo] == hv);
+                    }
+                }
+                const unsigned long long bal = __ballot(ok);
+                const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+                if (ok && rank < need) {
+                    oi[mc + got + rank] = hv;
+                    os[mc + got + rank] = (double)(-x - 100);
+                    osrc[mc + got + rank] = 1;
+                }
+                const int take = __popcll(bal) < need ? __popcll(bal) : need;
+                got += take;
+                need -= take;
+            }
+        }
+        for (int i = mc + got + lane; i < topk; i += WAVE) {
+            oi[i] = -1;
+            os[i] = 0.0;
+            osrc[i] = -1;
+        }
+        if (lane == 0) out_cnt[q] = mc + got;
+        wave_sync_lds();
+    }
+}
+
 // CSR row offsets of the (i, j)-sorted similarity entries: off[r] = first
 // entry with i >= r (binary search per row; no atomics)
 __global__ __launch_bounds__(256) void cf_row_offsets_kernel(const int32_t* __restrict__ ei, int64_t n,
@@ -1062,6 +1208,12 @@ static int bits_for(int64_t n) {  // smallest b with 2^b > n
     return b;
 }
 
+static inline int cf_wide_k(int k) {
+    int p = 64;
+    while (p < k) p <<= 1;
+    return p;
+}
+
 }  // namespace nrk
 
 using namespace nrk;
@@ -1144,11 +1296,21 @@ int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
                     int32_t* out_cnt, nrk_stream_t stream) {
     clear_error();
     NRK_REQUIRE(topn >= 1, "topn must be >= 1");
-    if (topn > 64) NRK_UNSUPPORTED("topn must be <= 64");
+    if (topn > CF_WIDE_MAX) NRK_UNSUPPORTED("topn must be <= 2048");
     NRK_REQUIRE(n_rows >= 0, "n_rows < 0");
     if (n_rows == 0) return NRK_OK;
     // cols / vals / first may be null when the CSR has no entries (empty torch tensors)
     NRK_REQUIRE(row_off && out_cols && out_vals && out_cnt, "null pointer");
+    if (topn > 64) {
+        const int K = cf_wide_k(topn);
+        const size_t lds = (size_t)2 * K * sizeof(CfEnt);
+        (void)hipFuncSetAttribute((const void*)cf_topn_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        cf_topn_wide_kernel<<<(int)(n_rows < 65536 ? n_rows : 65536), 64, lds, as_stream(stream)>>>(
+            row_off, n_rows, cols, vals, first, topn, K, out_cols, out_vals, out_cnt);
+        NRK_CHECK_LAUNCH();
+        return NRK_OK;
+    }
     const int64_t g = (n_rows + 3) / 4;
     cf_topn_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, as_stream(stream)>>>(
         row_off, n_rows, cols, vals, first, topn, out_cols, out_vals, out_cnt);
@@ -1191,7 +1353,7 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
     clear_error();
     NRK_REQUIRE(n_query >= 0 && n_cand >= 0 && n_hot >= 0, "negative size");
     NRK_REQUIRE(topk >= 1, "topk must be >= 1");
-    if (topk > 64) NRK_UNSUPPORTED("topk must be <= 64");
+    if (topk > CF_WIDE_MAX) NRK_UNSUPPORTED("topk must be <= 2048");
     NRK_REQUIRE(topn >= 1 && n_items >= 1 && ke >= 0, "bad sizes");
     NRK_REQUIRE(n_cand < (int64_t(1) << 31) - RS_TILE, "n_cand must be < 2^31");
     if (n_query == 0) return NRK_OK;
@@ -1239,8 +1401,18 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
     } else {
         (void)hipMemsetAsync(w.n_emit, 0, sizeof(int64_t), s);
     }
-    rc_topk_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, hot, n_hot, w.eq, w.ej, w.ev, w.ef,
-                                      w.n_emit, topk, out_items, out_scores, out_src, out_cnt);
+    if (topk <= 64) {
+        rc_topk_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, hot, n_hot, w.eq, w.ej, w.ev, w.ef,
+                                          w.n_emit, topk, out_items, out_scores, out_src, out_cnt);
+    } else {
+        const int K = cf_wide_k(topk);
+        const size_t lds = (size_t)2 * K * sizeof(CfEnt);
+        (void)hipFuncSetAttribute((const void*)rc_topk_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        rc_topk_wide_kernel<<<(int)(n_query < 65536 ? n_query : 65536), 64, lds, s>>>(
+            q_slot, n_query, offsets, items, hot, n_hot, w.eq, w.ej, w.ev, w.ef, w.n_emit, topk, K, out_items,
+            out_scores, out_src, out_cnt);
+    }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

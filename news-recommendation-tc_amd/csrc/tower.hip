@@ -122,6 +122,76 @@ __global__ __launch_bounds__(256) void tt_user_kernel(
     }
 }
 
+// Any depth (youtubednn_hidden_units is a list, youtubednn_recaller.py:105-112):
+// user_tower = [Linear(in_l, w_l), ReLU, Dropout] per layer.  Same gather
+// and re-normalisation as tt_user_kernel; the layers run from one packed
+// weight buffer (per layer W_l [w_l, in_l] row-major, then b_l [w_l]) read
+// through the caches, lane o owning outputs o, o + 64, ..., inputs broadcast
+// from a per-wave LDS row; each output is the same q-ascending fma chain as
+// the two-layer kernel.
+constexpr int TT_MAXL = 8, TT_MAXW = 256;
+struct TtLayers {
+    int n;
+    int w[TT_MAXL];
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void tt_user_mlp_kernel(
+    const float* __restrict__ user_table, const float* __restrict__ item_table,
+    const int32_t* __restrict__ uid, const int32_t* __restrict__ hist,
+    const int32_t* __restrict__ hist_len, int64_t n, int T, const float* __restrict__ wts, TtLayers ly,
+    float* __restrict__ out) {
+    __shared__ float sx[4][2][TT_MAXW > 2 * D ? TT_MAXW : 2 * D];
+    constexpr int P = WAVE / D;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int d = lane % D, ph = lane / D;
+    const int64_t wstride = (int64_t)gridDim.x * 4;
+    for (int64_t u = (int64_t)blockIdx.x * 4 + wave; u < n; u += wstride) {
+        const int len = hist_len[u];
+        const int32_t hv = lane < T ? hist[u * T + lane] : 0;
+        const float xu = user_table[(int64_t)uid[u] * D + d];
+        float sum = 0.0f;
+        const int nit = (len + P - 1) / P;
+        for (int i = 0; i < nit; ++i) {
+            const int t = ph + P * i;
+            const int32_t r = __shfl(hv, t < T ? t : 0, WAVE);
+            const float v = item_table[(int64_t)(t < len ? r : 0) * D + d];
+            if (t < len) sum += v;  // t ascending
+        }
+#pragma unroll
+        for (int off = D; off < WAVE; off <<= 1) sum += __shfl_xor(sum, off, WAVE);
+        const float xm = sum / ((float)len + 1e-8f);
+        if (lane < D) {
+            sx[wave][0][lane] = xu;
+            sx[wave][0][D + lane] = xm;
+        }
+        wave_sync_lds();
+        int in = 2 * D, cur = 0;
+        const float* wl = wts;
+        for (int l = 0; l < ly.n; ++l) {
+            const int wo = ly.w[l];
+            const float* bl = wl + (size_t)wo * in;
+            for (int o = lane; o < wo; o += WAVE) {
+                float z = bl[o];
+                const float* wr = wl + (size_t)o * in;
+                for (int qq = 0; qq < in; ++qq) z += wr[qq] * sx[wave][cur][qq];
+                sx[wave][cur ^ 1][o] = fmaxf(z, 0.0f);
+            }
+            wave_sync_lds();
+            wl = bl + wo;
+            in = wo;
+            cur ^= 1;
+        }
+        const float v = lane < D ? sx[wave][cur][lane] : 0.0f;
+        const float nn = sqrtf(wave_sum_f32(v * v));
+        const float v1 = v / fmaxf(nn, 1e-12f);
+        float n2 = sqrtf(wave_sum_f32(v1 * v1));
+        if (n2 == 0.0f) n2 = 1.0f;
+        if (lane < D) out[u * D + lane] = v1 / n2;
+        wave_sync_lds();  // sx is rewritten for the next user
+    }
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void tt_item_kernel(const float* __restrict__ table,
                                                       const int32_t* __restrict__ ids, int64_t n,
@@ -185,6 +255,35 @@ int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* i
     else if (dim == 32) NRK_TT_LAUNCH(32);
     else NRK_TT_LAUNCH(64);
 #undef NRK_TT_LAUNCH
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_tt_user_fwd_layers(const float* user_table, int64_t n_user_rows, const float* item_table,
+                           int64_t n_item_rows, int dim, const int32_t* uid, const int32_t* hist,
+                           const int32_t* hist_len, int64_t n, int seq_len, const float* weights, int n_layers,
+                           const int* widths, float* out, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n >= 0 && seq_len >= 1 && seq_len <= 64, "bad sizes (seq_len must be in [1, 64])");
+    NRK_REQUIRE(n_user_rows > 0 && n_item_rows > 0, "empty embedding tables");
+    if (!(dim == 16 || dim == 32 || dim == 64)) NRK_UNSUPPORTED("dim must be 16, 32 or 64");
+    NRK_REQUIRE(widths != nullptr, "null widths");
+    if (n_layers < 1 || n_layers > TT_MAXL) NRK_UNSUPPORTED("1 to 8 hidden layers are compiled");
+    TtLayers ly{};
+    ly.n = n_layers;
+    for (int l = 0; l < n_layers; ++l) {
+        if (widths[l] < 1 || widths[l] > TT_MAXW) NRK_UNSUPPORTED("hidden widths must be in [1, 256]");
+        ly.w[l] = widths[l];
+    }
+    NRK_REQUIRE(widths[n_layers - 1] == dim, "last hidden width must equal the embedding dim "
+                                             "(youtubednn_recaller.py:461-465)");
+    if (n == 0) return NRK_OK;
+    NRK_REQUIRE(user_table && item_table && uid && hist && hist_len && weights && out, "null pointer");
+    hipStream_t s = as_stream(stream);
+    const int grid = (int)std::min<int64_t>((n + 3) / 4, 2048);
+    if (dim == 16) tt_user_mlp_kernel<16><<<grid, 256, 0, s>>>(user_table, item_table, uid, hist, hist_len, n, seq_len, weights, ly, out);
+    else if (dim == 32) tt_user_mlp_kernel<32><<<grid, 256, 0, s>>>(user_table, item_table, uid, hist, hist_len, n, seq_len, weights, ly, out);
+    else tt_user_mlp_kernel<64><<<grid, 256, 0, s>>>(user_table, item_table, uid, hist, hist_len, n, seq_len, weights, ly, out);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

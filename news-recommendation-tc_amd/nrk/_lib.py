@@ -27,6 +27,7 @@ SIGNATURES = {
     "nrk_last_error": (ctypes.c_char_p, []),
     "nrk_abi_version": (INT, []),
     "nrk_tt_user_fwd": (INT, [P, I64, P, I64, INT, P, P, P, I64, INT, P, P, INT, P, P, INT, P, P]),
+    "nrk_tt_user_fwd_layers": (INT, [P, I64, P, I64, INT, P, P, P, I64, INT, P, INT, P, P, P]),
     "nrk_tt_item_fwd": (INT, [P, I64, INT, P, I64, P, P]),
     "nrk_ip_catalog_bytes": (SZ, [I64, INT]),
     "nrk_ip_catalog_build": (INT, [P, I64, INT, P, P]),
@@ -56,6 +57,7 @@ SIGNATURES = {
     "nrk_gather_rows": (INT, [P, I64, INT, P, I64, P, P]),
     "nrk_fuse_minmax": (INT, [P, I64, P, P]),
     "nrk_fuse": (INT, [P, I64, P, P, P, P, INT, P, INT, INT, F64, F64, P, P, P, P, INT, P, P, P, P]),
+    "nrk_fuse_wide": (INT, [P, I64, P, P, P, P, INT, P, INT, INT, F64, F64, P, P, P, P, INT, INT, P, P, P, P]),
     "nrk_ctx_features": (INT, [P, P, P, P, P]),
     "nrk_din_prep_bytes": (SZ, [INT]),
     "nrk_din_prepare": (INT, [P, INT, P, INT, I64, P, P]),

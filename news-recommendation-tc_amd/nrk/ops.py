@@ -69,6 +69,38 @@ def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1):
     return out
 
 
+def tt_user_fwd_layers(user_table, item_table, uid, hist, hist_len, layers):
+    """The user tower at any depth (youtubednn_recaller.py:105-112):
+    ``layers`` = [(W_l [w_l, in_l], b_l [w_l]), ...] fp32 device tensors, the
+    last width equal to the embedding dim."""
+    import ctypes
+
+    _dev(user_table, item_table, uid, hist, hist_len, *[t for wb in layers for t in wb])
+    n, T = hist.shape
+    D = user_table.shape[1]
+    _need(user_table, torch.float32, name="user_table")
+    _need(item_table, torch.float32, (item_table.shape[0], D), "item_table")
+    _need(uid, torch.int32, (n,), "uid")
+    _need(hist, torch.int32, name="hist")
+    _need(hist_len, torch.int32, (n,), "hist_len")
+    widths, packed, fan_in = [], [], 2 * D
+    for l, (w, b) in enumerate(layers):
+        _need(w, torch.float32, (w.shape[0], fan_in), f"W{l}")
+        _need(b, torch.float32, (w.shape[0],), f"b{l}")
+        widths.append(int(w.shape[0]))
+        packed += [w.reshape(-1), b]
+        fan_in = w.shape[0]
+    if n and (int(hist_len.min()) < 0 or int(hist_len.max()) > T):
+        raise ValueError("hist_len out of [0, T]")
+    wts = torch.cat(packed).contiguous()
+    out = torch.empty((n, D), dtype=torch.float32, device=uid.device)
+    wv = (ctypes.c_int * len(widths))(*widths)
+    _lib.call("nrk_tt_user_fwd_layers", _ptr(user_table), user_table.shape[0], _ptr(item_table),
+              item_table.shape[0], D, _ptr(uid), _ptr(hist), _ptr(hist_len), n, T, _ptr(wts), len(widths),
+              ctypes.cast(wv, _P), _ptr(out), _stream())
+    return out
+
+
 def tt_item_fwd(item_table, ids):
     """get_item_embedding + re-normalisation (youtubednn_recaller.py:184-188, :485-489)."""
     _dev(item_table, ids)
@@ -84,6 +116,7 @@ def tt_item_fwd(item_table, ids):
 # ------------------------------------------------------------------ top-k --
 IP_KFAST = 128   # k on the MFMA screen path (csrc/ip_topk.hip); larger k takes the exact path
 IP_KMAX = 2048   # largest k compiled
+CF_TOPK_MAX = 2048  # nrk_itemcf_topn / nrk_itemcf_recall (register path <= 64, LDS path above)
 
 
 class Catalog:
@@ -395,6 +428,8 @@ def itemcf_topn(row_off, cols, vals, first, topn=20):
     """Per-row top-n by (score desc, first asc) -- the reference's stable
     ``sorted(..., reverse=True)[:topn]`` (itemcf_recaller.py:41-54).
     Returns (cols [R, topn] int32 -1 padded, vals [R, topn] f64, cnt [R])."""
+    if not (1 <= topn <= CF_TOPK_MAX):
+        raise NotImplementedError(f"topn must be in [1, {CF_TOPK_MAX}]")
     _dev(row_off, cols, vals, first)
     _need(row_off, torch.int64, name="row_off")
     _need(cols, torch.int32, name="cols")
@@ -435,8 +470,8 @@ def itemcf_recall(q_slot, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created, 
         _need(emb_cols, torch.int32, (n_items, ke), "emb_cols")
         _need(emb_vals, torch.float64, (n_items, ke), "emb_vals")
         _need(emb_cnt, torch.int32, (n_items,), "emb_cnt")
-    if not (1 <= topk <= 64):
-        raise NotImplementedError("topk must be in [1, 64]")
+    if not (1 <= topk <= CF_TOPK_MAX):
+        raise NotImplementedError(f"topk must be in [1, {CF_TOPK_MAX}]")
     nq = q_slot.numel()
     dev = q_slot.device
     cand_off = torch.empty(nq + 1, dtype=torch.int64, device=dev)

@@ -21,7 +21,7 @@ scores, tie order unpinned).
 Here the grouping is a stable host argsort of the user column (the data
 prep the reference does in pandas); the per-user top-k by (score desc, row
 asc) runs on the GPU through nrk_itemcf_topn (one wave per user, running
-top-64 bitonic merge).  top_k <= 64.
+top-64 bitonic merge; top_k > 64: a running top-K in LDS).  top_k <= 2048.
 """
 from __future__ import annotations
 
@@ -37,8 +37,8 @@ from .. import ops
 def rank_topk(user_ids, probs, top_k: int = 10, device="cuda"):
     """Per-user top-k rows.  Returns (users [G] ascending, rows [G, top_k]
     int32 into the inputs (-1 padded), scores [G, top_k] float32, counts [G])."""
-    if not (1 <= top_k <= 64):
-        raise NotImplementedError("top_k must be in [1, 64]")
+    if not (1 <= top_k <= ops.CF_TOPK_MAX):
+        raise NotImplementedError(f"top_k must be in [1, {ops.CF_TOPK_MAX}]")
     user_ids = np.asarray(user_ids)
     p = probs.detach().float().cpu().numpy() if torch.is_tensor(probs) else np.asarray(probs, np.float32)
     if len(p) != len(user_ids):

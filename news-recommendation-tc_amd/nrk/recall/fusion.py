@@ -32,6 +32,8 @@ from .._lib import P, call
 STRATEGIES = {"weighted_sum": 0, "weighted_avg": 1, "max_score": 2, "harmonic_mean": 3,
               "diversity_weighted": 4, "rrf": 5}
 NORMS = {"local": 0, "global": 1, "z-score": 2}
+FUSE_MAX = 256        # entries per user (and topk) of nrk_fuse (4 per lane, registers)
+FUSE_WIDE_MAX = 2048  # entries per user of nrk_fuse_wide (LDS)
 
 
 class RecallFusion:
@@ -57,8 +59,6 @@ class RecallFusion:
         if not self.recall_results:
             raise ValueError("No recall results added. Use add_recall_result() first.")
         names = list(self.recall_results)
-        if len(names) > 16:
-            raise NotImplementedError("at most 16 recall methods")
         # the reference's user order: a set updated method by method (:306-309)
         all_users = set()
         for nm in names:
@@ -86,16 +86,29 @@ class RecallFusion:
             mt.append(np.full(n, m, np.int32))
             rk.append((np.arange(n) - np.repeat(np.cumsum(lens) - lens, lens)).astype(np.int32))
             if NORMS.get(self.normalize_method, 0) == 2 and n:
+                # fusion.py:155-175 with numpy on the host: the same mean / std
+                # of the Python list and the same np.exp, so the sigmoid is the
+                # reference's to the bit; the device then takes the scores as
+                # pre-normalised (norm 3)
                 all_scores = [t[1] for t in flat]
-                zmean[m] = np.mean(all_scores)
-                zstd[m] = np.std(all_scores)
+                mean_score = np.mean(all_scores)
+                std_score = np.std(all_scores)
+                if std_score > 0:
+                    z = (scores - mean_score) / std_score
+                    sc[-1] = 1.0 / (1.0 + np.exp(-z))
+                else:
+                    sc[-1] = np.full(n, 0.5)
         us = np.concatenate(us)
+        if len(us) == 0:  # every list empty: {user: []} as the reference (:311-333)
+            self.fused_results = {u: [] for u in users}
+            return self.fused_results
         order = np.argsort(us, kind="stable")  # by user; method order, then list order inside
         item_codes, item_keys = pd.factorize(np.concatenate(it)) if len(us) else (np.zeros(0, np.int64), [])
         score = np.concatenate(sc)[order]
         counts = np.bincount(us, minlength=len(users))
-        if counts.max(initial=0) > 256:
-            raise NotImplementedError("more than 256 recalled entries for one user")
+        max_entries = int(counts.max(initial=0))
+        if max_entries > FUSE_WIDE_MAX:
+            raise NotImplementedError(f"more than {FUSE_WIDE_MAX} recalled entries for one user")
         offsets = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
         dev = self.device
         d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
@@ -103,6 +116,8 @@ class RecallFusion:
         t_score, t_m = d(score), d(np.concatenate(mt)[order])
         t_rank, t_w = d(np.concatenate(rk)[order]), d(np.array([self.weights[n] for n in names], np.float64))
         norm = NORMS.get(self.normalize_method, 0)
+        if norm == 2:
+            norm = 3  # normalised on the host above
         gmin = gmax = 0.0
         if norm == 1 and len(score):
             mm = torch.empty(2, dtype=torch.float64, device=dev)
@@ -115,8 +130,9 @@ class RecallFusion:
             lens = np.fromiter((len(x) for x in lists), np.int64, count=len(lists))
             flat = _obj(list(chain.from_iterable(lists)))
             codes = code_of.get_indexer(flat) if code_of is not None and len(flat) else np.full(len(flat), -1)
-            seen_off = d(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64))
-            seen = d(np.where(codes >= 0, codes, -2).astype(np.int32))  # -2 never matches an item code
+            if len(flat):  # no history item at all (e.g. cold-start users): nothing to remove
+                seen_off = d(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64))
+                seen = d(np.where(codes >= 0, codes, -2).astype(np.int32))  # -2 never matches an item code
         strat = STRATEGIES.get(self.fusion_strategy, 1)
         nu = len(users)
         o_item = torch.empty((nu, topk), dtype=torch.int32, device=dev)
@@ -124,9 +140,14 @@ class RecallFusion:
         o_cnt = torch.empty(nu, dtype=torch.int32, device=dev)
         zm, zs = d(zmean), d(zstd)
         p = lambda t: P(t.data_ptr()) if t is not None else None  # noqa: E731
-        call("nrk_fuse", p(t_off), nu, p(t_item), p(t_score), p(t_m), p(t_rank), len(names), p(t_w), strat, norm,
-             float(gmin), float(gmax), p(zm), p(zs), p(seen_off), p(seen), int(topk), p(o_item), p(o_score),
-             p(o_cnt), ops._stream())
+        if max_entries <= FUSE_MAX and topk <= FUSE_MAX:
+            call("nrk_fuse", p(t_off), nu, p(t_item), p(t_score), p(t_m), p(t_rank), len(names), p(t_w), strat,
+                 norm, float(gmin), float(gmax), p(zm), p(zs), p(seen_off), p(seen), int(topk), p(o_item),
+                 p(o_score), p(o_cnt), ops._stream())
+        else:
+            call("nrk_fuse_wide", p(t_off), nu, p(t_item), p(t_score), p(t_m), p(t_rank), len(names), p(t_w),
+                 strat, norm, float(gmin), float(gmax), p(zm), p(zs), p(seen_off), p(seen), max_entries, int(topk),
+                 p(o_item), p(o_score), p(o_cnt), ops._stream())
         oi, os_, oc = o_item.cpu().numpy(), o_score.cpu().numpy(), o_cnt.cpu().numpy()
         keys = np.asarray(item_keys, dtype=object)
         raw = keys[np.maximum(oi, 0)] if len(keys) else np.zeros(oi.shape, dtype=object)

@@ -141,8 +141,6 @@ class ItemCFRecaller(BaseRecaller):
                     continue
                 rows[pi] = [(pos[j], v) for j, v in dd.items() if j in pos]
             ke = max([len(r) for r in rows.values()] + [1])
-            if ke > 64:
-                raise NotImplementedError("more than 64 embedding neighbours per item")
             ec = np.full((n, ke), -1, np.int32)
             ev = np.zeros((n, ke), np.float64)
             en = np.zeros(n, np.int32)

@@ -73,21 +73,22 @@ class YoutubeDNNRecaller(BaseRecaller):
         user_tower.0.*, user_tower.3.*)."""
         sd = {k: (v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v))
               for k, v in state_dict.items()}
-        if len([k for k in sd if k.startswith("user_tower.") and k.endswith(".weight")]) != 2:
-            raise NotImplementedError("the GPU user tower is compiled for two hidden layers")
+        # user_tower = [Linear, ReLU, Dropout] per hidden unit: Linear l at index 3 l (:105-112)
+        n_layers = len([k for k in sd if k.startswith("user_tower.") and k.endswith(".weight")])
         user_col = np.asarray(click_df["user_id"], np.int64)
         uid, hist, hlen, item_raw, profile = extractors.youtubednn_histories(
             user_col, np.asarray(click_df["click_article_id"], np.int64), self.seq_max_len)
         user_raw = np.unique(user_col)
         dev = self.device
         f = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-        ue = ops.tt_user_fwd(
-            f(sd["user_embedding.weight"].astype(np.float32)),
-            f(sd["item_embedding.weight"].astype(np.float32)),
-            f(uid.astype(np.int32)), f(hist.astype(np.int32)), f(hlen.astype(np.int32)),
-            f(sd["user_tower.0.weight"]), f(sd["user_tower.0.bias"]),
-            f(sd["user_tower.3.weight"]), f(sd["user_tower.3.bias"]),
-        )
+        tabs = (f(sd["user_embedding.weight"].astype(np.float32)), f(sd["item_embedding.weight"].astype(np.float32)),
+                f(uid.astype(np.int32)), f(hist.astype(np.int32)), f(hlen.astype(np.int32)))
+        layers = [(f(sd[f"user_tower.{3 * l}.weight"].astype(np.float32)),
+                   f(sd[f"user_tower.{3 * l}.bias"].astype(np.float32))) for l in range(n_layers)]
+        if n_layers == 2 and layers[0][0].shape[0] <= 128:  # the tuned two-layer kernel (LDS-resident weights)
+            ue = ops.tt_user_fwd(*tabs, *layers[0], *layers[1])
+        else:
+            ue = ops.tt_user_fwd_layers(*tabs, layers)
         ie = ops.tt_item_fwd(f(sd["item_embedding.weight"].astype(np.float32)),
                              f(profile.astype(np.int32)))
         self._set_state(ue, ie, user_raw, item_raw)
@@ -116,9 +117,10 @@ class YoutubeDNNRecaller(BaseRecaller):
         if self.user_embeddings is None or self.catalog is None:
             raise ValueError("Model not trained. Call train() first.")
         n_users = self.user_embeddings.shape[0]
-        try:
-            idx = self._user_index.get_indexer(np.asarray(user_ids, dtype=np.int64))
-        except (TypeError, ValueError, OverflowError):  # non-integer ids: the dict's own lookup
+        arr = np.asarray(user_ids)
+        if arr.dtype.kind in "iu" and arr.ndim == 1 and self._user_index.is_unique:
+            idx = self._user_index.get_indexer(arr.astype(np.int64))
+        else:  # str / float / mixed ids: the reference's own dict lookup (user_rawid_2_index.get, :511)
             idx = np.array([self.user_rawid_2_index.get(u, -1) for u in user_ids], np.int64)
         known = (idx >= 0) & (idx < n_users)
         results: Dict[int, List[Tuple[int, float]]] = dict.fromkeys(user_ids)

@@ -37,8 +37,8 @@ class EmbeddingSimilarity(BaseSimilarityCalculator):
         """Device path: fp32 [n, d] rows -> (scores f32 [n, topk+1], rows i32
         [n, topk+1]) of the self-search, column 0 included."""
         topk = self.config.embedding_topk if topk is None else int(topk)
-        if topk + 1 > 32:
-            raise NotImplementedError("embedding_topk + 1 > 32 is not compiled")
+        if topk + 1 > ops.IP_KMAX:
+            raise NotImplementedError(f"embedding_topk + 1 > {ops.IP_KMAX} is not compiled")
         xn, nr = ops.row_normalize(emb.contiguous(), norms=True)
         if emb.shape[0] and not bool(torch.isfinite(nr).all() and (nr > 0).all()):
             raise ValueError("item embeddings must be finite with non-zero norm")

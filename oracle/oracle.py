@@ -133,6 +133,13 @@ def embedding_sim_dict(ids, scores, rows):
 # Two-tower forward (fp32, numpy)
 # --------------------------------------------------------------------------
 def tower_user(user_emb, item_emb, uid, hist, hist_len, w0, b0, w1, b1):
+    """YoutubeDNN.forward (youtubednn_recaller.py:129-182) + numpy re-norm (:467-470), two layers."""
+    return tower_user_layers(user_emb, item_emb, uid, hist, hist_len, [(w0, b0), (w1, b1)])
+
+
+def tower_user_layers(user_emb, item_emb, uid, hist, hist_len, layers):
+    """Any depth: user_tower = [Linear, ReLU, Dropout] per hidden unit
+    (youtubednn_recaller.py:105-112); ``layers`` = [(W_l, b_l), ...]."""
     f32 = np.float32
     ue = user_emb[uid].astype(f32)
     he = item_emb[hist].astype(f32)
@@ -140,8 +147,8 @@ def tower_user(user_emb, item_emb, uid, hist, hist_len, w0, b0, w1, b1):
     mask = (np.arange(T)[None, :] < hist_len[:, None]).astype(f32)[:, :, None]
     avg = (he * mask).sum(1, dtype=f32) / (hist_len.astype(f32)[:, None] + f32(1e-8))
     x = np.concatenate([ue, avg.astype(f32)], 1)
-    x = np.maximum(x @ w0.T.astype(f32) + b0.astype(f32), 0).astype(f32)
-    x = np.maximum(x @ w1.T.astype(f32) + b1.astype(f32), 0).astype(f32)
+    for w, b in layers:
+        x = np.maximum(x @ w.T.astype(f32) + b.astype(f32), 0).astype(f32)
     n = np.maximum(np.sqrt((x * x).sum(1, keepdims=True, dtype=f32)), f32(1e-12))
     x = (x / n).astype(f32)
     n2 = np.linalg.norm(x, axis=1, keepdims=True)

@@ -52,8 +52,10 @@ def test_argument_errors_raise_valueerror():
     for k in (61, 129):
         rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, k, 0, None, None, None, None, 0, None)
         assert rc == _lib.NRK_EINVAL and b"null pointer" in L.nrk_last_error()
-    # the workspace grows with k (band + appended maxima) but not beyond the screen path
-    assert L.nrk_ip_topk_workspace_bytes(1000, 364047, 32, 101) > L.nrk_ip_topk_workspace_bytes(1000, 364047, 32, 31)
+    # the append lists live in the workspace: bounded at config 2 (250k users), none on the exact path
+    ws31 = L.nrk_ip_topk_workspace_bytes(250000, 364047, 32, 31)
+    assert 0 < ws31 < 4 << 30
+    assert L.nrk_ip_topk_workspace_bytes(1000, 364047, 32, 129) < L.nrk_ip_topk_workspace_bytes(1000, 364047, 32, 101)
 
 
 def test_din_prepare_refuses_unsupported_item_counts():

@@ -242,7 +242,8 @@ def _reference_rank_and_recommend(main_df, probs, top_k):
     return rec
 
 
-@pytest.mark.parametrize("n_rows,n_users,top_k", [(1, 1, 10), (5000, 700, 10), (20000, 300, 64), (3000, 2999, 3)])
+@pytest.mark.parametrize("n_rows,n_users,top_k", [(1, 1, 10), (5000, 700, 10), (20000, 300, 64), (3000, 2999, 3),
+                                                  (30000, 200, 150)])
 def test_rank_and_recommend_matches_reference(n_rows, n_users, top_k, tmp_path):
     """RankPipeline.rank_and_recommend (rank_pipeline.py:143-191): per-user
     nlargest with first-occurrence ties, NaN after numbers, float-formatted item ids."""

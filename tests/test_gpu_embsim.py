@@ -63,7 +63,7 @@ def test_embedding_similarity_matches_reference_golden(golden):
     assert es.get_similar_items(-12345) == []
 
 
-@pytest.mark.parametrize("n,d,k", [(3000, 250, 20), (4097, 64, 31), (500, 32, 10)])
+@pytest.mark.parametrize("n,d,k", [(3000, 250, 20), (4097, 64, 31), (500, 32, 10), (3000, 250, 50), (2000, 250, 150)])
 def test_embedding_similarity_vs_oracle(n, d, k):
     from nrk.similarity.embedding import EmbeddingSimilarity
 

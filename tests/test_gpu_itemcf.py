@@ -127,7 +127,7 @@ def test_itemcf_no_pairs():
     assert sim.cnt.cpu().tolist() == [0, 0, 0, 2]
 
 
-@pytest.mark.parametrize("topn", [1, 20, 64])
+@pytest.mark.parametrize("topn", [1, 20, 64, 65, 100, 300])
 def test_itemcf_topn_vs_oracle(topn):
     from nrk import ops
 
@@ -239,7 +239,8 @@ def _recall_case(rng, n_users, n_items, max_len, topn, n_hot):
 
 @pytest.mark.parametrize("n_users,n_items,max_len,topn,topk,n_hot",
                          [(1, 3, 1, 20, 5, 2), (40, 30, 12, 5, 64, 100), (500, 400, 40, 20, 30, 50),
-                          (3000, 20000, 25, 20, 30, 50), (60, 5000, 250, 64, 64, 64)])
+                          (3000, 20000, 25, 20, 30, 50), (60, 5000, 250, 64, 64, 64),
+                          (500, 4000, 40, 20, 100, 300), (300, 2000, 30, 100, 200, 150), (50, 60, 8, 20, 100, 30)])
 def test_itemcf_recall_vs_oracle(n_users, n_items, max_len, topn, topk, n_hot):
     """nrk_itemcf_recall vs the C restatement of ItemCFRecaller.recall
     (oracle_itemcf_recall): candidate sums in (loc, x) order, hot fill,

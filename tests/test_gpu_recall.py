@@ -226,6 +226,31 @@ def test_tower_vs_oracle(ops, D, h0):
     np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-5, rtol=0)
 
 
+@pytest.mark.parametrize("widths", [[32], [64, 48, 32], [128, 96, 64, 32], [256, 32]])
+def test_tower_any_depth_vs_oracle(ops, widths):
+    """youtubednn_hidden_units of any length (youtubednn_recaller.py:105-112)."""
+    rng = np.random.default_rng(len(widths) * 11 + widths[0])
+    U, I, T, n, D = 300, 2000, 30, 555, widths[-1]
+    ue = (rng.standard_normal((U, D)) * 0.01).astype(np.float32)
+    ie = (rng.standard_normal((I, D)) * 0.01).astype(np.float32)
+    layers, fan = [], 2 * D
+    for w in widths:
+        layers.append(((rng.standard_normal((w, fan)) * 0.2).astype(np.float32),
+                       (rng.standard_normal(w) * 0.01).astype(np.float32)))
+        fan = w
+    uid = rng.integers(0, U, n)
+    hlen = rng.integers(0, T + 1, n)
+    hist = rng.integers(0, I, (n, T)) * (np.arange(T)[None] < hlen[:, None])
+    out = ops.tt_user_fwd_layers(_dev(ue), _dev(ie), _dev(uid, torch.int32), _dev(hist, torch.int32),
+                                 _dev(hlen, torch.int32), [(_dev(w), _dev(b)) for w, b in layers])
+    ref = oracle.tower_user_layers(ue, ie, uid, hist, hlen, layers)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-5, rtol=0)
+    if len(widths) == 2 and widths[0] <= 128:  # same bits as the two-layer kernel
+        two = ops.tt_user_fwd(_dev(ue), _dev(ie), _dev(uid, torch.int32), _dev(hist, torch.int32),
+                              _dev(hlen, torch.int32), *[_dev(a) for wb in layers for a in wb])
+        assert torch.equal(two, out)
+
+
 def test_full_size_topk_properties(ops):
     """Config 2 shapes (250k x 364,047 x 32, k=31): sortedness, exact scores,
     and oracle agreement on a user sample."""
