@@ -1250,22 +1250,20 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
         // dev A/B switch (tools/screen_time.py): NRK_SCAN_VARIANT
         static const int var = [] { const char* e = getenv("NRK_SCAN_VARIANT"); return e ? atoi(e) : 0; }();
         switch (var) {
-            case 1: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 2: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 3: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 4: launch_scan_v<DP, 8, 4, 2, MT, 3, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 5: launch_scan_v<DP, 8, 3, 2, MT, 3, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 6: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 7: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 8: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 1: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 2: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 3: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
             default: break;
         }
     }
-    // 8 waves (two per SIMD) share a 3-slot ring; 2 workgroups per CU.  k <= 32
-    // appends whole tiles (TAPP).  Config 2: 7.5 ms against 7.9 for 4-wave
-    // workgroups with a 4-slot ring (tools/scan_ab.sh)
+    // 8 waves share a 3-slot ring, 2 workgroups (4 waves / SIMD) per CU; k <= 32
+    // appends whole tiles (TAPP), every tile inserts (IE = 1).  Config 2
+    // (tools/scan_ab.sh, screen = scan + select): 7.1-7.2 ms; 4-wave
+    // workgroups 7.9-8.2, 4 / 6 / 8 ring slots 7.3-7.4, alternating inserts
+    // (IE = 2) 8.1 (the lagging cut doubles the appends the select reads);
+    // without any append / insert work (DBG = 1) 4.9-6.4 ms
     constexpr int NW = (UG == 2) ? 8 : 4, NSL = (UG == 2) ? 3 : 4;
-    launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 2, MT == 16>(users, n_users, cat, n_items, dim, k, w, s);
+    launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 1, MT == 16>(users, n_users, cat, n_items, dim, k, w, s);
 }
 
 template <int DP>
