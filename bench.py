@@ -11,18 +11,26 @@ index build (faiss add) and happens once, before the timed region.
 value = recalled user-item pairs / s = users x 30 / step time (rank 0 of the
 31 is dropped by recall(), youtubednn_recaller.py:524).
 
-With --gpus N > 1 (torch.distributed.run, one process per GPU, RCCL): by
-default every rank processes its own 250k users against the full catalog
-(weak scaling, no data-path collective); --shard catalog runs BASELINE
-config 4 instead (catalog split N-way, all_to_all of the shard-local top-31
-+ nrk_topk_merge, strong scaling).  The timed region is bracketed by
-barriers and the max over ranks is used.
+With --gpus N > 1 (torch.distributed.run, one process per GPU, RCCL) the
+layouts are BASELINE's (layout_plan):
+  * recall = config 4 (default --shard catalog): the same 250k users, the
+    catalog's 32-item blocks split N-way in whole screen tiles; each rank
+    runs the user tower for its user block (all_gather -> every user),
+    screens its item range for every user, the ranks exchange the shard
+    bounds (all_gather) and the band candidates (all_to_all to the user's
+    owner), and each rank refines its own user block exactly (strong
+    scaling: value = 250k x 30 / the slowest rank's step).  --shard users
+    runs N independent 250k-user problems instead (weak scaling).
+  * DIN = config 3: the 165 Dice batches of 4096 (last 3,909) split
+    round-robin, batch b on rank b mod N (value = 675,653 / the slowest
+    rank's pass).
+The timed regions are bracketed by barriers and the max over ranks is used.
 
-Extra fields on the JSON line: "roofline" for the dominant kernel
-(ip_screen), "cpu_baseline" (the oracle's per-user exact scan -- the
-reference's nq=1 IndexFlatIP shape -- on a bounded user sample, rank 0, N=1),
-and "din" (BASELINE config 3, DIN scored pairs/s) when the DIN kernels are
-built.
+Extra fields on the JSON line: "roofline" for the dominant kernel (the
+fp16 MFMA screen, ip_scan_kernel), "cpu_baseline" (the oracle's per-user
+exact scan -- the reference's nq=1 IndexFlatIP shape -- on a bounded user
+sample, rank 0, N=1), "din" (BASELINE config 3, DIN scored pairs/s),
+"itemcf" and "plugins" (N=1 only).
 """
 from __future__ import annotations
 
@@ -45,20 +53,46 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02e_traffic.json")
-BUSY_FILE = os.path.join(REPO, "profiles", "r02e_busy.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
+BUSY_FILE = os.path.join(REPO, "profiles", "r03_busy.json")
+CSRC = os.path.join(REPO, "news-recommendation-tc_amd", "csrc")
+
+
+def source_digest():
+    """sha256 (16 hex) of the kernel sources the PMC files were measured on:
+    tools/pmc_traffic.py / pmc_busy.py stamp it into the profile files, and
+    bench.py only reports their numbers while the sources still match."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(CSRC, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def _profile(path):
+    """A committed PMC summary, or None when absent or measured on other
+    kernel sources (stale)."""
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    return d if d.get("sources") == source_digest() else None
 
 
 def pmc_busy(kernels, default_config):
     """MFMA-busy / VALU-busy / stall shares of ``kernels`` from the committed
     rocprofv3 SQ-counter passes of this bench's default workloads
-    (tools/pmc_busy.sh -> tools/pmc_busy.py); None off the default config."""
-    if not default_config or not os.path.exists(BUSY_FILE):
+    (tools/pmc_busy.sh -> tools/pmc_busy.py, calibrated against the pure-MFMA /
+    pure-VALU micro-kernels of tools/calib); None off the default config or
+    when the file is stale."""
+    b = _profile(BUSY_FILE) if default_config else None
+    if b is None:
         return None
-    b = json.load(open(BUSY_FILE))
     out = {}
     for k in kernels:
-        m = [v for name, v in b.items() if name.startswith(k)]
+        m = [v for name, v in b["kernels"].items() if name.startswith(k)]
         if m:
             out[k.replace("nrk::", "")] = {x: m[0].get(x) for x in ("mfma_busy", "valu_busy", "wait_any", "wait_inst",
                                                                      "active")}
@@ -66,7 +100,7 @@ def pmc_busy(kernels, default_config):
 
 
 def _traffic_file():
-    return json.load(open(TRAFFIC_FILE)) if os.path.exists(TRAFFIC_FILE) else None
+    return _profile(TRAFFIC_FILE)
 
 
 def pmc_traffic(kernels, default_config):
@@ -163,6 +197,28 @@ def cpu_baseline_recall_gemm(users_np, items_np, k, sample, seconds):
         dt += time.perf_counter() - t0
         done += q.shape[0]
     return done * (k - 1) / dt, dt, done
+
+
+def cpu_share():
+    """Threads for the cpu_baseline legs: every CPU this process may run on
+    (sched_getaffinity), capped by a cgroup CPU quota (cpu.max) and by the
+    pool's OMP_NUM_THREADS -- on the MI355X pool a one-GPU box is given 16
+    CPUs of a 256-CPU host whose affinity mask it shares with other jobs, so
+    the affinity count alone would time contention, not the reference.
+    Returns (threads, how the number was chosen)."""
+    lim = [("sched_getaffinity", len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+            else os.cpu_count() or 1)]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            lim.append(("cgroup cpu.max", max(1, int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        lim.append(("OMP_NUM_THREADS", int(omp)))
+    t = min(v for _, v in lim)
+    return t, ", ".join(f"{n} {v}" for n, v in lim)
 
 
 def host_info():
@@ -298,21 +354,43 @@ def run_itemcf(args, device):
     if not args.no_cpu_baseline:
         from oracle import oracle
 
-        # the C restatement (single thread) on a bounded prefix of the same
-        # users, grown 4x until one timed run takes >= 2 s (or covers them all)
-        nu = 1000
-        while True:
-            nu = min(nu, len(users))
-            t0 = time.perf_counter()
-            oracle.itemcf_sim(offs[:nu + 1], dense[:offs[nu]].astype(np.int32), ts[:offs[nu]], created, len(ids))
-            dt = time.perf_counter() - t0
-            if dt >= 2.0 or nu == len(users):
-                break
-            nu *= 4
-        sp = int(((offs[1:nu + 1] - offs[:nu]) ** 2).sum())
-        out["cpu_baseline"] = {"value": round(sp / dt, 1), "unit": "ordered pairs/s (similarity)", "cores": 1,
-                               "kind": "port",
-                               "sample": f"first {nu} users, oracle/nrk_oracle.c oracle_itemcf_sim ({dt:.1f}s)"}
+        threads, why = cpu_share()
+        dn = dense.astype(np.int32)
+
+        def prefix(fn, budget, nu=1000):
+            # a bounded prefix of the same users, grown 4x until one timed run
+            # takes >= budget seconds (or covers them all)
+            while True:
+                nu = min(nu, len(users))
+                t0 = time.perf_counter()
+                fn(nu)
+                dt = time.perf_counter() - t0
+                if dt >= budget or nu == len(users):
+                    return nu, dt, int(((offs[1:nu + 1] - offs[:nu]) ** 2).sum())
+                nu *= 4
+
+        nu, dt, sp = prefix(lambda nu: oracle.itemcf_sim_omp(offs[:nu + 1], dn[:offs[nu]], ts[:offs[nu]], created,
+                                                             len(ids), threads), 3.0, 4000)
+        n1, d1, s1 = prefix(lambda nu: oracle.itemcf_sim(offs[:nu + 1], dn[:offs[nu]], ts[:offs[nu]], created,
+                                                         len(ids)), 2.0)
+
+        def pyloop(nu):
+            uit = {u: list(zip(dn[offs[u]:offs[u + 1]].tolist(), ts[offs[u]:offs[u + 1]].tolist()))
+                   for u in range(nu)}
+            oracle.itemcf_sim_pyloop(uit, created)
+
+        n2, d2, s2 = prefix(pyloop, 2.0, 250)
+        out["cpu_baseline"] = {
+            "value": round(sp / dt, 1), "unit": "ordered pairs/s (similarity)", "cores": threads, "kind": "port",
+            "threads_from": why,
+            "sample": f"first {nu} users, oracle_itemcf_sim_omp (C, OpenMP, rows split i mod {threads}; "
+                      f"bit-identical to the sequential sums) ({dt:.1f}s)",
+            "variants": [
+                {"value": round(s1 / d1, 1), "unit": "ordered pairs/s (similarity)", "cores": 1, "kind": "port",
+                 "sample": f"first {n1} users, oracle_itemcf_sim (C, one thread) ({d1:.1f}s)"},
+                {"value": round(s2 / d2, 1), "unit": "ordered pairs/s (similarity)", "cores": 1, "kind": "port",
+                 "sample": f"first {n2} users, oracle.itemcf_sim_pyloop: item_cf.py:33-84's Python dict loops "
+                           f"with numpy-scalar weights, the reference's own per-pair cost ({d2:.1f}s)"}]}
     return out
 
 
@@ -464,9 +542,23 @@ DIN_N_CTX, DIN_VOCAB_C = 16, 11
 DIN_BYTES_PER_PAIR = 225 * 4 + 225 * 64 + 4  # idx + bf16 rows + output
 
 
-def din_workload(seed, n, T, device):
+def din_batches(n, B, world, rank):
+    """Config 3 layout over N ranks: the Dice batches of B (last one short)
+    round-robin, batch b on rank b mod N.  Returns (this rank's batch ids,
+    its sample rows in batch order).  The short last batch is the highest id,
+    so it stays last on its rank and every rank's rows split into its own
+    batches of B exactly as on one GPU."""
+    nb = -(-n // B)
+    mine = list(range(rank, nb, world))
+    rows = (np.concatenate([np.arange(b * B, min(n, (b + 1) * B)) for b in mine]) if mine
+            else np.zeros(0, np.int64))
+    return mine, rows
+
+
+def din_workload(seed, n, T, device, rows=None):
     """Config 3 synthetic: uniform indices, hist_len ~ U[1, T] with 20% all-pad
-    rows, torch-default-initialised DINModel-shaped weights (seed 23)."""
+    rows, torch-default-initialised DINModel-shaped weights (seed 23).  The
+    same n samples on every rank; ``rows`` picks this rank's share."""
     torch.manual_seed(23)
     sd = {}
     uf = [f"u{i}" for i in range(len(DIN_VOCAB_U))]
@@ -495,29 +587,37 @@ def din_workload(seed, n, T, device):
         "ctx": rng.integers(0, DIN_VOCAB_C, (n, DIN_N_CTX), dtype=np.int32),
         "mask": mask,
     }
+    if rows is not None:
+        enc = {k: np.ascontiguousarray(v[rows]) for k, v in enc.items()}
     dev = {k: torch.from_numpy(v).to(device) for k, v in enc.items()}
     return sd, (uf, itf, cf), enc, dev
 
 
 def run_din(args, device, rank, world):
-    """BASELINE config 3: every one of the 675,653 samples scored, batches of
-    4096 (last 3,909), one nrk_din_forward per batch; the indices are resident
-    in HBM before the timed region."""
+    """BASELINE config 3: every one of the 675,653 samples scored in Dice
+    batches of 4096 (last 3,909), all of a rank's batches in one
+    nrk_din_forward_segments call; with N ranks batch b runs on rank b mod N
+    (din_batches).  The indices are resident in HBM before the timed region."""
     from nrk import ops
 
     n, T, B = args.din_samples, 50, 4096
-    sd, feats, enc, dev = din_workload(101 + rank, n, T, device)
+    mine, rows = din_batches(n, B, world, rank)
+    sd, feats, enc, dev = din_workload(101, n, T, device, rows=rows if world > 1 else None)
+    n_loc = int(dev["mask"].shape[0])
     p = ops.DinParams(sd, *feats, table_dtype="bf16", device=device)
-    ws = ops.din_workspace(p, n, T, device, batch_size=B)
-    probs = torch.empty(n, dtype=torch.float32, device=device)
-    ops.din_validate(p, dev["user"], dev["item"], dev["hist"], dev["ctx"])  # once, untimed
+    ws = ops.din_workspace(p, max(n_loc, 2), T, device, batch_size=B)
+    probs = torch.empty(n_loc, dtype=torch.float32, device=device)
+    if n_loc:
+        ops.din_validate(p, dev["user"], dev["item"], dev["hist"], dev["ctx"])  # once, untimed
     full = tuple(dev[k] for k in ("user", "item", "hist", "ctx", "mask"))
 
     def one_pass(ev=None):
-        # every Dice batch of B (last one short) in one nrk_din_forward_segments call
+        # every Dice batch of this rank (B each, the global last one short)
+        # in one nrk_din_forward_segments call
         if ev is not None:
             ev[0].record()
-        ops.din_forward(p, *full, workspace=ws, out=probs, validate=False, batch_size=B)
+        if n_loc:
+            ops.din_forward(p, *full, workspace=ws, out=probs, validate=False, batch_size=B)
         if ev is not None:
             ev[1].record()
 
@@ -544,24 +644,31 @@ def run_din(args, device, rank, world):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     pass_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    value = n / dt
-    achieved = DIN_BYTES_PER_PAIR * n / (pass_ms * 1e-3) / 1e9
-    t = pmc_din_pass(n == DIN_SAMPLES)
+    value = n / dt  # every sample of the job once / the slowest rank's pass
+    achieved = DIN_BYTES_PER_PAIR * n_loc / (pass_ms * 1e-3) / 1e9
+    default_cfg = n == DIN_SAMPLES and world == 1
+    t = pmc_din_pass(default_cfg)
     din_traffic = round(t) if t else None
-    out = {"value": round(value * world, 1), "unit": "DIN scored pairs/s", "ms_per_pass": round(dt * 1e3, 3),
+    out = {"value": round(value, 1), "unit": "DIN scored pairs/s", "ms_per_pass": round(dt * 1e3, 3),
            "samples": n, "batch": B, "seq_len": T, "dtype": "fp32 math, bf16 tables",
+           "parallelism": (f"Dice batches round-robin x{world} (batch b on rank b mod {world}; rank 0: "
+                           f"{len(mine)} batches, {n_loc} samples)" if world > 1 else "single"),
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": din_traffic,
-                        "traffic_unit": "bytes per pass, every launch of one nrk_din_forward_segments call (profiles/r02e_traffic.json din_pass)",
-                        "kernel": f"nrk_din_forward_segments ({n} samples in Dice batches of {B}, one call)",
+                        "traffic_unit": "bytes per pass, every launch of one nrk_din_forward_segments call "
+                                        "(profiles/r03_traffic.json din_pass)",
+                        "kernel": f"nrk_din_forward_segments ({n_loc} samples in Dice batches of {B}, one call)",
                         "kernel_ms": round(pass_ms, 4),
-                        "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * n,
+                        "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * n_loc,
                         "busy": pmc_busy(["nrk::din_att", "nrk::din_wh", "nrk::din_mlp1", "nrk::din_mlp2",
-                                          "nrk::din_head"], n == DIN_SAMPLES)}}
+                                          "nrk::din_head"], default_cfg)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle
 
         m = args.din_cpu_sample
+        threads, why = cpu_share()
+        torch_threads = torch.get_num_threads()
+        torch.set_num_threads(threads)
         sdn = {k: v.numpy() for k, v in sd.items()}
         model = oracle.DinTorchCPU(sdn, feats, round_bf16=True)
         tt = {k: torch.from_numpy(v) if k == "mask" else torch.from_numpy(v.astype(np.int64)) for k, v in enc.items()}
@@ -575,8 +682,9 @@ def run_din(args, device, rank, world):
         sl0 = {k: v[:m] for k, v in enc.items()}
         po, _, _ = oracle.din_forward(sdn, sl0["user"], sl0["item"], sl0["hist"], sl0["ctx"], sl0["mask"], feats,
                                       round_bf16=True)
+        torch.set_num_threads(torch_threads)
         out["cpu_baseline"] = {"value": round(nb * m / cdt, 1), "unit": "DIN scored pairs/s",
-                               "cores": torch.get_num_threads(), "kind": "port",
+                               "cores": threads, "kind": "port", "threads_from": why,
                                "sample": f"{nb} batches x {m} samples of the same workload, torch-CPU eval forward "
                                          f"of DINModel's formulation (oracle.DinTorchCPU, fp32), {cdt:.1f}s"}
         gp = ops.din_forward(p, *(dev[k][:m] for k in ("user", "item", "hist", "ctx", "mask")), workspace=ws)
@@ -629,20 +737,72 @@ def launch_ranks(n, argv):
     return rc
 
 
+def layout_plan(args, world):
+    """Per-rank work of the N-rank run (the dry run prints it, the workload
+    follows it):
+      recall: "catalog" (BASELINE config 4, default at N > 1): rank r screens
+              the 32-item blocks shard_blocks(I, N, r, tile) (whole screen
+              tiles) for every user, runs the tower for and refines the user
+              block shard_range(U, N, r); "users": every rank its own U users
+              against the whole catalog; N = 1: "single".
+      din:    the Dice batches of 4096 round-robin (din_batches)."""
+    from nrk.dist import shard_blocks, shard_range
+    from nrk.ops import ip_topk_tile_blocks
+
+    U, I, D = args.users, args.items, args.dim
+    layout = "single" if world == 1 else args.shard
+    tb = ip_topk_tile_blocks(D)
+    per = []
+    for r in range(world):
+        if layout == "catalog":
+            blo, bhi = shard_blocks(I, world, r, tb)
+            per.append({"rank": r, "blocks": [blo, bhi], "items": [min(I, 32 * blo), min(I, 32 * bhi)],
+                        "users": list(shard_range(U, world, r))})
+        else:
+            per.append({"rank": r, "blocks": [0, -(-I // 32)], "items": [0, I], "users": [0, U]})
+    rec = {"layout": layout, "tile_blocks": tb, "per_rank": per,
+           "parallelism": {"single": "single",
+                           "catalog": f"catalog-sharded x{world} (BASELINE config 4: shard screen, bound "
+                                      f"all_gather, band all_to_all, owner refine)",
+                           "users": f"users-sharded x{world} (independent replicas)"}[layout]}
+    n, B = args.din_samples, 4096
+    dper = []
+    for r in range(world):
+        mine, rows = din_batches(n, B, world, r)
+        dper.append({"rank": r, "batches": len(mine), "samples": int(len(rows)),
+                     "short_batch": bool(mine) and mine[-1] == -(-n // B) - 1 and n % B != 0})
+    din = {"batches": -(-n // B), "batch": B, "per_rank": dper,
+           "parallelism": (f"Dice batches round-robin x{world} (batch b on rank b mod {world})" if world > 1
+                           else "single")}
+    return {"recall": rec, "din": din}
+
+
 def dry_run(args, world, rank, local):
-    """--dry-run: the launcher and rendezvous without the workload (CPU
-    tests use it with --backend gloo): every rank joins the process group,
-    checks the world with an all_reduce, and rank 0 prints a JSON line."""
+    """--dry-run: the launcher, rendezvous and layout without the workload
+    (CPU tests use it with --backend gloo): every rank joins the process
+    group, checks the world with an all_reduce and that the ranks' own shares
+    of layout_plan cover the work once (item blocks, user blocks, DIN
+    samples), and rank 0 prints a JSON line with the plan."""
     import torch.distributed as dist
 
+    plan = layout_plan(args, world)
+    rec, din = plan["recall"]["per_rank"][rank], plan["din"]["per_rank"][rank]
+    mine = torch.tensor([1, rec["blocks"][1] - rec["blocks"][0], rec["users"][1] - rec["users"][0],
+                         din["samples"], din["batches"]], dtype=torch.int64)
     if world > 1:
         dist.init_process_group(args.backend or "gloo")
-        t = torch.ones(1)
-        dist.all_reduce(t)
-        assert int(t.item()) == world, (t, world)
-    log(f"[rank {rank}/{world}] local_rank {local} pid {os.getpid()} backend {args.backend or 'gloo'} (dry run)")
+        dist.all_reduce(mine)
+    tot = [int(x) for x in mine]
+    assert tot[0] == world, (tot, world)
+    if plan["recall"]["layout"] == "catalog":
+        assert tot[1] == -(-args.items // 32) and tot[2] == args.users, tot
+    assert tot[3] == args.din_samples and tot[4] == plan["din"]["batches"], tot
+    log(f"[rank {rank}/{world}] local_rank {local} pid {os.getpid()} backend {args.backend or 'gloo'} (dry run) "
+        f"blocks {rec['blocks']} users {rec['users']} din batches {din['batches']} samples {din['samples']}")
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry_run": True}), flush=True)
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry_run": True, "layout": plan,
+                          "covered": {"item_blocks": tot[1], "users": tot[2], "din_samples": tot[3],
+                                      "din_batches": tot[4]}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -673,9 +833,10 @@ def main(argv=None):
     ap.add_argument("--fused-items", type=int, default=5_000_000)
     ap.add_argument("--fused-hash-ctx", action="store_true",
                     help="config 5 with the synthetic hash-bin context instead of the real context features")
-    ap.add_argument("--shard", choices=["users", "catalog"], default="users",
-                    help="N>1 layout: users-sharded (weak scaling, no collective) or "
-                         "catalog-sharded (BASELINE config 4: all_to_all of shard top-k + merge)")
+    ap.add_argument("--shard", choices=["users", "catalog"], default="catalog",
+                    help="N>1 recall layout: catalog-sharded (BASELINE config 4, the default: shard "
+                         "screens, bound all_gather, band all_to_all, owner refine; strong scaling) or "
+                         "users-sharded (N independent 250k-user problems, weak scaling)")
     ap.add_argument("--din-samples", type=int, default=DIN_SAMPLES)
     ap.add_argument("--din-steps", type=int, default=10)
     ap.add_argument("--din-warmup", type=int, default=2)
@@ -713,22 +874,20 @@ def main(argv=None):
         return
 
     U, I, D, K = args.users, args.items, args.dim, args.topk + 1
-    catalog_mode = world > 1 and args.shard == "catalog"
+    plan = layout_plan(args, world)
+    catalog_mode = plan["recall"]["layout"] == "catalog"
     t0 = time.time()
     # users-sharded: every rank its own users (seed 23 + rank); catalog-sharded:
-    # one shared workload, rank r owns item rows [lo, hi)
+    # one shared workload, rank r screens item blocks [blk_lo, blk_hi)
     wl = recall_workload(23 if catalog_mode else 23 + rank, U, I, D, device)
     item_vec = ops.tt_item_fwd(wl["item_table"], torch.arange(I, dtype=torch.int32, device=device))
-    row_lo = 0
-    if catalog_mode:
-        from nrk.dist import HipShard, catalog_sharded_topk, gather_users, shard_range
-
-        row_lo, row_hi = shard_range(I, world, rank)
-        item_vec = item_vec[row_lo:row_hi].contiguous()
-        ulo, uhi = shard_range(U, world, rank)  # this rank's user-tower block
     cat = ops.Catalog(item_vec)
     if catalog_mode:
-        shard = HipShard(cat, row_lo, K, U)
+        from nrk.dist import HipRangeShard, catalog_sharded_owner, gather_users
+
+        me = plan["recall"]["per_rank"][rank]
+        (blo, bhi), (ulo, uhi) = me["blocks"], me["users"]
+        shard = HipRangeShard(cat, blo, bhi, K, U)
     else:
         ws = ops.ip_topk_workspace(U, cat, K, device)
         out_s = torch.empty((U, K), dtype=torch.float32, device=device)
@@ -737,9 +896,10 @@ def main(argv=None):
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s: U={U} I={I} D={D} K={K} clicks={wl['n_clicks']}")
 
     def step_catalog(ev=None):
-        # tower for this rank's users only, all_gather -> every user on every
-        # rank; screen the shard, all_reduce(MAX) the bounds, refine above the
-        # global bound, all_to_all + merge (nrk.dist.catalog_sharded_topk)
+        # tower for this rank's user block, all_gather -> every user on every
+        # rank; screen this rank's item blocks for every user, all_gather the
+        # shard bounds, band pack + all_to_all to each user's owner, exact
+        # refine of the own user block (nrk.dist.catalog_sharded_owner)
         if ev is not None:
             ev[0].record()
         u_loc = ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"][ulo:uhi], wl["hist"][ulo:uhi],
@@ -747,10 +907,10 @@ def main(argv=None):
         u = gather_users(u_loc, U)
         if ev is not None:
             ev[1].record()
-        res = catalog_sharded_topk(u, shard, K)
+        mark = None if ev is None else (lambda ph: ev[2 if ph == "screen" else 3].record())
+        res = catalog_sharded_owner(u, shard, K, mark=mark)
         if ev is not None:
-            ev[2].record()
-            ev[3].record()
+            ev[4].record()
         return res
 
     def step(ev=None):
@@ -768,12 +928,13 @@ def main(argv=None):
         ops.ip_topk_finish(u, cat, K, ws, out_s, out_r)
         if ev is not None:
             ev[3].record()
+            ev[4].record()
         return u
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -792,36 +953,50 @@ def main(argv=None):
     tower_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     screen_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     finish_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    refine_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
     pairs = U * args.topk * (1 if catalog_mode else world)
     value = pairs / (elapsed / args.steps)
 
-    flops = 2.0 * U * cat.n * D
+    # catalog mode: this rank's screen covers its own item blocks
+    n_scr = (min(I, bhi * 32) - blo * 32) if catalog_mode else cat.n
+    flops = 2.0 * U * n_scr * D
     achieved = flops / (screen_ms * 1e-3) / 1e12
-    default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and not catalog_mode
-    traffic = pmc_traffic(["nrk::ip_screen_kernel<32,"], default_cfg)
+    default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and world == 1
+    traffic = pmc_traffic(["nrk::ip_scan_kernel<"], default_cfg)
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                 "traffic": round(traffic) if traffic else None,
-                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r02e_traffic.json)",
-                "kernel": "ip_screen_kernel<32> (fp16 MFMA 32x32x16)", "kernel_ms": round(screen_ms, 4),
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r03_traffic.json; "
+                                "null when absent or measured on other kernel sources)",
+                "kernel": ("ip_scan_kernel (fp16 MFMA 32x32x16 screen) + ip_select + bound all_gather, this "
+                           "rank's item blocks" if catalog_mode else
+                           "ip_scan_kernel (fp16 MFMA 32x32x16 screen) + ip_select_kernel"),
+                "kernel_ms": round(screen_ms, 4),
                 "algorithmic_flop_per_launch": flops,
-                "busy": pmc_busy(["nrk::ip_screen_kernel", "nrk::ip_refine_kernel", "nrk::tt_user_kernel"], default_cfg),
-                "busy_source": "profiles/r02e_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
-                               "SQ_WAIT_ANY, GRBM_GUI_ACTIVE passes; tools/pmc_busy.py)"}
+                "busy": pmc_busy(["nrk::ip_scan_kernel", "nrk::ip_select_kernel", "nrk::ip_refine_kernel",
+                                  "nrk::tt_user_kernel"], default_cfg),
+                "busy_source": "profiles/r03_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
+                               "SQ_WAIT_ANY, GRBM_GUI_ACTIVE passes; tools/pmc_busy.py, calibrated by "
+                               "tools/calib)"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
+        threads, why = cpu_share()
         u = step()
         torch.cuda.synchronize()
         v, dt, nu = cpu_baseline_recall(u.cpu().numpy(), item_vec.cpu().numpy(), K,
                                         args.cpu_sample, threads, args.cpu_seconds)
         cpu = {"value": round(v, 1), "unit": "recalled pairs/s", "cores": threads, "kind": "port",
+               "threads_from": why, "per_core": round(v / threads, 1),
                "sample": f"first {nu} of the same {U} users x {I} items, exact fp64 top-{K} scan "
-                         f"(oracle/nrk_oracle.c, the reference's per-user nq=1 shape, {dt:.1f}s)"}
+                         f"(oracle/nrk_oracle.c, the reference's per-user nq=1 shape, OpenMP over users, "
+                         f"{dt:.1f}s)"}
+        torch_threads = torch.get_num_threads()
+        torch.set_num_threads(threads)
         vg, dtg, nug = cpu_baseline_recall_gemm(u.cpu().numpy(), item_vec.cpu().numpy(), K, args.cpu_sample,
                                                 args.cpu_seconds / 2)
-        cpu["variants"] = [{"value": round(vg, 1), "unit": "recalled pairs/s", "cores": torch.get_num_threads(),
+        torch.set_num_threads(torch_threads)
+        cpu["variants"] = [{"value": round(vg, 1), "unit": "recalled pairs/s", "cores": threads,
                             "kind": "port", "sample": f"first {nug} users, batched fp32 GEMM + torch.topk on "
                                                       f"torch-CPU ({dtg:.1f}s; fp32 scores, not exact ties)"}]
         # correctness spot check of the timed outputs against the oracle
@@ -856,13 +1031,19 @@ def main(argv=None):
             "scaling": "strong" if catalog_mode else "weak",
             "vs_baseline": None, "dtype": "fp16",
             "data": "synthetic Tianchi-shaped click log (seeded), random-init YouTubeDNN weights",
-            "config": {"workload": "BASELINE config 2: YouTubeDNN recall (user tower + exact top-31 "
-                                   "IP search), 250k users x 364,047 items, D=32",
-                       "users_per_gpu": U, "items": I, "dim": D, "topk": args.topk,
-                       "parallelism": (f"catalog-sharded x{world} (all_to_all + topk_merge)" if catalog_mode
-                                       else f"users-sharded x{world}" if world > 1 else "single")},
-            "phase_ms": {"tower": round(tower_ms, 4), "screen": round(screen_ms, 4),
-                         "finish": round(finish_ms, 4)},
+            "config": {"workload": (f"BASELINE config 4: YouTubeDNN recall (user tower + exact top-31 IP "
+                                    f"search), {U} users x {I} items, D={D}, catalog sharded {world}-way"
+                                    if catalog_mode else
+                                    "BASELINE config 2: YouTubeDNN recall (user tower + exact top-31 "
+                                    "IP search), 250k users x 364,047 items, D=32"),
+                       "users": U, "items": I, "dim": D, "topk": args.topk,
+                       "parallelism": plan["recall"]["parallelism"],
+                       "din_parallelism": plan["din"]["parallelism"]},
+            "phase_ms": ({"tower_and_gather": round(tower_ms, 4), "screen_and_bound_exchange": round(screen_ms, 4),
+                          "band_pack_and_all_to_all": round(finish_ms, 4), "owner_refine": round(refine_ms, 4)}
+                         if catalog_mode else
+                         {"tower": round(tower_ms, 4), "screen": round(screen_ms, 4),
+                          "finish": round(finish_ms, 4)}),
             "roofline": roofline, "cpu_baseline": cpu, "din": din, "itemcf": itemcf, "plugins": plugins,
             "host": host_info(),
         }

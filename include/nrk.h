@@ -87,7 +87,8 @@ int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* cat
  * lower row; fewer than k items -> rows -1 / scores -FLT_MAX.
  * out_rows are catalog rows + row_offset (global rows of a shard).
  * out_exact (nullable) receives the fp64 scores used for ordering (the
- * merge key for catalog-sharded runs).  k <= 32; dim <= 256. */
+ * merge key for catalog-sharded runs).  1 <= k <= 2048 (the fp16 MFMA screen
+ * path up to k = 128, an exact radix-select path above); dim <= 256. */
 size_t nrk_ip_topk_workspace_bytes(int64_t n_users, int64_t n_items, int dim, int k);
 int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const void* catalog,
                 int64_t n_items, int dim, int k, int64_t row_offset, float* out_scores,
@@ -111,11 +112,12 @@ int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
 
 /* Catalog-sharded runs, between screen and
  * finish:
- *   nrk_ip_topk_bound writes, per user, the m (<= 32) largest exact lower
+ *   nrk_ip_topk_bound (same k as the screen) writes, per user, the m
+ *   (<= 256) largest exact lower
  *   bounds this shard's screen found, descending, fp32 [n_users, m], -inf
  *   padded: each one bounds a distinct item's exact score from below.
  *   After an all_gather of every shard's [n_users, m] block (layout
- *   [n_lists][n_users][m], n_lists * m <= 64), nrk_ip_topk_apply_bound takes
+ *   [n_lists][n_users][m], n_lists * m <= 512), nrk_ip_topk_apply_bound takes
  *   the k-th largest of the user's n_lists * m values -- a lower bound of
  *   the user's k-th exact score over the WHOLE catalog -- and raises the
  *   shard's refine cut to it, so finish rescores only the candidates that
@@ -129,10 +131,37 @@ int nrk_ip_topk_bound(const float* users, int64_t n_users, const void* catalog, 
 int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, int m, int k, void* workspace,
                             size_t workspace_bytes, nrk_stream_t stream);
 
+/* Config 4 (catalog sharded) with owner refine: every rank
+ * holds the SAME packed catalog and fp32 rows (nrk_ip_catalog_build over all
+ * items) and screens only its block range [blk_lo, blk_hi) (32-item blocks;
+ * blk_lo a multiple of 8192 / (64 * pad_dim(dim)), blk_hi too unless it is
+ * the catalog end) for every user; half-block ids stay global.  After the
+ * bound exchange (nrk_ip_topk_bound / _apply_bound), nrk_ip_topk_band_pack
+ * writes each user's band entries at or above its cut, compacted to
+ * out_ent[u * band_cap + j] (8-B entries: scaled fp16 max, global half-block
+ * id), out_cnt[u] (-1: the user overflowed -> exact path on the owner);
+ * band_cap = nrk_ip_topk_band_cap(k).  The entries of each user block go to
+ * its owner (all_to_all), which runs nrk_ip_topk_refine_csr over its users:
+ * band_off [n_users + 1] CSR offsets into band (all shards' entries), ucut
+ * [n_users, 2] (cut, eps: the owner's own workspace values after
+ * apply_bound), ovf_in [n_users] (1 = exact fallback over the full catalog).
+ * Output = the final top-k (no merge).  New: no reference counterpart. */
+int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
+                             int dim, int k, int64_t blk_lo, int64_t blk_hi, void* workspace,
+                             size_t workspace_bytes, nrk_stream_t stream);
+int nrk_ip_topk_band_cap(int k);
+int nrk_ip_topk_band_pack(int64_t n_users, int64_t n_items, int dim, int k, const void* workspace,
+                          size_t workspace_bytes, void* out_ent, int32_t* out_cnt, nrk_stream_t stream);
+int nrk_ip_topk_refine_csr(const float* users, int64_t n_users, const float* items, const void* catalog,
+                           int64_t n_items, int dim, int k, int64_t row_offset, const int64_t* band_off,
+                           const void* band, const float* ucut, const int32_t* ovf_in, float* out_scores,
+                           int32_t* out_rows, double* out_exact, void* workspace, size_t workspace_bytes,
+                           nrk_stream_t stream);
+
 /* Merge n_lists per-shard top-k_in lists (fp64 exact scores + global rows,
  * list l of user u at [l * list_stride + u * k_in]) into the top-k_out by
  * (score desc, row asc).  New: the catalog-sharded multi-GPU merge
- * (SURVEY.md §8e); n_lists * k_in <= 512. */
+ * (SURVEY.md §8e); n_lists * k_in <= 1024. */
 int nrk_topk_merge(const double* in_exact, const int32_t* in_rows, int n_lists,
                    int64_t list_stride, int64_t n_users, int k_in, int k_out, float* out_scores,
                    int32_t* out_rows, double* out_exact, nrk_stream_t stream);

@@ -203,7 +203,7 @@ template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true
 __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
     int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
-    float4* __restrict__ uinfo) {
+    float4* __restrict__ uinfo, int tile_lo, int tile_hi) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
     constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : 8192 / BLOCK_BYTES;
@@ -219,7 +219,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     const int ubase = blockIdx.x * (NW * 32 * UG) + wave * (32 * UG);
 
     const int nblk = (n_items + 31) >> 5;
-    const int ntile = (nblk + TB - 1) / TB;
+    // tiles [tile_lo, tile_hi) of the catalog (a catalog shard of config 4
+    // screens its own range of the shared packed catalog; one GPU: all)
+    const int ntile = tile_hi;
     const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk * BLOCK_BYTES);
     const float vmax = hdr->max_norm, sv_scale = hdr->scale, dvmax = hdr->max_dnorm;
     const int jk = (k + 1) / 2 - 1;  // list position whose pair-min bounds the k-th: 2 (jk + 1) >= k
@@ -506,8 +508,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         else tile(tt, afr, std::true_type{}, ig_c);
     };
 #pragma unroll
-    for (int p = 0; p < NSL - 1; ++p) issue_tile(p);
-    for (int tt = 0; tt < ntile; ++tt) step(tt, 0);
+    for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p);
+    for (int tt = tile_lo; tt < ntile; ++tt) step(tt, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
 
 #pragma unroll
@@ -659,16 +661,20 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
     const uint2* __restrict__ cand, int bandcap, const int32_t* __restrict__ cand_cnt,
     const float2* __restrict__ ucut, const int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
     int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
-    double* __restrict__ out_e) {
+    double* __restrict__ out_e, const int64_t* __restrict__ band_off = nullptr) {
     constexpr int SE = SV / WAVE;
     __shared__ Cand surv[4][SV];
     __shared__ int32_t krow[DS4 > 0 ? 4 : 1][DS4 > 0 ? IP_KRING : 1];
     constexpr int RS = DS4 + 1;  // staged row stride in float4 (one float4 of padding)
     __shared__ float4 stage[DS4 > 0 ? 4 : 1][DS4 > 0 ? 64 * RS : 1];
-    __shared__ uint32_t bandq[4][SV + 32];
+    __shared__ uint32_t bandq[4][SV + 32 > IP_BQ ? SV + 32 : IP_BQ];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users || ovf_flag[u]) return;
+    if (band_off && band_off[u + 1] - band_off[u] > IP_BQ) {  // more than the LDS holds: exact path
+        if ((threadIdx.x & 63) == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
+        return;
+    }
     const float* uv = users + u * dim;
     // zero user: every score is exactly 0 -> the lowest rows win the ties
     float nz = 0.0f;
@@ -683,8 +689,10 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         }
         return;
     }
-    const int nbd = cand_cnt[u];
-    const uint2* bd = cand + (size_t)u * bandcap;
+    // band: per-user slots of the select (band_off == nullptr) or a CSR of
+    // the entries every catalog shard sent for this user (config 4 owner)
+    const int nbd = band_off ? (int)(band_off[u + 1] - band_off[u]) : cand_cnt[u];
+    const uint2* bd = band_off ? cand + band_off[u] : cand + (size_t)u * bandcap;
     const float2 ce = ucut[u];
     double thr = -INFINITY;
     if (ce.x != -INFINITY) {
@@ -1148,6 +1156,54 @@ __global__ __launch_bounds__(256) void ip_apply_bound_kernel(float2* __restrict_
     }
 }
 
+// ------------------------------------------------ config-4 band exchange --
+// After the screen (+ nrk_ip_topk_apply_bound): per user the band entries
+// at or above the user's (raised) cut, compacted to out_ent[u * bandcap + j],
+// j < out_cnt[u]; out_cnt[u] = -1 when the user overflowed (the owner then
+// runs the exact fallback).  Entries keep the screen's scaled fp16 max and
+// the GLOBAL half-block id (every shard screens a range of one packed
+// catalog, so the scale is common).
+__global__ __launch_bounds__(256) void ip_band_pack_kernel(int64_t n_users, int bandcap, const uint2* __restrict__ cand,
+                                                           const int32_t* __restrict__ cand_cnt,
+                                                           const float2* __restrict__ ucut,
+                                                           const float4* __restrict__ uinfo,
+                                                           const int32_t* __restrict__ ovf_flag,
+                                                           uint2* __restrict__ out_ent, int32_t* __restrict__ out_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (u >= n_users) return;
+    if (ovf_flag[u]) {
+        if (lane == 0) out_cnt[u] = -1;
+        return;
+    }
+    const int n = cand_cnt[u];
+    const float2 ce = ucut[u];
+    const float cs = ce.x == -INFINITY ? -INFINITY : ce.x * uinfo[u].z;  // exact power-of-two rescale
+    int c = 0;
+    for (int b0 = 0; b0 < n; b0 += WAVE) {
+        const int e = b0 + lane;
+        uint2 ent = make_uint2(0u, 0u);
+        if (e < n) ent = cand[(size_t)u * bandcap + e];
+        const bool kp = e < n && !(__uint_as_float(ent.x) < cs);
+        const unsigned long long bal = __ballot(kp);
+        if (kp) out_ent[(size_t)u * bandcap + c + __popcll(bal & ((1ull << lane) - 1ull))] = ent;
+        c += __popcll(bal);
+    }
+    if (lane == 0) out_cnt[u] = c;
+}
+
+// owner side: users flagged for the exact path -> the fallback's list
+__global__ void ip_ovf_collect_kernel(int64_t n_users, const int32_t* __restrict__ ovf_in,
+                                      int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
+                                      int32_t* __restrict__ ovf_count) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_users;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        const int f = ovf_in ? ovf_in[u] : 0;
+        ovf_flag[u] = f;
+        if (f) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
+    }
+}
+
 // ------------------------------------------------------------- workspace --
 // [hdr 256 B: ovf_count] [ucut f2] [cand_cnt] [ovf_flag] [ovf_list] [uinfo f4]
 // [acnt 2 per user] [cand: bandcap per user] [app: 2 x m2 per user]
@@ -1163,6 +1219,7 @@ struct IpWs {
     uint2* cand;
     uint2* app;
     int bandcap, m2;
+    int blk_lo, blk_hi;  // block range screened (config-4 shards), set by the caller
     size_t bytes;
 };
 
@@ -1201,6 +1258,8 @@ static IpWs ip_ws_layout(void* base, int64_t n_users, int64_t n_items, int k, in
     IpWs w;
     w.bandcap = ip_bandcap(k);
     w.m2 = ip_m2(n_items, k, dim);
+    w.blk_lo = 0;
+    w.blk_hi = (int)n_blocks_of(n_items);
     uint8_t* p = reinterpret_cast<uint8_t*>(base);
     size_t off = 0;
     w.ovf_count = reinterpret_cast<int32_t*>(p + off);
@@ -1237,8 +1296,11 @@ template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1,
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
     const int per_wg = NW * 32 * UG;
+    constexpr int TB = 64 * DP >= 8192 ? 1 : 8192 / (64 * DP);
+    const int nblk = (n_items + 31) / 32;
+    const int t_lo = w.blk_lo / TB, t_hi = (std::min(w.blk_hi, nblk) + TB - 1) / TB;
     ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP, DBG><<<(n_users + per_wg - 1) / per_wg, NW * 64, 0, s>>>(
-        users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo);
+        users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi);
 }
 
 template <int DP, int MT>
@@ -1338,14 +1400,23 @@ static int ip_check(const float* users, int64_t n_users, const float* items, con
     return NRK_OK;
 }
 
-int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
-                       int dim, int k, void* workspace, size_t workspace_bytes,
-                       nrk_stream_t stream) {
+int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
+                             int dim, int k, int64_t blk_lo, int64_t blk_hi, void* workspace,
+                             size_t workspace_bytes, nrk_stream_t stream) {
     clear_error();
     int rc = ip_check(users, n_users, (const float*)catalog, catalog, n_items, dim, k, workspace,
                       workspace_bytes);
     if (rc != NRK_OK || n_users == 0) return rc;
-    const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
+    IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
+    {
+        const int tb = 64 * pad_dim(dim) >= 8192 ? 1 : 8192 / (64 * pad_dim(dim));
+        NRK_REQUIRE(blk_lo >= 0 && blk_lo <= blk_hi && blk_hi <= n_blocks_of(n_items), "block range out of bounds");
+        NRK_REQUIRE(blk_lo == blk_hi || (blk_lo % tb == 0 && (blk_hi % tb == 0 || blk_hi == n_blocks_of(n_items))),
+                    "block range must start (and end, unless at the catalog end) on a 8-KB tile");
+        w.blk_lo = (int)blk_lo;
+        w.blk_hi = (int)blk_hi;
+        if (blk_hi == blk_lo) n_items = 0;  // empty range: every output row is padding
+    }
     hipStream_t s = as_stream(stream);
     if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
         set_error("nrk_ip_topk_screen: hipMemsetAsync failed");
@@ -1378,6 +1449,13 @@ int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog,
     }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
+}
+
+int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
+                       int dim, int k, void* workspace, size_t workspace_bytes,
+                       nrk_stream_t stream) {
+    return nrk_ip_topk_screen_range(users, n_users, catalog, n_items, dim, k, 0, n_blocks_of(n_items), workspace,
+                                    workspace_bytes, stream);
 }
 
 int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
@@ -1491,6 +1569,72 @@ int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, i
     else if (tot <= 256) NRK_APPLY(4, 256);
     else NRK_APPLY(0, next_pow2(tot));
 #undef NRK_APPLY
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_ip_topk_band_pack(int64_t n_users, int64_t n_items, int dim, int k, const void* workspace,
+                          size_t workspace_bytes, void* out_ent, int32_t* out_cnt, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_users >= 0 && n_items >= 0 && dim > 0 && dim <= 256, "bad sizes");
+    NRK_REQUIRE(k >= 1 && k <= IP_KMAX, "k out of range");
+    if (n_users == 0) return NRK_OK;
+    NRK_REQUIRE(workspace && out_ent && out_cnt, "null pointer");
+    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users, n_items, k, dim).bytes, "workspace too small");
+    const IpWs w = ip_ws_layout(const_cast<void*>(workspace), n_users, n_items, k, dim);
+    ip_band_pack_kernel<<<(int)((n_users + 3) / 4), 256, 0, as_stream(stream)>>>(
+        n_users, w.bandcap, w.cand, w.cnt, w.ucut, w.uinfo, w.ovf_flag, reinterpret_cast<uint2*>(out_ent), out_cnt);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_ip_topk_band_cap(int k) { return k >= 1 && k <= IP_KMAX ? ip_bandcap(k) : 0; }
+
+int nrk_ip_topk_refine_csr(const float* users, int64_t n_users, const float* items, const void* catalog,
+                           int64_t n_items, int dim, int k, int64_t row_offset, const int64_t* band_off,
+                           const void* band, const float* ucut, const int32_t* ovf_in, float* out_scores,
+                           int32_t* out_rows, double* out_exact, void* workspace, size_t workspace_bytes,
+                           nrk_stream_t stream) {
+    clear_error();
+    int rc = ip_check(users, n_users, items, items, n_items, dim, k, workspace, workspace_bytes);
+    if (rc != NRK_OK || n_users == 0) return rc;
+    NRK_REQUIRE(out_scores && out_rows && band_off && ucut, "null pointer");
+    if (k > IP_KFAST) NRK_UNSUPPORTED("the band refine needs k <= 128 (larger k: exact path, ovf_in = 1)");
+    const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
+        set_error("nrk_ip_topk_refine_csr: hipMemsetAsync failed");
+        return NRK_EHIP;
+    }
+    ip_ovf_collect_kernel<<<(int)std::min<int64_t>((n_users + 255) / 256, 4096), 256, 0, s>>>(
+        n_users, ovf_in, w.ovf_flag, w.ovf_list, w.ovf_count);
+    const int g2 = (int)((n_users + 3) / 4);
+    const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
+    const uint2* bd = reinterpret_cast<const uint2*>(band);
+    const float2* uc = reinterpret_cast<const float2*>(ucut);
+#define NRK_REFINE(DS4, SV)                                                                                   \
+    ip_refine_kernel<DS4, SV><<<g2, 256, 0, s>>>(users, n_users, items, cat, n_items, dim, k, row_offset, bd, 0, \
+                                                 nullptr, uc, w.ovf_flag, w.ovf_list, w.ovf_count, out_scores,   \
+                                                 out_rows, out_exact, band_off)
+#define NRK_REFINE_SV(DS4)                 \
+    do {                                   \
+        if (k <= 64) NRK_REFINE(DS4, 128); \
+        else NRK_REFINE(DS4, 256);         \
+    } while (0)
+    if (dim == 32) NRK_REFINE_SV(8);
+    else if (dim == 16) NRK_REFINE_SV(4);
+    else if (dim == 64) NRK_REFINE_SV(16);
+    else NRK_REFINE_SV(0);
+#undef NRK_REFINE_SV
+#undef NRK_REFINE
+    if (n_items > 0) {
+        const int ns = next_pow2(std::max(k, 64));
+        const size_t lds = (size_t)ns * sizeof(Cand);
+        (void)hipFuncSetAttribute((const void*)ip_fallback_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        ip_fallback_kernel<<<(int)std::min<int64_t>(n_users, 256), 256, lds, s>>>(
+            users, items, n_items, dim, k, ns, row_offset, w.ovf_list, w.ovf_count, out_scores, out_rows, out_exact);
+    }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

@@ -3,15 +3,22 @@ torch.distributed over RCCL ("nccl" on ROCm), 127.0.0.1 rendezvous.
 
 * users-sharded  -- every rank scores its own contiguous user block against
   the full (replicated) catalog.  No data-path collective (weak scaling).
-* catalog-sharded (BASELINE config 4) -- rank r holds items [lo_r, hi_r).
-  Each rank runs the user tower for its own user block and all_gathers the
-  vectors (gather_users); every rank then screens ALL users against its
-  shard, the per-user screen bounds are all_reduced (MAX) so every shard
-  refines only candidates above the global k-th-score bound, and an
-  all_to_all of the shard-local top-k (fp64 exact score + int32 global row,
-  12 B per entry) hands each user block's lists to its owner, where
-  nrk_topk_merge orders by (score desc, row asc) -- the same tie-break as a
-  single GPU, so the merged lists are identical to the 1-GPU result.
+* catalog-sharded (BASELINE config 4), owner refine (catalog_sharded_owner,
+  the default) -- every rank holds the whole packed catalog and fp32 rows
+  (69 MB at config 2) and screens only its block range [lo_r, hi_r) for
+  ALL users (gather_users: each rank runs the user tower for its own user
+  block, all_gather).  Two exchanges: an all_gather of every shard's m
+  largest screen bounds per user, whose k-th largest bounds the user's
+  GLOBAL k-th score (nrk_ip_topk_apply_bound raises each shard's cut to
+  it), then an all_to_all of the band entries at or above the cut (8 B
+  each, global half-block ids) to the owner of each user block, which runs
+  the exact refine for its users only (nrk_ip_topk_refine_csr): the refine
+  shrinks 1/N with the screen and no merge is needed.  Same rows and
+  scores as one GPU.
+* catalog-sharded, merge (catalog_sharded_topk, round 2) -- each shard
+  refines every user against its own rows and an all_to_all of the
+  shard-local top-k (fp64 exact + int32 global row) goes to the owner,
+  where nrk_topk_merge orders by (score desc, row asc).
 * users-sharded ItemCF similarity (itemcf_sim_sharded) -- rank r holds the
   click lists of users [lo_r, hi_r) and owns items [ilo_r, ihi_r).  Every
   rank emits the pair tuples (key, GLOBAL slot, weight) of its users; one
@@ -148,6 +155,151 @@ def catalog_sharded_topk(users, shard, k: int, group=None, merge=None, exchange_
     s_, r_, x_ = merge(re.view(world, per, k), rr.view(world, per, k), k)
     lo, hi = shard_range(U, world, rank)
     return s_[: hi - lo], r_[: hi - lo], x_[: hi - lo]
+
+
+class HipRangeShard:
+    """Config 4 with owner refine: the shared catalog (every rank builds the
+    same ops.Catalog over ALL items) and this rank's block range, tile
+    aligned (shard_blocks).  screen / band on this rank's range for every
+    user; refine for the owner's user block."""
+
+    def __init__(self, catalog, blk_lo: int, blk_hi: int, k: int, n_users: int):
+        from . import ops
+
+        self.ops, self.cat, self.k = ops, catalog, int(k)
+        self.blk_lo, self.blk_hi, self.n_users = int(blk_lo), int(blk_hi), int(n_users)
+        self.ws = ops.ip_topk_workspace(n_users, catalog, k, catalog.items.device)
+        self.rws = None
+
+    def screen(self, users, m: int):
+        self.ops.ip_topk_screen_range(users, self.cat, self.k, self.blk_lo, self.blk_hi, self.ws)
+        return self.ops.ip_topk_bound(users, self.cat, self.k, m, self.ws)
+
+    def band(self, bounds=None):
+        if bounds is not None:
+            self.ops.ip_topk_apply_bound(bounds, self.k, self.ws)
+        return self.ops.ip_topk_band_pack(self.n_users, self.cat, self.k, self.ws)
+
+    def ucut(self, lo: int, hi: int):
+        return self.ops.ip_topk_ucut(self.ws, self.n_users)[lo:hi].contiguous()
+
+    def refine(self, users, band_off, band, ucut, ovf):
+        if self.rws is None:
+            self.rws = self.ops.ip_topk_workspace(users.shape[0], self.cat, self.k, users.device)
+        return self.ops.ip_topk_refine_csr(users, self.cat, self.k, band_off, band, ucut, ovf, workspace=self.rws)
+
+
+def shard_blocks(n_items: int, world: int, rank: int, tile_blocks: int):
+    """Block range of rank r: whole screen tiles (tile_blocks 32-item blocks)
+    split contiguously; the last rank ends at the catalog's last block."""
+    nblk = -(-n_items // 32)
+    ntile = -(-nblk // tile_blocks)
+    lo, hi = shard_range(ntile, world, rank)
+    return min(nblk, lo * tile_blocks), min(nblk, hi * tile_blocks)
+
+
+def exchange_bands(cnt, ent, n_users: int, group=None):
+    """The owner exchange: rank r sends, for the users of every owner block
+    shard_range(n_users, world, o), its band entries (cnt [U] int32, -1 =
+    overflowed; ent [U, cap] int64) to owner o.  Returns this rank's users'
+    (band_off int64 [n_own + 1], band int64 [nnz] (sources in rank order per
+    user), ovf int32 [n_own])."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    dev = cnt.device
+    lo, hi = shard_range(n_users, world, rank)
+    n_own = hi - lo
+    c = cnt.to(torch.int64)
+    take = (torch.arange(ent.shape[1], device=dev)[None, :] < c.clamp(min=0)[:, None])
+    if world == 1:
+        band = ent[take]
+        off = torch.zeros(n_users + 1, dtype=torch.int64, device=dev)
+        off[1:] = torch.cumsum(c.clamp(min=0), 0)
+        return off, band, (c < 0).to(torch.int32)
+    per = -(-n_users // world)
+    cpad = torch.full((per * world,), 0, dtype=torch.int64, device=dev)
+    cpad[:n_users] = c
+    rc = torch.empty_like(cpad)
+    dist.all_to_all_single(rc, cpad, group=group)  # block s = source s's counts for my users
+    rc = rc.view(world, per)[:, :n_own]
+    flat = ent[take]  # user-major, so each owner's entries are one contiguous run
+    send = torch.stack([c.clamp(min=0)[slice(*shard_range(n_users, world, o))].sum() for o in range(world)])
+    recv = rc.clamp(min=0).sum(1)
+    sc, rcv = send.tolist(), recv.tolist()
+    buf = torch.empty(int(sum(rcv)), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(buf, flat.contiguous(), rcv, sc, group=group)
+    # regroup by user (stable: sources stay in rank order inside a user)
+    who = torch.repeat_interleave(torch.arange(n_own, device=dev).repeat(world), rc.clamp(min=0).reshape(-1))
+    order = torch.sort(who, stable=True).indices
+    band = buf[order]
+    per_user = rc.clamp(min=0).sum(0)
+    off = torch.zeros(n_own + 1, dtype=torch.int64, device=dev)
+    off[1:] = torch.cumsum(per_user, 0)
+    ovf = (rc < 0).any(0).to(torch.int32)
+    return off, band, ovf
+
+
+def catalog_sharded_owner(users, shard, k: int, group=None, exchange_bound: bool = True, mark=None):
+    """Config 4, owner refine (see the module docstring): ``users`` [U, D]
+    on every rank, ``shard`` a HipRangeShard (or a stand-in with screen /
+    band / ucut / refine in the gloo tests).  Returns (scores f32, rows i32,
+    exact f64) of THIS rank's user block shard_range(U, world, rank).
+    ``mark(phase)``, if given, is called after the screen + bound exchange
+    ("screen") and after the band pack + all_to_all ("exchange") -- bench.py
+    records HIP events there."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    U = users.shape[0]
+    m = bound_width(k, world) if exchange_bound else 0
+    b = shard.screen(users, max(m, 1))
+    bounds = None
+    if m:
+        bounds = torch.empty((world * b.shape[0], b.shape[1]), dtype=b.dtype, device=b.device)
+        dist.all_gather_into_tensor(bounds, b.contiguous(), group=group)
+        bounds = bounds.view(world, b.shape[0], b.shape[1])
+    if mark is not None:
+        mark("screen")
+    cnt, ent = shard.band(bounds)
+    off, band, ovf = exchange_bands(cnt, ent, U, group)
+    if mark is not None:
+        mark("exchange")
+    lo, hi = shard_range(U, world, rank)
+    return shard.refine(users[lo:hi].contiguous(), off, band, shard.ucut(lo, hi), ovf)
+
+
+def owner_replay(users, shards, k: int, timer=None):
+    """One-process replay of catalog_sharded_owner over ``shards`` (one
+    HipRangeShard per emulated rank, all on this device): the two exchanges
+    become stacks / concatenations.  ``timer(phase, rank, fn)`` may wrap each
+    rank's steps (tools/catalog_replay.py times them).  Returns the full
+    (scores f32 [U, k], rows i32 [U, k], exact f64 [U, k])."""
+    run = timer or (lambda phase, r, fn: fn())
+    world = len(shards)
+    U = users.shape[0]
+    m = bound_width(k, world)
+    bs = [run("screen", r, lambda sh=sh: sh.screen(users, max(m, 1))) for r, sh in enumerate(shards)]
+    bounds = torch.stack(bs).contiguous() if m else None
+    packs = [run("band", r, lambda sh=sh: sh.band(bounds)) for r, sh in enumerate(shards)]
+    outs = []
+    for o in range(world):
+        lo, hi = shard_range(U, world, o)
+        n_own = hi - lo
+        cnts = torch.stack([c[lo:hi].to(torch.int64) for c, _ in packs])  # [world, n_own]
+        parts, whos = [], []
+        for src, (c, ent) in enumerate(packs):
+            cc = c[lo:hi].to(torch.int64).clamp(min=0)
+            take = torch.arange(ent.shape[1], device=ent.device)[None, :] < cc[:, None]
+            parts.append(ent[lo:hi][take])
+            whos.append(torch.repeat_interleave(torch.arange(n_own, device=ent.device), cc))
+        order = torch.sort(torch.cat(whos), stable=True).indices
+        band = torch.cat(parts)[order].contiguous()
+        off = torch.zeros(n_own + 1, dtype=torch.int64, device=users.device)
+        off[1:] = torch.cumsum(cnts.clamp(min=0).sum(0), 0)
+        ovf = (cnts < 0).any(0).to(torch.int32)
+        sh = shards[o]
+        outs.append(run("refine", o, lambda sh=sh, lo=lo, hi=hi, off=off, band=band, ovf=ovf: sh.refine(
+            users[lo:hi].contiguous(), off, band, sh.ucut(lo, hi), ovf)))
+    return tuple(torch.cat([x[i] for x in outs]) for i in range(3))
 
 
 def _default_pairs(offsets, items, ts, created, n_items, slot_base):

@@ -165,6 +165,97 @@ int64_t oracle_itemcf_sim(int64_t n_users, const int64_t* offsets, const int32_t
     return n_slots;
 }
 
+/* The same similarity on T OpenMP threads (a CPU baseline variant for
+ * bench.py's ItemCF leg, not a checker).  Thread t owns the rows i with
+ * i % T == t: it walks every user list in order but only accumulates the
+ * pairs of its own rows, so each (i, j) sum sees its terms in the sequential
+ * order and the values are bit-identical to oracle_itemcf_sim's.  Thread t
+ * writes its entries (its own first-insertion order) to
+ * out[base[t] .. base[t] + n[t]); base[t] is the prefix of the per-thread
+ * pair counts (an upper bound on its distinct pairs).  The caller sizes the
+ * outputs for sum(L^2) entries.  Returns the total number of entries. */
+int64_t oracle_itemcf_sim_omp(int64_t n_users, const int64_t* offsets, const int32_t* items,
+                              const int64_t* ts, const double* created, int32_t n_items,
+                              double loc_alpha, double loc_alpha_rev, double loc_beta,
+                              double time_alpha, double created_alpha, int nthreads,
+                              int32_t* out_i, int32_t* out_j, double* out_v, int64_t* base,
+                              int64_t* n_out) {
+    int T = nthreads > 0 ? nthreads : 1;
+    int64_t* cnt = (int64_t*)calloc((size_t)n_items, sizeof(int64_t));
+    int64_t* need = (int64_t*)calloc((size_t)T, sizeof(int64_t));
+    for (int64_t u = 0; u < n_users; ++u) {
+        const int64_t b = offsets[u], L = offsets[u + 1] - b;
+        for (int64_t l = 0; l < L; ++l) {
+            cnt[items[b + l]] += 1;
+            need[items[b + l] % T] += L;
+        }
+    }
+    int64_t acc = 0;
+    for (int t = 0; t < T; ++t) {
+        base[t] = acc;
+        acc += need[t];
+    }
+#ifdef _OPENMP
+#pragma omp parallel num_threads(T)
+#endif
+    {
+#ifdef _OPENMP
+        const int t = omp_get_thread_num();
+#else
+        const int t = 0;
+#endif
+        int64_t cap = 1;
+        while (cap < 2 * need[t] + 16) cap <<= 1;
+        hent_t* tab = (hent_t*)malloc(sizeof(hent_t) * (size_t)cap);
+        for (int64_t h = 0; h < cap; ++h) tab[h].slot = -1;
+        int32_t* oi = out_i + base[t];
+        int32_t* oj = out_j + base[t];
+        double* ov = out_v + base[t];
+        int64_t n = 0;
+        for (int64_t u = 0; u < n_users; ++u) {
+            const int64_t b = offsets[u], L = offsets[u + 1] - offsets[u];
+            const double user_penalty = 1.0 / log((double)(L + 1));
+            for (int64_t l1 = 0; l1 < L; ++l1) {
+                const int32_t i = items[b + l1];
+                if (i % T != t) continue;
+                const int64_t ti = ts[b + l1];
+                for (int64_t l2 = 0; l2 < L; ++l2) {
+                    const int32_t j = items[b + l2];
+                    if (i == j) continue;
+                    const int64_t tj = ts[b + l2];
+                    const double la = (l2 > l1) ? loc_alpha : loc_alpha_rev;
+                    const int64_t dl = (l2 > l1 ? l2 - l1 : l1 - l2) - 1;
+                    const double loc_weight = la * pow(loc_beta, (double)dl);
+                    const int64_t dt = ti > tj ? ti - tj : tj - ti;
+                    const double click_w = exp(pow(time_alpha, (double)dt));
+                    const double created_w = exp(pow(created_alpha, fabs(created[i] - created[j])));
+                    const double w = loc_weight * click_w * created_w * user_penalty;
+                    const uint64_t key = ((uint64_t)(uint32_t)i << 32) | (uint32_t)j;
+                    uint64_t h = mix64(key) & (uint64_t)(cap - 1);
+                    while (tab[h].slot >= 0 && tab[h].key != key) h = (h + 1) & (uint64_t)(cap - 1);
+                    if (tab[h].slot < 0) {
+                        tab[h].key = key;
+                        tab[h].slot = n;
+                        oi[n] = i;
+                        oj[n] = j;
+                        ov[n] = 0.0;
+                        ++n;
+                    }
+                    ov[tab[h].slot] += w;
+                }
+            }
+        }
+        for (int64_t s = 0; s < n; ++s) ov[s] = ov[s] / sqrt((double)(cnt[oi[s]] * cnt[oj[s]]));
+        n_out[t] = n;
+        free(tab);
+    }
+    int64_t tot = 0;
+    for (int t = 0; t < T; ++t) tot += n_out[t];
+    free(cnt);
+    free(need);
+    return tot;
+}
+
 /* ------------------------------------------------------------------------ */
 /* A9: ItemCFRecaller._precompute_topk_similar_items, itemcf_recaller.py     */
 /* :41-54: per row, stable sort by score desc (ties keep insertion order),    */

@@ -53,6 +53,9 @@ def lib():
         L.oracle_ip_topk.restype = None
         L.oracle_itemcf_sim.argtypes = [i64, P, P, P, P, i32, f64, f64, f64, f64, f64, i64, P, P, P, P, P]
         L.oracle_itemcf_sim.restype = i64
+        L.oracle_itemcf_sim_omp.argtypes = [i64, P, P, P, P, i32, f64, f64, f64, f64, f64, ctypes.c_int, P, P, P,
+                                            P, P]
+        L.oracle_itemcf_sim_omp.restype = i64
         L.oracle_topn_rows.argtypes = [i64, P, P, P, ctypes.c_int, P, P, P]
         L.oracle_topn_rows.restype = None
         L.oracle_itemcf_recall.argtypes = [i64, P, P, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int,
@@ -189,6 +192,57 @@ def itemcf_sim(offsets, items, ts, created, n_items):
                                 CREATED_ALPHA, cap, _p(oi), _p(oj), _p(ov), _p(rank), _p(cnt))
     assert n >= 0
     return oi[:n], oj[:n], ov[:n], rank, cnt
+
+
+def itemcf_sim_omp(offsets, items, ts, created, n_items, nthreads):
+    """oracle_itemcf_sim on ``nthreads`` OpenMP threads (rows partitioned by
+    i % T; bit-identical values, per-thread first-insertion order).  A CPU
+    baseline variant (bench.py ItemCF leg), not a checker.  Returns (i, j, v)."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    items = np.ascontiguousarray(items, np.int32)
+    ts = np.ascontiguousarray(ts, np.int64)
+    created = np.ascontiguousarray(created, np.float64)
+    L = np.diff(offsets)
+    cap = int((L * L).sum()) + 1
+    oi = np.empty(cap, np.int32)
+    oj = np.empty(cap, np.int32)
+    ov = np.empty(cap, np.float64)
+    base = np.zeros(nthreads, np.int64)
+    n = np.zeros(nthreads, np.int64)
+    lib().oracle_itemcf_sim_omp(len(offsets) - 1, _p(offsets), _p(items), _p(ts), _p(created), n_items,
+                                LOC_ALPHA, LOC_ALPHA_REV, LOC_BETA, TIME_ALPHA, CREATED_ALPHA, int(nthreads),
+                                _p(oi), _p(oj), _p(ov), _p(base), _p(n))
+    take = np.concatenate([np.arange(b, b + c) for b, c in zip(base, n)]) if nthreads else np.zeros(0, np.int64)
+    return oi[take], oj[take], ov[take]
+
+
+def itemcf_sim_pyloop(user_item_time, created):
+    """item_cf.py:33-84 as the reference writes it: Python dict loops over
+    ``user_item_time`` ({user: [(item, time), ...]}) with WeightCalculator's
+    np.exp / np.abs / math.log (weights.py:7-60) per pair.  A CPU baseline
+    variant (the reference's own per-pair cost), not a checker.  Returns
+    {i: {j: sim}}."""
+    import math
+
+    i2i, cnt = {}, {}
+    for _, lst in user_item_time.items():
+        for loc1, (i, ti) in enumerate(lst):
+            cnt[i] = cnt.get(i, 0) + 1
+            i2i.setdefault(i, {})
+            for loc2, (j, tj) in enumerate(lst):
+                if i == j:
+                    continue
+                la = LOC_ALPHA if loc2 > loc1 else LOC_ALPHA_REV
+                loc_w = la * (LOC_BETA ** (np.abs(loc2 - loc1) - 1))
+                click_w = np.exp(TIME_ALPHA ** np.abs(ti - tj))
+                created_w = np.exp(CREATED_ALPHA ** np.abs(created[i] - created[j]))
+                pen = 1.0 / math.log(len(lst) + 1)
+                i2i[i].setdefault(j, 0)
+                i2i[i][j] += loc_w * click_w * created_w * pen
+    for i, row in i2i.items():
+        for j, w in row.items():
+            row[j] = w / math.sqrt(cnt[i] * cnt[j])
+    return i2i
 
 
 def sim_to_rows(i, j, v, n_items):

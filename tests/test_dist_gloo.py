@@ -120,6 +120,124 @@ def test_catalog_sharded_matches_single(U, I, k):
         assert sum(g[5] for g in got) > 0
 
 
+class _OwnerShard:
+    """CPU stand-in for nrk.dist.HipRangeShard (config 4, owner refine):
+    bounds = the range's m largest exact scores minus a margin; band = the
+    range's rows with exact >= (k-th largest of every shard's bounds) -
+    margin, as int64 entries (the stand-in's own row encoding); the owner's
+    refine = exact top-k over the received rows ((score desc, row asc)),
+    the whole catalog for users flagged overflowed (one user is forced)."""
+
+    def __init__(self, items, lo, hi, k, force_ovf=None):
+        self.items, self.lo, self.hi, self.k, self.force = items, lo, hi, k, force_ovf
+
+    def screen(self, users, m):
+        self.users = users.double().numpy()
+        sc = self.users @ self.items[self.lo:self.hi].astype(np.float64).T
+        top = -np.sort(-sc, axis=1)[:, :m] - 1e-9
+        if top.shape[1] < m:
+            top = np.concatenate([top, np.full((len(top), m - top.shape[1]), -np.inf)], 1)
+        return torch.from_numpy(top.astype(np.float32) - np.float32(1e-6))
+
+    def band(self, bounds):
+        U = self.users.shape[0]
+        g = np.full(U, -np.inf)
+        if bounds is not None:
+            L, _, m = bounds.shape
+            vals = bounds.permute(1, 0, 2).reshape(U, L * m).double().numpy()
+            if L * m >= self.k:
+                g = -np.sort(-vals, axis=1)[:, self.k - 1]
+        sc = self.users @ self.items[self.lo:self.hi].astype(np.float64).T
+        keep = sc >= (g[:, None] - 1e-6)
+        cnt = keep.sum(1)
+        cap = max(1, int(cnt.max(initial=0)))
+        ent = np.zeros((U, cap), np.int64)
+        for u in range(U):
+            rows = np.nonzero(keep[u])[0] + self.lo
+            ent[u, :len(rows)] = rows
+        cnt = cnt.astype(np.int32)
+        if self.force is not None:
+            cnt[self.force] = -1
+        self.g = g
+        return torch.from_numpy(cnt), torch.from_numpy(ent)
+
+    def ucut(self, lo, hi):
+        return torch.from_numpy(np.stack([self.g[lo:hi], np.zeros(hi - lo)], 1).astype(np.float32))
+
+    def refine(self, users, off, band, ucut, ovf):
+        u = users.double().numpy()
+        off, band, ovf = off.numpy(), band.numpy(), ovf.numpy()
+        n, k = len(u), self.k
+        s = np.full((n, k), -np.finfo(np.float32).max, np.float32)
+        r = np.full((n, k), -1, np.int32)
+        e = np.full((n, k), -np.inf)
+        for i in range(n):
+            rows = np.arange(len(self.items)) if ovf[i] else np.unique(band[off[i]:off[i + 1]])
+            sc = (u[i] @ self.items[rows].astype(np.float64).T) if len(rows) else np.zeros(0)
+            order = np.lexsort((rows, -sc))[:k]
+            m = len(order)
+            r[i, :m], e[i, :m], s[i, :m] = rows[order], sc[order], sc[order].astype(np.float32)
+        return torch.from_numpy(s), torch.from_numpy(r), torch.from_numpy(e)
+
+
+def _owner_worker(rank, world, port, U, I, D, k, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nrk.dist import catalog_sharded_owner, shard_range
+
+        rng = np.random.default_rng(11)
+        users = rng.standard_normal((U, D)).astype(np.float32)
+        items = rng.standard_normal((I, D)).astype(np.float32)
+        items[I // 2 + 1] = items[3]  # cross-shard exact tie -> lower row must win
+        lo, hi = shard_range(I, world, rank)
+        shard = _OwnerShard(items, lo, hi, k, force_ovf=2 if rank == world - 1 else None)
+        s, r, e = catalog_sharded_owner(torch.from_numpy(users), shard, k)
+        ulo, uhi = shard_range(U, world, rank)
+        q.put((rank, ulo, uhi, s.numpy(), r.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,U,I,k", [(2, 37, 101, 31), (3, 50, 400, 8), (2, 64, 40, 31), (3, 5, 7, 10)])
+def test_catalog_sharded_owner_refine_matches_single(world, U, I, k):
+    """Config 4 with owner refine: bound all_gather, band all_to_all (CSR
+    regrouping by user, sources in rank order), overflowed users on the exact
+    path -- the merged result equals one GPU's."""
+    from oracle import oracle
+
+    D = 16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, U, I, D, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(11)
+    users = rng.standard_normal((U, D)).astype(np.float32)
+    items = rng.standard_normal((I, D)).astype(np.float32)
+    items[I // 2 + 1] = items[3]
+    so, ro = oracle.ip_topk(users, items, k)
+    for rank, ulo, uhi, s, r in got:
+        assert np.array_equal(r, ro[ulo:uhi]), rank
+        assert np.array_equal(s, so[ulo:uhi]), rank
+
+
+def test_shard_blocks_tile_aligned():
+    from nrk.dist import shard_blocks
+
+    for n in (1, 5000, 364_047):
+        for w in (1, 2, 3, 8):
+            spans = [shard_blocks(n, w, r, 4) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == -(-n // 32)
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert all(a[0] % 4 == 0 for a in spans if a[1] > a[0])  # empty tail ranges sit at the end
+
+
 def test_shard_range_covers():
     from nrk.dist import shard_range
 

@@ -328,6 +328,51 @@ def test_catalog_shards_bound_full_size(ops):
     assert np.array_equal(s[sample].cpu().numpy(), so)
 
 
+@pytest.mark.parametrize("n_shards,k", [(2, 31), (3, 31), (8, 31), (8, 61), (4, 10)])
+def test_catalog_owner_refine_equals_single(ops, n_shards, k):
+    """Config 4, owner refine (nrk.dist.owner_replay: the two exchanges
+    in-process): every rank screens its tile range of the shared catalog,
+    bands above the global bound go to each user block's owner, which
+    refines its users -- rows and scores identical to one GPU, incl. a
+    cross-shard exact tie, a zero user and the tie-stress overflow path."""
+    from nrk.dist import HipRangeShard, owner_replay, shard_blocks
+
+    rng = np.random.default_rng(n_shards * 100 + k)
+    users = _unit(rng.standard_normal((300, 32)))
+    users[7] = 0.0
+    items = _unit(rng.standard_normal((20000, 32)))
+    items[19990] = items[10]
+    items[5000:5600] = items[100]  # dense exact duplicates -> overflowed users take the exact path
+    users[9] = items[100]
+    so, ro = oracle.ip_topk(users, items, k)
+    cat = ops.Catalog(_dev(items))
+    tb = ops.ip_topk_tile_blocks(32)
+    shards = [HipRangeShard(cat, *shard_blocks(len(items), n_shards, r, tb), k, len(users)) for r in range(n_shards)]
+    s, r, e = owner_replay(_dev(users), shards, k)
+    assert np.array_equal(r.cpu().numpy(), ro)
+    assert np.array_equal(s.cpu().numpy(), so)
+
+
+def test_catalog_owner_refine_full_size(ops):
+    """The 8-shard owner replay at config 2's catalog (364,047 x 32): rows and
+    scores bit-exact vs the oracle on a user sample."""
+    from nrk.dist import HipRangeShard, owner_replay, shard_blocks
+
+    U, I, D, K, N = 4096, 364_047, 32, 31, 8
+    g = torch.Generator(device="cuda").manual_seed(5)
+    users = torch.nn.functional.normalize(torch.randn(U, D, device="cuda", generator=g), dim=1).contiguous()
+    items = torch.nn.functional.normalize(torch.randn(I, D, device="cuda", generator=g), dim=1).contiguous()
+    cat = ops.Catalog(items)
+    tb = ops.ip_topk_tile_blocks(D)
+    shards = [HipRangeShard(cat, *shard_blocks(I, N, r, tb), K, U) for r in range(N)]
+    s, r, e = owner_replay(users, shards, K)
+    torch.cuda.synchronize()
+    sample = np.arange(0, U, 16)
+    so, ro = oracle.ip_topk(users[sample].cpu().numpy(), items.cpu().numpy(), K, nthreads=8)
+    assert np.array_equal(r[sample].cpu().numpy().astype(np.int64), ro)
+    assert np.array_equal(s[sample].cpu().numpy(), so)
+
+
 @pytest.mark.parametrize("d", [16, 32, 64])
 def test_screen_eps_bounds_the_fp16_rounding(ops, d):
     """The screen's per-user error bound (ucut.y, ip_topk.hip ip_screen_kernel:

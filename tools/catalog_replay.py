@@ -1,13 +1,17 @@
-"""One-GPU replay of the catalog-sharded recall (BASELINE config 4) (dev tool).
+"""One-GPU replay of the catalog-sharded recall (BASELINE config 4) with the
+owner refine (nrk.dist.owner_replay) (dev tool).
 
-Times, for 250k users x 364,047 items (D = 32, k = 31): the unsharded screen
-and refine, then each of N shards' screen, refine without the bound exchange
-and refine with it (the all_reduce(MAX) replayed as a max over the shards'
-bounds), and checks the merged result against the unsharded one.
-usage: python tools/catalog_replay.py [N]
+For 250k users x 364,047 items (D = 32, k = 31): the unsharded screen +
+finish, then N emulated ranks on one GPU.  Per rank: the screen of its tile
+range for every user (+ the bound), the band pack after the bound exchange,
+and the owner refine of its user block -- HIP events around each rank's own
+kernels, so "per rank" = what one GPU of an N-GPU node would run (the
+collectives are not in these numbers).  Checks the result against the
+unsharded rows.  usage: python tools/catalog_replay.py [N]
 """
 import os
 import sys
+from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(REPO, "news-recommendation-tc_amd"), REPO):
@@ -16,19 +20,7 @@ for p in (os.path.join(REPO, "news-recommendation-tc_amd"), REPO):
 import torch  # noqa: E402
 
 from nrk import ops  # noqa: E402
-from nrk.dist import HipShard, bound_width, shard_range  # noqa: E402
-
-
-def timed(fn, reps=5):
-    fn()
-    torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
-        out = fn()
-    b.record()
-    torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps, out
+from nrk.dist import HipRangeShard, owner_replay, shard_blocks  # noqa: E402
 
 
 def main():
@@ -37,35 +29,50 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(23)
     users = torch.nn.functional.normalize(torch.relu(torch.randn(U, D, device="cuda", generator=g)), dim=1).contiguous()
     items = torch.nn.functional.normalize(torch.randn(I, D, device="cuda", generator=g), dim=1).contiguous()
-    full = HipShard(ops.Catalog(items), 0, K, U)
-    t_scr, _ = timed(lambda: full.screen(users, 1))
-    t_ref, (e1, r1) = timed(lambda: full.finish(users))
-    r1 = r1.clone()
-    print(f"unsharded: screen {t_scr:.3f} ms, refine {t_ref:.3f} ms")
-    shards = [HipShard(ops.Catalog(items[lo:hi].contiguous()), lo, K, U)
-              for lo, hi in (shard_range(I, N, r) for r in range(N))]
-    m = bound_width(K, N)
-    rows = []
-    for i, sh in enumerate(shards):
-        ts, b = timed(lambda: sh.screen(users, m))
-        tr0, _ = timed(lambda: sh.finish(users))
-        rows.append((ts, tr0, b.clone()))
-    gb = torch.stack([r[2] for r in rows]).contiguous()
-    lists = []
-    for i, sh in enumerate(shards):
-        def both():
-            sh.screen(users, m)
-            return sh.finish(users, gb)
-        tsb, out = timed(both)
-        lists.append((out[0].clone(), out[1].clone()))
-        ts, tr0, _ = rows[i]
-        kept = int((out[1] >= 0).sum())
-        print(f"shard {i}: screen {ts:.3f} ms, refine {tr0:.3f} ms (own bound) / {tsb - ts:.3f} ms (global bound), "
-              f"kept entries {kept / U:.2f} per user")
-    s, r, e = ops.topk_merge(torch.stack([x[0] for x in lists]).contiguous(),
-                             torch.stack([x[1] for x in lists]).contiguous(), K)
+    cat = ops.Catalog(items)
+    ws = ops.ip_topk_workspace(U, cat, K, "cuda")
+    s1 = torch.empty((U, K), dtype=torch.float32, device="cuda")
+    r1 = torch.empty((U, K), dtype=torch.int32, device="cuda")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for rep in range(3):
+        ev[0].record()
+        ops.ip_topk_screen(users, cat, K, ws)
+        ev[1].record()
+        ops.ip_topk_finish(users, cat, K, ws, s1, r1)
+        ev[2].record()
+        torch.cuda.synchronize()
+    t_scr, t_fin = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+    print(f"unsharded: screen {t_scr:.3f} ms, finish {t_fin:.3f} ms, total {t_scr + t_fin:.3f} ms")
+    del ws
+    tb = ops.ip_topk_tile_blocks(D)
+    shards = [HipRangeShard(cat, *shard_blocks(I, N, r, tb), K, U) for r in range(N)]
+    times = defaultdict(float)
+
+    def timer(phase, r, fn):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = fn()
+        b.record()
+        torch.cuda.synchronize()
+        times[(phase, r)] += a.elapsed_time(b)
+        return out
+
+    owner_replay(users, shards, K)  # warm-up
+    times.clear()
+    reps = 3
+    for _ in range(reps):
+        s, r, e = owner_replay(users, shards, K, timer=timer)
     torch.cuda.synchronize()
-    print("merged == unsharded:", bool(torch.equal(r, r1)))
+    worst = 0.0
+    for k in range(N):
+        t = {ph: times[(ph, k)] / reps for ph in ("screen", "band", "refine")}
+        tot = sum(t.values())
+        worst = max(worst, tot)
+        print(f"rank {k}: screen+bound {t['screen']:.3f} ms, band pack {t['band']:.3f} ms, "
+              f"owner refine {t['refine']:.3f} ms, total {tot:.3f} ms")
+    print(f"max per-rank compute {worst:.3f} ms against {t_scr + t_fin:.3f} ms unsharded "
+          f"(x{(t_scr + t_fin) / worst:.2f}, collectives not included)")
+    print("owner rows == unsharded:", bool(torch.equal(r, r1)), " scores:", bool(torch.equal(s, s1)))
 
 
 if __name__ == "__main__":

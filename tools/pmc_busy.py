@@ -10,7 +10,14 @@ Per kernel (averaged over its dispatches):
   wait_any / wait_inst / active = shares of SQ_WAVE_CYCLES (parked on
                s_waitcnt or a barrier / issue-stalled / issuing);
   insts per wave-instruction mix: SQ_INSTS_{VALU,MFMA,LDS,SALU,VMEM}.
-usage: pmc_busy.py DIR  (DIR/{scr,din}{1,2}/.../run_counter_collection.csv)
+Calibration (din_head read valu_busy 1.02): the raw formulas
+above are divided by what the pure loops of tools/calib/calib.hip read under
+the same counters (DIR/cal{1,2}): mfma_loop (back-to-back MFMAs, matrix pipe
+saturated) and valu_loop (independent v_fma_f32, 8 waves per SIMD, VALU issue
+saturated).  SQ_ACTIVE_INST_VALU counts each wave's VALU issue time, and
+waves on one SIMD overlap there, so the raw VALU formula of a saturated SIMD
+reads about 2, not 1.  Both raw and calibrated values are written.
+usage: pmc_busy.py DIR  (DIR/{scr,din,cal}{1,2}/.../run_counter_collection.csv)
 """
 import csv
 import glob
@@ -39,24 +46,49 @@ def load(path):
     return vals
 
 
+def raw_busy(c):
+    cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    if not cyc:
+        return None, None, cyc
+    return (c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (cyc * SIMDS),
+            4.0 * c.get("SQ_ACTIVE_INST_VALU", 0.0) / (cyc * SIMDS), cyc)
+
+
+def merged(root, grp):
+    m = defaultdict(dict)
+    for i in (1, 2):
+        for k, cs in load(os.path.join(root, f"{grp}{i}")).items():
+            for c, v in cs.items():
+                m[k][c] = sum(v) / len(v)
+    return m
+
+
 def main():
     root = sys.argv[1]
-    out = {}
-    for grp in ("scr", "din"):
-        merged = defaultdict(dict)
-        for i in (1, 2):
-            for k, cs in load(os.path.join(root, f"{grp}{i}")).items():
-                for c, v in cs.items():
-                    merged[k][c] = sum(v) / len(v)
-        for k, c in merged.items():
-            if not any(s in k for s in KEEP):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    cal = merged(root, "cal")
+    cm = [raw_busy(c)[0] for k, c in cal.items() if "mfma_loop" in k]
+    cv = [raw_busy(c)[1] for k, c in cal.items() if "valu_loop" in k]
+    cal_mfma = cm[0] if cm and cm[0] else 1.0
+    cal_valu = cv[0] if cv and cv[0] else 1.0
+    out = {"sources": bench.source_digest(),
+           "calibration": {"mfma_loop_raw_mfma_busy": cal_mfma, "valu_loop_raw_valu_busy": cal_valu,
+                           "note": "mfma_busy / valu_busy below = raw formula / these pure-loop readings"},
+           "kernels": {}}
+    for grp in ("scr", "din", "cal"):
+        for k, c in merged(root, grp).items():
+            if grp != "cal" and not any(s in k for s in KEEP):
                 continue
-            cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+            mb, vb, cyc = raw_busy(c)
             wc = c.get("SQ_WAVE_CYCLES", 0.0)
             r = {"kernel_cycles": round(cyc)}
             if cyc:
-                r["mfma_busy"] = round(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (cyc * SIMDS), 4)
-                r["valu_busy"] = round(4.0 * c.get("SQ_ACTIVE_INST_VALU", 0.0) / (cyc * SIMDS), 4)
+                r["mfma_busy"] = round(mb / cal_mfma, 4)
+                r["valu_busy"] = round(vb / cal_valu, 4)
+                r["mfma_busy_raw"] = round(mb, 4)
+                r["valu_busy_raw"] = round(vb, 4)
             if wc:
                 for n, key in (("wait_any", "SQ_WAIT_ANY"), ("wait_inst", "SQ_WAIT_INST_ANY"),
                                ("active", "SQ_ACTIVE_INST_ANY")):
@@ -65,7 +97,7 @@ def main():
                         "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS"):
                 if key in c:
                     r[key] = c[key]
-            out[k] = r
+            out["kernels"][k] = r
     json.dump(out, sys.stdout, indent=1)
     print()
 

@@ -63,7 +63,13 @@ def din_pass(fetch, write):
 
 
 def main(rf, rw, df, dw, out):
-    json.dump({"source": [rf, rw, df, dw], "correction": "FETCH_SIZE x1024 x2, WRITE_SIZE x1024",
+    import os
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    json.dump({"sources": bench.source_digest(), "source": [rf, rw, df, dw],
+               "correction": "FETCH_SIZE x1024 x2, WRITE_SIZE x1024",
                "kernels": per_kernel(rf, rw), "din_kernels": per_kernel(df, dw),
                "din_pass": din_pass(df, dw)}, open(out, "w"), indent=1)
 
