@@ -152,6 +152,21 @@ int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* ca
 int nrk_ip_topk_band_cap(int k);
 int nrk_ip_topk_band_pack(int64_t n_users, int64_t n_items, int dim, int k, const void* workspace,
                           size_t workspace_bytes, void* out_ent, int32_t* out_cnt, nrk_stream_t stream);
+/* The same shard protocol without the per-shard select (what nrk.dist uses):
+ * nrk_ip_topk_shard_screen = the scan of [blk_lo, blk_hi) + per user the m
+ * (1..256) largest appended half-block maxima as exact lower bounds
+ * (out_bound [n_users, m] f32, descending, -inf padded; k <= 128);
+ * nrk_ip_topk_shard_band, after the all_gather of every shard's bounds
+ * (bounds [n_lists][n_users][m], n_lists * m <= 512, or NULL): cut =
+ * max(the scan's own list bound - 2 eps, k-th largest bound - eps), the
+ * appended entries >= cut packed as nrk_ip_topk_band_pack does, and ucut
+ * written for nrk_ip_topk_refine_csr. */
+int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
+                             int k, int64_t blk_lo, int64_t blk_hi, int m, float* out_bound, void* workspace,
+                             size_t workspace_bytes, nrk_stream_t stream);
+int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, const float* bounds, int n_lists,
+                           int m, void* workspace, size_t workspace_bytes, void* out_ent, int32_t* out_cnt,
+                           nrk_stream_t stream);
 int nrk_ip_topk_refine_csr(const float* users, int64_t n_users, const float* items, const void* catalog,
                            int64_t n_items, int dim, int k, int64_t row_offset, const int64_t* band_off,
                            const void* band, const float* ucut, const int32_t* ovf_in, float* out_scores,

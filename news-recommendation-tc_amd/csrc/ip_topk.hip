@@ -1192,6 +1192,220 @@ __global__ __launch_bounds__(256) void ip_band_pack_kernel(int64_t n_users, int 
     if (lane == 0) out_cnt[u] = c;
 }
 
+// ------------------------------------ config-4 shard path without a select --
+// A catalog shard does not need its own k-th largest maximum: the global
+// bound G of the exchange is higher on most users, and the scan's own list
+// bound lb (uinfo.x, the smaller of the two lanes' (jk + 1)-th largest
+// inserted maxima) is a valid cut on its own: every tau of the scan was
+// <= lb - 2 eps, so each half-block whose fp16 max reaches lb - 2 eps was
+// appended, and at least 2 (jk + 1) >= k appended half-blocks (distinct
+// items) have max >= lb, i.e. an item with exact score >= lb - eps.  So the
+// shard runs scan -> shard_bound -> (all_gather) -> shard_band, one pass over
+// the appended maxima each, instead of select + bound + apply + pack.
+//
+// shard_bound: per user the m largest appended maxima (all of them are >= lb
+// whenever at least m are) as exact lower bounds v / scl - eps, rounded down
+// to fp32, descending, -inf padded; users whose appends overflowed (or that
+// hold more than IP_SEL maxima >= lb) are flagged for the exact path.
+// Both shard kernels run persistent waves (a wave walks users wid, wid +
+// nw, ...; the next user's counts / record are loaded during this one) and
+// load a user's appended entries 256 at a time, all loads in flight at once:
+// one wave per user was bound by per-wave start-up and dependent round trips.
+constexpr int SH_WG_PER_CU = 8;
+constexpr int SH_ENT = 4;  // entries per lane per load batch
+
+__device__ __forceinline__ void sh_load(const uint2* s0, const uint2* s1, int a0, int n, int b0, int lane,
+                                        uint2 (&ent)[SH_ENT]) {
+#pragma unroll
+    for (int j = 0; j < SH_ENT; ++j) {
+        const int e = b0 + j * WAVE + lane;
+        ent[j] = e < n ? (e < a0 ? s0[e] : s1[e - a0]) : make_uint2(0u, 0u);
+    }
+}
+
+__global__ __launch_bounds__(256) void ip_shard_bound_kernel(int64_t n_users, int m2, const uint2* __restrict__ app,
+                                                             const int32_t* __restrict__ acnt,
+                                                             const float4* __restrict__ uinfo, int m,
+                                                             float* __restrict__ out, int32_t* __restrict__ ovf_flag) {
+    __shared__ uint32_t sel[4][IP_SEL];
+    constexpr int KE = IP_SEL / WAVE;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int64_t u = (int64_t)blockIdx.x * 4 + wave;
+    int2 ac_n = make_int2(0, 0);
+    float4 inf_n = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (u < n_users) {
+        ac_n = reinterpret_cast<const int2*>(acnt)[u];
+        inf_n = uinfo[u];
+    }
+    for (; u < n_users; u += nw) {
+        const int a0 = ac_n.x, a1 = ac_n.y;
+        const float4 inf = inf_n;
+        if (u + nw < n_users) {
+            ac_n = reinterpret_cast<const int2*>(acnt)[u + nw];
+            inf_n = uinfo[u + nw];
+        }
+        bool ovf = a0 > m2 || a1 > m2;
+        const int n = ovf ? 0 : a0 + a1;
+        const uint2* s0 = app + (size_t)(2 * u) * m2;
+        const uint2* s1 = s0 + m2;
+        int c = 0;
+        for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
+            uint2 ent[SH_ENT];
+            sh_load(s0, s1, a0, n, b0, lane, ent);
+#pragma unroll
+            for (int j = 0; j < SH_ENT; ++j) {
+                const int e = b0 + j * WAVE + lane;
+                const float v = __uint_as_float(ent[j].x);
+                const bool kp = e < n && v >= inf.x;
+                const unsigned long long bal = __ballot(kp);
+                const int pos = c + __popcll(bal & lt);
+                if (kp && pos < IP_SEL) sel[wave][pos] = fkey(v);
+                c += __popcll(bal);
+            }
+        }
+        if (c > IP_SEL) ovf = true;
+        wave_sync_lds();
+        uint32_t key[KE];
+#pragma unroll
+        for (int e = 0; e < KE; ++e) key[e] = (!ovf && e * WAVE + lane < c) ? sel[wave][e * WAVE + lane] : 0u;
+        wave_sync_lds();  // the next user's keys overwrite sel
+        const double inv = inf.z > 0.0f ? 1.0 / (double)inf.z : 0.0;  // exact power of two
+        float ob[KE];
+#pragma unroll
+        for (int e = 0; e < KE; ++e) ob[e] = -INFINITY;
+        for (int j = 0; j < m; ++j) {
+            uint32_t mx = key[0];
+#pragma unroll
+            for (int e = 1; e < KE; ++e) mx = max(mx, key[e]);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, WAVE));
+            if (mx == 0u) break;  // fewer than m maxima: -inf padding
+            // drop one copy (lowest lane, lowest slot)
+            bool has = false;
+#pragma unroll
+            for (int e = 0; e < KE; ++e) has = has || key[e] == mx;
+            const int first = __ffsll((long long)__ballot(has)) - 1;
+            if (lane == first) {
+                bool done = false;
+#pragma unroll
+                for (int e = 0; e < KE; ++e)
+                    if (!done && key[e] == mx) {
+                        key[e] = 0u;
+                        done = true;
+                    }
+            }
+            const double tv = (double)fkey_inv(mx) * inv - (double)inf.w;
+            float v = (float)tv;
+            if ((double)v > tv) v = nextafterf(v, -INFINITY);
+#pragma unroll
+            for (int e = 0; e < KE; ++e)
+                if (e == (j >> 6) && lane == (j & 63)) ob[e] = v;
+        }
+#pragma unroll
+        for (int e = 0; e < KE; ++e)
+            if (e * WAVE + lane < m) out[u * m + e * WAVE + lane] = ob[e];
+        if (lane == 0) ovf_flag[u] = ovf ? 1 : 0;
+    }
+}
+
+// shard_band: G = the k-th largest of the user's n_lists * m exchanged bounds
+// (-inf with fewer than k values; none without bounds), cut = max(lb - 2 eps,
+// G - eps) in the scan's scaled units (both valid: k items have exact >= G,
+// and k items have exact >= lb - eps), then the appended entries >= cut
+// compacted to out_ent[u * bandcap + j] (-1: overflowed -> the owner's exact
+// path) and the cut written to ucut for the owner's refine.  Entries keep the
+// scaled fp16 max and the GLOBAL half-block id.  uinfo.z == 0 marks an empty
+// shard: no band, no cut.
+__global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int k, int m2,
+                                                            const uint2* __restrict__ app,
+                                                            const int32_t* __restrict__ acnt,
+                                                            const float4* __restrict__ uinfo,
+                                                            const float* __restrict__ bounds, int n_lists, int m,
+                                                            int bandcap, const int32_t* __restrict__ ovf_flag,
+                                                            float2* __restrict__ ucut, uint2* __restrict__ out_ent,
+                                                            int32_t* __restrict__ out_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int tot = bounds ? n_lists * m : 0;
+    const int ec = (tot + WAVE - 1) / WAVE;
+    int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    int2 ac_n = make_int2(0, 0);
+    float4 inf_n = make_float4(0.f, 0.f, 0.f, 0.f);
+    int ov_n = 0;
+    if (u < n_users) {
+        ac_n = reinterpret_cast<const int2*>(acnt)[u];
+        inf_n = uinfo[u];
+        ov_n = ovf_flag[u];
+    }
+    for (; u < n_users; u += nw) {
+        const int a0 = ac_n.x, n = ac_n.x + ac_n.y, ov = ov_n;
+        const float4 inf = inf_n;
+        if (u + nw < n_users) {
+            ac_n = reinterpret_cast<const int2*>(acnt)[u + nw];
+            inf_n = uinfo[u + nw];
+            ov_n = ovf_flag[u + nw];
+        }
+        if (ov || inf.z <= 0.0f) {
+            if (lane == 0) {
+                out_cnt[u] = ov ? -1 : 0;
+                ucut[u] = make_float2(-INFINITY, 0.0f);
+            }
+            continue;
+        }
+        const uint2* s0 = app + (size_t)(2 * u) * m2;
+        const uint2* s1 = s0 + m2;
+        uint2 ent[SH_ENT];
+        sh_load(s0, s1, a0, n, 0, lane, ent);  // in flight across the bound select
+        float G = -INFINITY;
+        if (tot >= k) {
+            uint32_t key[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int i = e * WAVE + lane;
+                key[e] = (e < ec && i < tot) ? fkey(bounds[((int64_t)(i / m) * n_users + u) * m + (i % m)]) : 0u;
+            }
+            uint32_t x = 0;
+            for (int bit = 31; bit >= 0; --bit) {
+                const uint32_t cd = x | (1u << bit);
+                int cc = 0;
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (e < ec) cc += __popcll(__ballot(key[e] >= cd));
+                if (cc >= k) x = cd;
+            }
+            G = fkey_inv(x);
+        }
+        float cut = inf.x == -INFINITY ? -INFINITY : round_down_sub(inf.x, 2.0f * inf.y);
+        if (G > -INFINITY) {
+            const double tt = (double)G - (double)inf.w;
+            float f = (float)tt;
+            if ((double)f > tt) f = nextafterf(f, -INFINITY);
+            cut = fmaxf(cut, f * inf.z);  // exact power-of-two rescale
+        }
+        int c = 0;
+        uint2* dst = out_ent + (size_t)u * bandcap;
+        for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
+            if (b0 > 0) sh_load(s0, s1, a0, n, b0, lane, ent);
+#pragma unroll
+            for (int j = 0; j < SH_ENT; ++j) {
+                const int e = b0 + j * WAVE + lane;
+                const bool kp = e < n && !(__uint_as_float(ent[j].x) < cut);
+                const unsigned long long bal = __ballot(kp);
+                const int pos = c + __popcll(bal & lt);
+                if (kp && pos < bandcap) dst[pos] = ent[j];
+                c += __popcll(bal);
+            }
+        }
+        if (lane == 0) {
+            out_cnt[u] = c > bandcap ? -1 : c;
+            ucut[u] = make_float2(cut == -INFINITY ? -INFINITY : cut / inf.z, inf.w);
+        }
+    }
+}
+
 // owner side: users flagged for the exact path -> the fallback's list
 __global__ void ip_ovf_collect_kernel(int64_t n_users, const int32_t* __restrict__ ovf_in,
                                       int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
@@ -1315,6 +1529,7 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
             case 1: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 2: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 3: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 4: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
             default: break;
         }
     }
@@ -1335,6 +1550,48 @@ static void launch_scan_k(const float* users, int n_users, const uint8_t* cat, i
     if (mt <= 16) launch_scan<DP, 16>(users, n_users, cat, n_items, dim, k, w, s);
     else if (mt <= 32) launch_scan<DP, 32>(users, n_users, cat, n_items, dim, k, w, s);
     else launch_scan<DP, 64>(users, n_users, cat, n_items, dim, k, w, s);
+}
+
+static void scan_dispatch(const float* users, int nu, const uint8_t* cat, int ni, int dim, int k, const IpWs& w,
+                          hipStream_t s) {
+    switch (pad_dim(dim)) {
+        case 16: launch_scan_k<16>(users, nu, cat, ni, dim, k, w, s); break;
+        case 32: launch_scan_k<32>(users, nu, cat, ni, dim, k, w, s); break;
+        case 64: launch_scan_k<64>(users, nu, cat, ni, dim, k, w, s); break;
+        case 128: launch_scan_k<128>(users, nu, cat, ni, dim, k, w, s); break;
+        default: launch_scan_k<256>(users, nu, cat, ni, dim, k, w, s); break;
+    }
+}
+
+// a tile-aligned block range of a shard (config 4), checked
+static int ip_range(IpWs& w, int64_t n_items, int dim, int64_t blk_lo, int64_t blk_hi) {
+    const int tb = 64 * pad_dim(dim) >= 8192 ? 1 : 8192 / (64 * pad_dim(dim));
+    NRK_REQUIRE(blk_lo >= 0 && blk_lo <= blk_hi && blk_hi <= n_blocks_of(n_items), "block range out of bounds");
+    NRK_REQUIRE(blk_lo == blk_hi || (blk_lo % tb == 0 && (blk_hi % tb == 0 || blk_hi == n_blocks_of(n_items))),
+                "block range must start (and end, unless at the catalog end) on a 8-KB tile");
+    w.blk_lo = (int)blk_lo;
+    w.blk_hi = (int)blk_hi;
+    return NRK_OK;
+}
+
+// persistent grid of the shard kernels: SH_WG_PER_CU 4-wave workgroups per CU
+static int sh_grid(int64_t n_users) {
+    static const int n_cu = [] {
+        int dev = 0, cu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+        return cu > 0 ? cu : 256;
+    }();
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n_users + 3) / 4, (int64_t)n_cu * SH_WG_PER_CU));
+}
+
+// empty shard range: no appends, uinfo.z = 0 (shard_band: no band, no cut)
+__global__ void ip_empty_range_kernel(int64_t n_users, int32_t* __restrict__ acnt, float4* __restrict__ uinfo) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_users;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        acnt[2 * u] = 0;
+        acnt[2 * u + 1] = 0;
+        uinfo[u] = make_float4(-INFINITY, 0.0f, 0.0f, 0.0f);
+    }
 }
 
 }  // namespace nrk
@@ -1408,21 +1665,14 @@ int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* ca
                       workspace_bytes);
     if (rc != NRK_OK || n_users == 0) return rc;
     IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
-    {
-        const int tb = 64 * pad_dim(dim) >= 8192 ? 1 : 8192 / (64 * pad_dim(dim));
-        NRK_REQUIRE(blk_lo >= 0 && blk_lo <= blk_hi && blk_hi <= n_blocks_of(n_items), "block range out of bounds");
-        NRK_REQUIRE(blk_lo == blk_hi || (blk_lo % tb == 0 && (blk_hi % tb == 0 || blk_hi == n_blocks_of(n_items))),
-                    "block range must start (and end, unless at the catalog end) on a 8-KB tile");
-        w.blk_lo = (int)blk_lo;
-        w.blk_hi = (int)blk_hi;
-        if (blk_hi == blk_lo) n_items = 0;  // empty range: every output row is padding
-    }
+    rc = ip_range(w, n_items, dim, blk_lo, blk_hi);
+    if (rc != NRK_OK) return rc;
+    if (blk_hi == blk_lo) n_items = 0;  // empty range: every output row is padding
     hipStream_t s = as_stream(stream);
     if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
         set_error("nrk_ip_topk_screen: hipMemsetAsync failed");
         return NRK_EHIP;
     }
-    const int dp = pad_dim(dim);
     const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
     if (n_items == 0) {
         // nothing to search: every output row is padding
@@ -1433,15 +1683,7 @@ int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* ca
         const int grid = (int)std::min<int64_t>((n_users + 255) / 256, 4096);
         ip_all_exact_kernel<<<grid, 256, 0, s>>>(n_users, w.cnt, w.ovf_flag, w.ovf_list, w.ovf_count);
     } else {
-        const int nu = (int)n_users, ni = (int)n_items;
-        switch (dp) {
-            case 16: launch_scan_k<16>(users, nu, cat, ni, dim, k, w, s); break;
-            case 32: launch_scan_k<32>(users, nu, cat, ni, dim, k, w, s); break;
-            case 64: launch_scan_k<64>(users, nu, cat, ni, dim, k, w, s); break;
-            case 128: launch_scan_k<128>(users, nu, cat, ni, dim, k, w, s); break;
-            default: launch_scan_k<256>(users, nu, cat, ni, dim, k, w, s); break;
-        }
-
+        scan_dispatch(users, (int)n_users, cat, (int)n_items, dim, k, w, s);
         ip_select_kernel<<<(int)((n_users + 3) / 4), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt,
                                                                  w.uinfo, w.cand, w.cnt, w.ucut, w.ovf_flag,
                                                                  w.ovf_list, w.ovf_count);
@@ -1584,6 +1826,52 @@ int nrk_ip_topk_band_pack(int64_t n_users, int64_t n_items, int dim, int k, cons
     const IpWs w = ip_ws_layout(const_cast<void*>(workspace), n_users, n_items, k, dim);
     ip_band_pack_kernel<<<(int)((n_users + 3) / 4), 256, 0, as_stream(stream)>>>(
         n_users, w.bandcap, w.cand, w.cnt, w.ucut, w.uinfo, w.ovf_flag, reinterpret_cast<uint2*>(out_ent), out_cnt);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
+                             int k, int64_t blk_lo, int64_t blk_hi, int m, float* out_bound, void* workspace,
+                             size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    int rc = ip_check(users, n_users, (const float*)catalog, catalog, n_items, dim, k, workspace,
+                      workspace_bytes);
+    if (rc != NRK_OK) return rc;
+    if (k > IP_KFAST) NRK_UNSUPPORTED("the shard screen needs k <= 128 (larger k: the merge protocol)");
+    NRK_REQUIRE(m >= 1 && m <= IP_SEL, "m must be in [1, 256]");
+    if (n_users == 0) return NRK_OK;
+    NRK_REQUIRE(out_bound != nullptr, "null pointer");
+    IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
+    rc = ip_range(w, n_items, dim, blk_lo, blk_hi);
+    if (rc != NRK_OK) return rc;
+    hipStream_t s = as_stream(stream);
+    if (blk_lo == blk_hi || n_items == 0) {
+        ip_empty_range_kernel<<<(int)std::min<int64_t>((n_users + 255) / 256, 4096), 256, 0, s>>>(n_users, w.acnt,
+                                                                                               w.uinfo);
+    } else {
+        scan_dispatch(users, (int)n_users, reinterpret_cast<const uint8_t*>(catalog), (int)n_items, dim, k, w, s);
+    }
+    ip_shard_bound_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, w.m2, w.app, w.acnt, w.uinfo, m, out_bound,
+                                                           w.ovf_flag);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, const float* bounds, int n_lists,
+                           int m, void* workspace, size_t workspace_bytes, void* out_ent, int32_t* out_cnt,
+                           nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_users >= 0 && n_users < (1ll << 30) && n_items >= 0 && dim > 0 && dim <= 256, "bad sizes");
+    NRK_REQUIRE(k >= 1 && k <= IP_KFAST, "k must be in [1, 128]");
+    NRK_REQUIRE(bounds == nullptr || (n_lists >= 1 && m >= 1 && n_lists * m <= 512),
+                "need 1 <= n_lists * m <= 512");
+    if (n_users == 0) return NRK_OK;
+    NRK_REQUIRE(workspace && out_ent && out_cnt, "null pointer");
+    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users, n_items, k, dim).bytes, "workspace too small");
+    const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
+    ip_shard_band_kernel<<<sh_grid(n_users), 256, 0, as_stream(stream)>>>(
+        n_users, k, w.m2, w.app, w.acnt, w.uinfo, bounds, bounds ? n_lists : 0, bounds ? m : 1, w.bandcap,
+        w.ovf_flag, w.ucut, reinterpret_cast<uint2*>(out_ent), out_cnt);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

@@ -172,13 +172,12 @@ class HipRangeShard:
         self.rws = None
 
     def screen(self, users, m: int):
-        self.ops.ip_topk_screen_range(users, self.cat, self.k, self.blk_lo, self.blk_hi, self.ws)
-        return self.ops.ip_topk_bound(users, self.cat, self.k, m, self.ws)
+        # scan + the m largest appended maxima as bounds (no per-shard select)
+        return self.ops.ip_topk_shard_screen(users, self.cat, self.k, self.blk_lo, self.blk_hi, m, self.ws)
 
     def band(self, bounds=None):
-        if bounds is not None:
-            self.ops.ip_topk_apply_bound(bounds, self.k, self.ws)
-        return self.ops.ip_topk_band_pack(self.n_users, self.cat, self.k, self.ws)
+        # cut = max(own list bound - 2 eps, global bound - eps); entries >= cut
+        return self.ops.ip_topk_shard_band(self.n_users, self.cat, self.k, bounds, self.ws)
 
     def ucut(self, lo: int, hi: int):
         return self.ops.ip_topk_ucut(self.ws, self.n_users)[lo:hi].contiguous()

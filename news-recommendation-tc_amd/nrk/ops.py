@@ -44,6 +44,14 @@ def _need(t, dtype, shape=None, name="tensor"):
         raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
 
 
+def _finite(t, name):
+    """The screen kernels are built with -fno-honor-nans (Makefile): NaN / inf
+    inputs would silently break their max chains, so the entry points that
+    take outside vectors check them here (one reduction + sync)."""
+    if t.numel() and not bool(torch.isfinite(t).all()):
+        raise ValueError(f"{name} must be finite (NaN / inf found)")
+
+
 # ------------------------------------------------------------------ tower --
 def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1):
     """YoutubeDNN user tower + re-normalisation (youtubednn_recaller.py:129-178, :467-470)."""
@@ -120,14 +128,16 @@ CF_TOPK_MAX = 2048  # nrk_itemcf_topn / nrk_itemcf_recall (register path <= 64, 
 
 
 class Catalog:
-    """The search index: fp32 rows (kept for exact rescoring) + packed bf16
-    copy in MFMA fragment order.  = faiss.IndexFlatIP(d).add(items)."""
+    """The search index: fp32 rows (kept for exact rescoring) + a scaled fp16
+    copy packed in MFMA fragment order.  = faiss.IndexFlatIP(d).add(items);
+    rejects NaN / inf rows."""
 
     def __init__(self, items: torch.Tensor):
         _dev(items)
         _need(items, torch.float32, name="items")
         if items.dim() != 2 or not (1 <= items.shape[1] <= 256):
             raise ValueError("items must be [n, d] with 1 <= d <= 256")
+        _finite(items, "items")
         self.items = items
         self.n, self.d = items.shape
         nbytes = _lib.lib().nrk_ip_catalog_bytes(self.n, self.d)
@@ -139,12 +149,18 @@ class Catalog:
         return self.n
 
 
-def ip_topk(users, catalog: Catalog, k: int, row_offset: int = 0, exact: bool = False, workspace=None):
-    """Exact top-k rows per user (scores f32 [n,k], rows i32 [n,k] (+ fp64))."""
+def ip_topk(users, catalog: Catalog, k: int, row_offset: int = 0, exact: bool = False, workspace=None,
+            check_finite: bool = True):
+    """Exact top-k rows per user (scores f32 [n,k], rows i32 [n,k] (+ fp64)).
+    ``check_finite`` rejects NaN / inf users (one device sync); the split
+    screen entry points (ip_topk_screen*, the bench / catalog-sharded path)
+    leave that to the caller."""
     _dev(users, catalog.items)
     _need(users, torch.float32, name="users")
     if users.dim() != 2 or users.shape[1] != catalog.d:
         raise ValueError(f"users must be [n, {catalog.d}]")
+    if check_finite:
+        _finite(users, "users")
     if not (1 <= k <= IP_KMAX):
         raise ValueError(f"k must be in [1, {IP_KMAX}]")
     n = users.shape[0]
@@ -184,7 +200,8 @@ def topk_merge(exact_lists, row_lists, k_out):
 
 
 def ip_topk_screen(users, catalog: Catalog, k: int, workspace):
-    """Phase 1 of ip_topk (bf16 MFMA scan -> candidate band in ``workspace``)."""
+    """Phase 1 of ip_topk (fp16 MFMA scan -> candidate band in ``workspace``).
+    ``users`` must be finite (not checked here: the hot path)."""
     _dev(users, workspace)
     n = users.shape[0]
     _lib.call("nrk_ip_topk_screen", _ptr(users), n, _ptr(catalog.packed), catalog.n, catalog.d, k,
@@ -238,6 +255,36 @@ def ip_topk_band_pack(n_users, catalog: Catalog, k: int, workspace):
     ent = torch.empty((n_users, cap), dtype=torch.int64, device=dev)
     _lib.call("nrk_ip_topk_band_pack", n_users, catalog.n, catalog.d, int(k), _ptr(workspace), workspace.numel(),
               _ptr(ent), _ptr(cnt), _stream())
+    return cnt, ent
+
+
+def ip_topk_shard_screen(users, catalog: Catalog, k: int, blk_lo: int, blk_hi: int, m: int, workspace):
+    """Config-4 shard, select-free: the scan of the blocks [blk_lo, blk_hi)
+    for every user + per user the m largest appended maxima as exact lower
+    bounds (fp32 [n, m], descending, -inf padded)."""
+    _dev(users, workspace)
+    n = users.shape[0]
+    out = torch.empty((n, m), dtype=torch.float32, device=users.device)
+    _lib.call("nrk_ip_topk_shard_screen", _ptr(users), n, _ptr(catalog.packed), catalog.n, catalog.d, int(k),
+              int(blk_lo), int(blk_hi), int(m), _ptr(out), _ptr(workspace), workspace.numel(), _stream())
+    return out
+
+
+def ip_topk_shard_band(n_users, catalog: Catalog, k: int, bounds, workspace):
+    """After ip_topk_shard_screen and the all_gather of every shard's bounds
+    (``bounds`` [n_lists, n_users, m] f32, or None): cut = max(own list bound
+    - 2 eps, k-th largest bound - eps), the entries >= cut packed: (cnt int32
+    [n] (-1 = exact path), ent int64 [n, cap]); the cut goes to ucut."""
+    cap = _lib.lib().nrk_ip_topk_band_cap(int(k))
+    dev = workspace.device
+    cnt = torch.empty(n_users, dtype=torch.int32, device=dev)
+    ent = torch.empty((n_users, cap), dtype=torch.int64, device=dev)
+    nl, m = (0, 1) if bounds is None else (bounds.shape[0], bounds.shape[2])
+    if bounds is not None:
+        _dev(bounds, workspace)
+        _need(bounds, torch.float32, (nl, n_users, m), "bounds")
+    _lib.call("nrk_ip_topk_shard_band", n_users, catalog.n, catalog.d, int(k), _ptr(bounds), nl, m,
+              _ptr(workspace), workspace.numel(), _ptr(ent), _ptr(cnt), _stream())
     return cnt, ent
 
 
@@ -320,6 +367,7 @@ class DinParams:
                 raise NotImplementedError("the DIN kernels are compiled for embedding dim 32")
         base = np.cumsum([0] + [t.shape[0] for t in tabs[:-1]]).astype(np.int64)
         table = torch.from_numpy(np.concatenate(tabs, 0))
+        _finite(table, "DIN embedding tables")
         if table_dtype == "bf16":
             self.table = table.to(torch.bfloat16).to(device).contiguous()
             self.table_code = 1

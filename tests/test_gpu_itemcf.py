@@ -156,6 +156,9 @@ def _near_ties_only(g_idx, o_idx, o_val_ext, valid, rtol=1e-12):
     only near-ties that the last ulp of exp / pow can reorder."""
     mism = (g_idx != o_idx) & valid
     r, p = np.nonzero(mism)
+    # VERDICT r2: say how many positions the near-tie rule had to excuse
+    print(f"near-tie check: {len(r)} differing positions in {int(np.unique(r).size)} rows "
+          f"of {int(valid.sum())} compared entries")
     if len(r) == 0:
         return True
     v = o_val_ext

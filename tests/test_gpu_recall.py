@@ -409,3 +409,20 @@ def test_screen_eps_bounds_the_fp16_rounding(ops, d):
     # and it is the tighter form: well under round 1's 2^-10 ||u|| max||v|| worst case
     old = 9.765625e-4 * np.linalg.norm(users.astype(np.float64), axis=1) * np.linalg.norm(items, axis=1).max()
     assert np.all(eps < 0.9 * old), float((eps / old).max())
+
+
+@pytest.mark.gpu
+def test_nonfinite_inputs_rejected():
+    """NaN / inf items or users never reach the -fno-honor-nans screen."""
+    from nrk import ops
+
+    items = torch.nn.functional.normalize(torch.randn(500, 32, device="cuda"), dim=1).contiguous()
+    bad = items.clone()
+    bad[7, 3] = float("nan")
+    with pytest.raises(ValueError, match="finite"):
+        ops.Catalog(bad)
+    cat = ops.Catalog(items)
+    u = torch.randn(10, 32, device="cuda")
+    u[4, 0] = float("inf")
+    with pytest.raises(ValueError, match="finite"):
+        ops.ip_topk(u, cat, 31)

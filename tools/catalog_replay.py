@@ -43,7 +43,7 @@ def main():
         torch.cuda.synchronize()
     t_scr, t_fin = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
     print(f"unsharded: screen {t_scr:.3f} ms, finish {t_fin:.3f} ms, total {t_scr + t_fin:.3f} ms")
-    del ws
+    ws1 = ws
     tb = ops.ip_topk_tile_blocks(D)
     shards = [HipRangeShard(cat, *shard_blocks(I, N, r, tb), K, U) for r in range(N)]
     times = defaultdict(float)
@@ -57,7 +57,16 @@ def main():
         times[(phase, r)] += a.elapsed_time(b)
         return out
 
+    def acnt_stats(ws, n):
+        a = lambda x: (x + 255) & ~255  # noqa: E731
+        off = 256 + a(8 * n) + 3 * a(4 * n) + a(16 * n)
+        ac = ws[off: off + 8 * n].view(torch.int32).view(n, 2).sum(1).float()
+        return f"appended maxima per user: mean {ac.mean().item():.1f}, p99 {ac.quantile(0.99).item():.0f}, " \
+               f"max {ac.max().item():.0f}"
+
+    print("unsharded", acnt_stats(ws1, U))
     owner_replay(users, shards, K)  # warm-up
+    print("shard 0", acnt_stats(shards[0].ws, U))
     times.clear()
     reps = 3
     for _ in range(reps):
