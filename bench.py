@@ -853,13 +853,23 @@ def main(argv=None):
     if args.dry_run:
         return dry_run(args, world, rank, local)
     dist = None
+    # one GPU per rank; with fewer visible GPUs than ranks (a one-GPU
+    # rehearsal of the N-rank layout, --backend gloo) ranks share devices
+    ndev = torch.cuda.device_count()
+    dev_idx = local % ndev if ndev else local
+    if ndev and local >= ndev:
+        log(f"[rank {rank}] {ndev} visible GPU(s): rank shares cuda:{dev_idx} (rehearsal, not a measurement)")
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        torch.cuda.set_device(dev_idx)
+        backend = args.backend or "nccl"
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(backend)
+    device = torch.device("cuda", dev_idx)
     torch.cuda.set_device(device)
     log(f"[rank {rank}/{world}] device {device} ({torch.cuda.get_device_name(device)}), pid {os.getpid()}")
 

@@ -533,6 +533,65 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
     return __uint_as_float((k >> 31) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
+// Descending ranks of the c keys of one wave's LDS row (0 = largest; equal
+// keys by position): a lane holds keys at positions pos + 64 e and
+// counts, over LDS broadcasts of all c keys (4 per read), the keys above its
+// own.  The row must be zero-padded to a multiple of 4.  VALU-only work with
+// independent steps -- the bitwise radix select it replaces (32 dependent
+// ballot / scalar-count rounds per user) cost 0.2 ms per 250k users.
+template <int E>
+__device__ __forceinline__ void lds_ranks(const uint32_t* __restrict__ row, int c, const uint32_t (&mine)[E],
+                                          int pos, int (&rank)[E]) {
+    // pos = the row position of mine[0]; mine[e] sits at pos + 64 e
+#pragma unroll
+    for (int e = 0; e < E; ++e) rank[e] = 0;
+    for (int j0 = 0; j0 < c; j0 += 4) {
+        const uint4 q = *reinterpret_cast<const uint4*>(row + j0);
+        const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                rank[e] += (qq[t] > mine[e] || (qq[t] == mine[e] && j0 + t < e * WAVE + pos)) ? 1 : 0;
+        }
+    }
+}
+
+// the key of rank r (r < c) of a wave's LDS row of c keys (see lds_ranks),
+// 64 keys at a time (a run-time loop: few registers whatever c is)
+__device__ __forceinline__ uint32_t lds_select(uint32_t* __restrict__ row, int c, int r, int lane) {
+    if (lane < 4) row[c + lane] = 0u;  // zero pad (the row has room: c + 4 <= its size)
+    wave_sync_lds();
+    uint32_t x = 0u;
+    for (int b0 = 0; b0 < c; b0 += WAVE) {
+        const uint32_t mine[1] = {b0 + lane < c ? row[b0 + lane] : 0u};
+        int rank[1];
+        lds_ranks<1>(row, c, mine, b0 + lane, rank);
+        const unsigned long long b = __ballot(b0 + lane < c && rank[0] == r);
+        if (b) {
+            x = (uint32_t)__shfl((int)mine[0], __ffsll((long long)b) - 1, WAVE);
+            break;
+        }
+    }
+    return x;
+}
+
+// The select and the shard kernels run persistent waves (a wave walks users
+// wid, wid + nw, ...; the next user's counts / record are loaded during this one) and
+// load a user's appended entries 256 at a time, all loads in flight at once:
+// one wave per user was bound by per-wave start-up and dependent round trips.
+constexpr int SH_WG_PER_CU = 8;
+constexpr int SH_ENT = 4;  // entries per lane per load batch
+
+__device__ __forceinline__ void sh_load(const uint2* s0, const uint2* s1, int a0, int n, int b0, int lane,
+                                        uint2 (&ent)[SH_ENT]) {
+#pragma unroll
+    for (int j = 0; j < SH_ENT; ++j) {
+        const int e = b0 + j * WAVE + lane;
+        ent[j] = e < n ? (e < a0 ? s0[e] : s1[e - a0]) : make_uint2(0u, 0u);
+    }
+}
+
 // Select: one wave per user.  theta = the exact k-th largest appended max:
 // the entries >= theta_lb (at least 2 (jk + 1) >= k of them: every value a
 // lane's final top list holds entered it at a position <= jk, above the tau
@@ -546,72 +605,78 @@ __global__ __launch_bounds__(256) void ip_select_kernel(
     const int32_t* __restrict__ acnt, const float4* __restrict__ uinfo, uint2* __restrict__ cand,
     int32_t* __restrict__ cand_cnt, float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag,
     int32_t* __restrict__ ovf_list, int32_t* __restrict__ ovf_count) {
-    __shared__ uint32_t sel[4][IP_SEL];
+    __shared__ __attribute__((aligned(16))) uint32_t sel[4][IP_SEL + 4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t u = (int64_t)blockIdx.x * 4 + wave;
-    if (u >= n_users) return;
-    const int a0 = acnt[2 * u], a1 = acnt[2 * u + 1];
-    const float4 inf = uinfo[u];
-    bool ovf = a0 > m2 || a1 > m2;
-    const int n = ovf ? 0 : a0 + a1;
-    const uint2* s0 = app + (size_t)(2 * u) * m2;
-    const uint2* s1 = s0 + m2;
-    auto entry = [&](int e) -> uint2 { return e < a0 ? s0[e] : s1[e - a0]; };
+    const int64_t nw = (int64_t)gridDim.x * 4;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    // pass 1: keys of the entries >= theta_lb
-    int c = 0;
-    for (int b0 = 0; b0 < n; b0 += WAVE) {
-        const int e = b0 + lane;
-        const float v = e < n ? __uint_as_float(entry(e).x) : -INFINITY;
-        const bool kp = e < n && v >= inf.x;
-        const unsigned long long bal = __ballot(kp);
-        const int pos = c + __popcll(bal & lt);
-        if (kp && pos < IP_SEL) sel[wave][pos] = fkey(v);
-        c += __popcll(bal);
+    // persistent waves (see the shard kernels): the next user's counts and
+    // record load during this one; entries load SH_ENT x 64 at a time
+    int64_t u = (int64_t)blockIdx.x * 4 + wave;
+    int2 ac_n = make_int2(0, 0);
+    float4 inf_n = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (u < n_users) {
+        ac_n = reinterpret_cast<const int2*>(acnt)[u];
+        inf_n = uinfo[u];
     }
-    if (c > IP_SEL) ovf = true;
-    float theta = -INFINITY;
-    if (!ovf && c >= k) {
+    for (; u < n_users; u += nw) {
+        const int a0 = ac_n.x, a1 = ac_n.y;
+        const float4 inf = inf_n;
+        if (u + nw < n_users) {
+            ac_n = reinterpret_cast<const int2*>(acnt)[u + nw];
+            inf_n = uinfo[u + nw];
+        }
+        bool ovf = a0 > m2 || a1 > m2;
+        const int n = ovf ? 0 : a0 + a1;
+        const uint2* s0 = app + (size_t)(2 * u) * m2;
+        const uint2* s1 = s0 + m2;
+        // pass 1: keys of the entries >= theta_lb
+        int c = 0;
+        uint2 ent[SH_ENT];
+        for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
+            sh_load(s0, s1, a0, n, b0, lane, ent);
+#pragma unroll
+            for (int j = 0; j < SH_ENT; ++j) {
+                const int e = b0 + j * WAVE + lane;
+                const float v = __uint_as_float(ent[j].x);
+                const bool kp = e < n && v >= inf.x;
+                const unsigned long long bal = __ballot(kp);
+                const int pos = c + __popcll(bal & lt);
+                if (kp && pos < IP_SEL) sel[wave][pos] = fkey(v);
+                c += __popcll(bal);
+            }
+        }
+        if (c > IP_SEL) ovf = true;
+        float theta = -INFINITY;
         wave_sync_lds();
-        const int ec = (c + WAVE - 1) / WAVE;
-        uint32_t key[IP_SEL / WAVE];
-#pragma unroll
-        for (int e = 0; e < IP_SEL / WAVE; ++e) {
-            const int i = e * WAVE + lane;
-            key[e] = (e < ec && i < c) ? sel[wave][i] : 0u;
+        if (!ovf && c >= k) {
+            const uint32_t x = lds_select(sel[wave], c, k - 1, lane);
+            theta = fkey_inv(x);
         }
-        uint32_t x = 0;
-        for (int bit = 31; bit >= 0; --bit) {
-            const uint32_t cd = x | (1u << bit);
-            int cc = 0;
+        wave_sync_lds();  // the next user's keys overwrite sel
+        float cut = theta;
+        if (inf.y != 0.0f && theta != -INFINITY) cut = round_down_sub(theta, 2.0f * inf.y);
+        // pass 2: the band (append order); a single batch is still in registers
+        int nb = 0;
+        uint2* bd = cand + (size_t)u * bandcap;
+        for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
+            if (n > SH_ENT * WAVE) sh_load(s0, s1, a0, n, b0, lane, ent);
 #pragma unroll
-            for (int e = 0; e < IP_SEL / WAVE; ++e)
-                if (e < ec) cc += __popcll(__ballot(key[e] >= cd));
-            if (cc >= k) x = cd;
+            for (int j = 0; j < SH_ENT; ++j) {
+                const int e = b0 + j * WAVE + lane;
+                const bool kp = e < n && __uint_as_float(ent[j].x) >= cut;
+                const unsigned long long bal = __ballot(kp);
+                const int pos = nb + __popcll(bal & lt);
+                if (kp && pos < bandcap) bd[pos] = ent[j];
+                nb += __popcll(bal);
+            }
         }
-        theta = fkey_inv(x);
-    }
-    float cut = theta;
-    if (inf.y != 0.0f && theta != -INFINITY) cut = round_down_sub(theta, 2.0f * inf.y);
-    // pass 2: the band (append order)
-    int nb = 0;
-    uint2* bd = cand + (size_t)u * bandcap;
-    for (int b0 = 0; b0 < n; b0 += WAVE) {
-        const int e = b0 + lane;
-        uint2 ent = make_uint2(0u, 0u);
-        if (e < n) ent = entry(e);
-        const bool kp = e < n && __uint_as_float(ent.x) >= cut;
-        const unsigned long long bal = __ballot(kp);
-        const int pos = nb + __popcll(bal & lt);
-        if (kp && pos < bandcap) bd[pos] = ent;
-        nb += __popcll(bal);
-    }
-    if (nb > bandcap) ovf = true;
-    if (lane == 0) {
-        cand_cnt[u] = ovf ? 0 : nb;
-        ucut[u] = make_float2(cut == -INFINITY ? -INFINITY : cut / inf.z, inf.w);
-        ovf_flag[u] = ovf ? 1 : 0;
-        if (ovf) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
+        if (nb > bandcap) ovf = true;
+        if (lane == 0) {
+            cand_cnt[u] = ovf ? 0 : nb;
+            ucut[u] = make_float2(cut == -INFINITY ? -INFINITY : cut / inf.z, inf.w);
+            ovf_flag[u] = ovf ? 1 : 0;
+            if (ovf) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
+        }
     }
 }
 
@@ -661,7 +726,8 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
     const uint2* __restrict__ cand, int bandcap, const int32_t* __restrict__ cand_cnt,
     const float2* __restrict__ ucut, const int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
     int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
-    double* __restrict__ out_e, const int64_t* __restrict__ band_off = nullptr) {
+    double* __restrict__ out_e, const int64_t* __restrict__ band_off = nullptr, int n_src = 0,
+    int64_t src_users = 0, int x_cap = 0, const int32_t* __restrict__ src_cnt = nullptr) {
     constexpr int SE = SV / WAVE;
     __shared__ Cand surv[4][SV];
     __shared__ int32_t krow[DS4 > 0 ? 4 : 1][DS4 > 0 ? IP_KRING : 1];
@@ -671,7 +737,22 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users || ovf_flag[u]) return;
-    if (band_off && band_off[u + 1] - band_off[u] > IP_BQ) {  // more than the LDS holds: exact path
+    // band: per-user slots of the select (band_off == nullptr, n_src == 0), a
+    // CSR of every catalog shard's entries for this user (band_off), or the
+    // fixed-slot exchange (n_src > 0): source s's entries at
+    // cand[(s * src_users + u) * x_cap + j], j < src_cnt[s * src_users + u]
+    int src_n = 0;  // lane s < n_src: source s's count
+    int nsrc_tot = 0;
+    if (n_src > 0) {
+        for (int s0 = 0; s0 < n_src; s0 += WAVE) {
+            const int sl = s0 + lane;
+            const int c = sl < n_src ? max(0, src_cnt[(int64_t)sl * src_users + u]) : 0;
+            if (s0 == 0) src_n = c;
+            nsrc_tot += (int)wave_sum_f32((float)c);
+        }
+    }
+    if ((band_off && band_off[u + 1] - band_off[u] > IP_BQ) || nsrc_tot > IP_BQ) {
+        // more than the LDS holds: exact path
         if ((threadIdx.x & 63) == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
         return;
     }
@@ -689,9 +770,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         }
         return;
     }
-    // band: per-user slots of the select (band_off == nullptr) or a CSR of
-    // the entries every catalog shard sent for this user (config 4 owner)
-    const int nbd = band_off ? (int)(band_off[u + 1] - band_off[u]) : cand_cnt[u];
+    const int nbd = n_src > 0 ? 0 : band_off ? (int)(band_off[u + 1] - band_off[u]) : cand_cnt[u];
     const uint2* bd = band_off ? cand + band_off[u] : cand + (size_t)u * bandcap;
     const float2 ce = ucut[u];
     double thr = -INFINITY;
@@ -725,16 +804,26 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         }
         pcut = ce.x * (su * hdr->scale);
     }
-    // (a) compact the band into LDS (list order kept)
+    // (a) compact the band into LDS (list order kept; sources in rank order)
     int nband = 0;
-    for (int b0 = 0; b0 < nbd; b0 += WAVE) {
-        const int e = b0 + lane;
-        uint2 ent = make_uint2(0u, 0u);
-        if (e < nbd) ent = bd[e];
-        const bool kp = e < nbd && (!pre || __uint_as_float(ent.x) >= pcut);
-        const unsigned long long bal = __ballot(kp);
-        if (kp) bandq[wave][nband + __popcll(bal & ((1ull << lane) - 1ull))] = ent.y;
-        nband += __popcll(bal);
+    auto take = [&](const uint2* __restrict__ src, int cnt) {
+        for (int b0 = 0; b0 < cnt; b0 += WAVE) {
+            const int e = b0 + lane;
+            uint2 ent = make_uint2(0u, 0u);
+            if (e < cnt) ent = src[e];
+            const bool kp = e < cnt && (!pre || __uint_as_float(ent.x) >= pcut);
+            const unsigned long long bal = __ballot(kp);
+            if (kp) bandq[wave][nband + __popcll(bal & ((1ull << lane) - 1ull))] = ent.y;
+            nband += __popcll(bal);
+        }
+    };
+    if (n_src > 0) {
+        for (int s2 = 0; s2 < n_src; ++s2) {
+            const int c2 = s2 < WAVE ? __shfl(src_n, s2, WAVE) : max(0, src_cnt[(int64_t)s2 * src_users + u]);
+            if (c2 > 0) take(cand + ((size_t)s2 * src_users + u) * x_cap, c2);
+        }
+    } else {
+        take(bd, nbd);
     }
     wave_sync_lds();
     const int nitem = nband * 16;
@@ -1207,28 +1296,13 @@ __global__ __launch_bounds__(256) void ip_band_pack_kernel(int64_t n_users, int 
 // whenever at least m are) as exact lower bounds v / scl - eps, rounded down
 // to fp32, descending, -inf padded; users whose appends overflowed (or that
 // hold more than IP_SEL maxima >= lb) are flagged for the exact path.
-// Both shard kernels run persistent waves (a wave walks users wid, wid +
-// nw, ...; the next user's counts / record are loaded during this one) and
-// load a user's appended entries 256 at a time, all loads in flight at once:
-// one wave per user was bound by per-wave start-up and dependent round trips.
-constexpr int SH_WG_PER_CU = 8;
-constexpr int SH_ENT = 4;  // entries per lane per load batch
-
-__device__ __forceinline__ void sh_load(const uint2* s0, const uint2* s1, int a0, int n, int b0, int lane,
-                                        uint2 (&ent)[SH_ENT]) {
-#pragma unroll
-    for (int j = 0; j < SH_ENT; ++j) {
-        const int e = b0 + j * WAVE + lane;
-        ent[j] = e < n ? (e < a0 ? s0[e] : s1[e - a0]) : make_uint2(0u, 0u);
-    }
-}
-
 __global__ __launch_bounds__(256) void ip_shard_bound_kernel(int64_t n_users, int m2, const uint2* __restrict__ app,
                                                              const int32_t* __restrict__ acnt,
                                                              const float4* __restrict__ uinfo, int m,
-                                                             float* __restrict__ out, int32_t* __restrict__ ovf_flag) {
-    __shared__ uint32_t sel[4][IP_SEL];
-    constexpr int KE = IP_SEL / WAVE;
+                                                             float* __restrict__ out, int32_t* __restrict__ ovf_flag,
+                                                             int bandcap, uint2* __restrict__ pre,
+                                                             int32_t* __restrict__ pre_cnt) {
+    __shared__ __attribute__((aligned(16))) uint32_t sel[4][IP_SEL + 4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * 4;
     const unsigned long long lt = (1ull << lane) - 1ull;
@@ -1250,7 +1324,12 @@ __global__ __launch_bounds__(256) void ip_shard_bound_kernel(int64_t n_users, in
         const int n = ovf ? 0 : a0 + a1;
         const uint2* s0 = app + (size_t)(2 * u) * m2;
         const uint2* s1 = s0 + m2;
-        int c = 0;
+        // the same pass keeps the entries >= the scan's own cut lb - 2 eps (a
+        // superset of every later band) in the pre-band, so shard_band reads
+        // those few instead of the whole append list
+        const float own = inf.x == -INFINITY ? -INFINITY : round_down_sub(inf.x, 2.0f * inf.y);
+        uint2* pb = pre + (size_t)u * bandcap;
+        int c = 0, cp = 0;
         for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
             uint2 ent[SH_ENT];
             sh_load(s0, s1, a0, n, b0, lane, ent);
@@ -1263,49 +1342,33 @@ __global__ __launch_bounds__(256) void ip_shard_bound_kernel(int64_t n_users, in
                 const int pos = c + __popcll(bal & lt);
                 if (kp && pos < IP_SEL) sel[wave][pos] = fkey(v);
                 c += __popcll(bal);
+                const bool kq = e < n && !(v < own);
+                const unsigned long long bq = __ballot(kq);
+                const int pq = cp + __popcll(bq & lt);
+                if (kq && pq < bandcap) pb[pq] = ent[j];
+                cp += __popcll(bq);
             }
         }
         if (c > IP_SEL) ovf = true;
-        wave_sync_lds();
-        uint32_t key[KE];
-#pragma unroll
-        for (int e = 0; e < KE; ++e) key[e] = (!ovf && e * WAVE + lane < c) ? sel[wave][e * WAVE + lane] : 0u;
-        wave_sync_lds();  // the next user's keys overwrite sel
+        if (lane == 0) pre_cnt[u] = cp > bandcap ? -1 : cp;
+        if (ovf) c = 0;
+        // the m largest: every key of rank < m goes to out[rank]
         const double inv = inf.z > 0.0f ? 1.0 / (double)inf.z : 0.0;  // exact power of two
-        float ob[KE];
-#pragma unroll
-        for (int e = 0; e < KE; ++e) ob[e] = -INFINITY;
-        for (int j = 0; j < m; ++j) {
-            uint32_t mx = key[0];
-#pragma unroll
-            for (int e = 1; e < KE; ++e) mx = max(mx, key[e]);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, WAVE));
-            if (mx == 0u) break;  // fewer than m maxima: -inf padding
-            // drop one copy (lowest lane, lowest slot)
-            bool has = false;
-#pragma unroll
-            for (int e = 0; e < KE; ++e) has = has || key[e] == mx;
-            const int first = __ffsll((long long)__ballot(has)) - 1;
-            if (lane == first) {
-                bool done = false;
-#pragma unroll
-                for (int e = 0; e < KE; ++e)
-                    if (!done && key[e] == mx) {
-                        key[e] = 0u;
-                        done = true;
-                    }
+        if (lane < 4) sel[wave][c + lane] = 0u;
+        wave_sync_lds();
+        for (int b0 = 0; b0 < c; b0 += WAVE) {
+            const uint32_t mine[1] = {b0 + lane < c ? sel[wave][b0 + lane] : 0u};
+            int rank[1];
+            lds_ranks<1>(sel[wave], c, mine, b0 + lane, rank);
+            if (b0 + lane < c && rank[0] < m) {
+                const double tv = (double)fkey_inv(mine[0]) * inv - (double)inf.w;
+                float v = (float)tv;
+                if ((double)v > tv) v = nextafterf(v, -INFINITY);
+                out[u * m + rank[0]] = v;
             }
-            const double tv = (double)fkey_inv(mx) * inv - (double)inf.w;
-            float v = (float)tv;
-            if ((double)v > tv) v = nextafterf(v, -INFINITY);
-#pragma unroll
-            for (int e = 0; e < KE; ++e)
-                if (e == (j >> 6) && lane == (j & 63)) ob[e] = v;
         }
-#pragma unroll
-        for (int e = 0; e < KE; ++e)
-            if (e * WAVE + lane < m) out[u * m + e * WAVE + lane] = ob[e];
+        for (int i = c + lane; i < m; i += WAVE) out[u * m + i] = -INFINITY;  // fewer than m maxima
+        wave_sync_lds();  // the next user's keys overwrite sel
         if (lane == 0) ovf_flag[u] = ovf ? 1 : 0;
     }
 }
@@ -1324,29 +1387,37 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
                                                             const float4* __restrict__ uinfo,
                                                             const float* __restrict__ bounds, int n_lists, int m,
                                                             int bandcap, const int32_t* __restrict__ ovf_flag,
+                                                            const uint2* __restrict__ pre,
+                                                            const int32_t* __restrict__ pre_cnt,
                                                             float2* __restrict__ ucut, uint2* __restrict__ out_ent,
-                                                            int32_t* __restrict__ out_cnt) {
-    const int lane = threadIdx.x & 63;
+                                                            int32_t* __restrict__ out_cnt, int x_cap, int dbg) {
+    __shared__ __attribute__((aligned(16))) uint32_t pool[4][2 * IP_SEL + 4];  // n_lists * m <= 512
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * 4;
     const unsigned long long lt = (1ull << lane) - 1ull;
     const int tot = bounds ? n_lists * m : 0;
-    const int ec = (tot + WAVE - 1) / WAVE;
     int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     int2 ac_n = make_int2(0, 0);
     float4 inf_n = make_float4(0.f, 0.f, 0.f, 0.f);
-    int ov_n = 0;
+    int ov_n = 0, pc_n = 0;
     if (u < n_users) {
         ac_n = reinterpret_cast<const int2*>(acnt)[u];
         inf_n = uinfo[u];
         ov_n = ovf_flag[u];
+        pc_n = pre_cnt[u];
     }
     for (; u < n_users; u += nw) {
-        const int a0 = ac_n.x, n = ac_n.x + ac_n.y, ov = ov_n;
+        const int ov = ov_n, pc = pc_n;
         const float4 inf = inf_n;
+        // the pre-band when it fit, else the whole append list
+        const uint2* s0 = pc >= 0 ? pre + (size_t)u * bandcap : app + (size_t)(2 * u) * m2;
+        const uint2* s1 = app + (size_t)(2 * u) * m2 + m2;
+        const int a0 = pc >= 0 ? pc : ac_n.x, n = pc >= 0 ? pc : ac_n.x + ac_n.y;
         if (u + nw < n_users) {
             ac_n = reinterpret_cast<const int2*>(acnt)[u + nw];
             inf_n = uinfo[u + nw];
             ov_n = ovf_flag[u + nw];
+            pc_n = pre_cnt[u + nw];
         }
         if (ov || inf.z <= 0.0f) {
             if (lane == 0) {
@@ -1355,28 +1426,15 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
             }
             continue;
         }
-        const uint2* s0 = app + (size_t)(2 * u) * m2;
-        const uint2* s1 = s0 + m2;
         uint2 ent[SH_ENT];
         sh_load(s0, s1, a0, n, 0, lane, ent);  // in flight across the bound select
         float G = -INFINITY;
-        if (tot >= k) {
-            uint32_t key[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int i = e * WAVE + lane;
-                key[e] = (e < ec && i < tot) ? fkey(bounds[((int64_t)(i / m) * n_users + u) * m + (i % m)]) : 0u;
-            }
-            uint32_t x = 0;
-            for (int bit = 31; bit >= 0; --bit) {
-                const uint32_t cd = x | (1u << bit);
-                int cc = 0;
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (e < ec) cc += __popcll(__ballot(key[e] >= cd));
-                if (cc >= k) x = cd;
-            }
-            G = fkey_inv(x);
+        if (tot >= k && dbg != 1) {
+            for (int i = lane; i < tot; i += WAVE)
+                pool[wave][i] = fkey(bounds[((int64_t)(i / m) * n_users + u) * m + (i % m)]);
+            wave_sync_lds();
+            G = fkey_inv(lds_select(pool[wave], tot, k - 1, lane));
+            wave_sync_lds();
         }
         float cut = inf.x == -INFINITY ? -INFINITY : round_down_sub(inf.x, 2.0f * inf.y);
         if (G > -INFINITY) {
@@ -1386,8 +1444,8 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
             cut = fmaxf(cut, f * inf.z);  // exact power-of-two rescale
         }
         int c = 0;
-        uint2* dst = out_ent + (size_t)u * bandcap;
-        for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
+        uint2* dst = out_ent + (size_t)u * x_cap;
+        for (int b0 = 0; b0 < (dbg == 2 ? 0 : n); b0 += SH_ENT * WAVE) {
             if (b0 > 0) sh_load(s0, s1, a0, n, b0, lane, ent);
 #pragma unroll
             for (int j = 0; j < SH_ENT; ++j) {
@@ -1395,12 +1453,12 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
                 const bool kp = e < n && !(__uint_as_float(ent[j].x) < cut);
                 const unsigned long long bal = __ballot(kp);
                 const int pos = c + __popcll(bal & lt);
-                if (kp && pos < bandcap) dst[pos] = ent[j];
+                if (kp && pos < x_cap) dst[pos] = ent[j];
                 c += __popcll(bal);
             }
         }
         if (lane == 0) {
-            out_cnt[u] = c > bandcap ? -1 : c;
+            out_cnt[u] = c > x_cap ? -1 : c;
             ucut[u] = make_float2(cut == -INFINITY ? -INFINITY : cut / inf.z, inf.w);
         }
     }
@@ -1529,18 +1587,20 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
             case 1: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 2: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 3: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 4: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 4: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
             default: break;
         }
     }
-    // 8 waves share a 3-slot ring, 2 workgroups (4 waves / SIMD) per CU; k <= 32
-    // appends whole tiles (TAPP), every tile inserts (IE = 1).  Config 2
-    // (tools/scan_ab.sh, screen = scan + select): 7.1-7.2 ms; 4-wave
-    // workgroups 7.9-8.2, 4 / 6 / 8 ring slots 7.3-7.4, alternating inserts
-    // (IE = 2) 8.1 (the lagging cut doubles the appends the select reads);
-    // without any append / insert work (DBG = 1) 4.9-6.4 ms
+    // 8 waves share a 3-slot ring, 2 workgroups (4 waves / SIMD) per CU; every
+    // tile inserts (IE = 1), appends per half-block max >= tau.  Config 2
+    // (tools/scan_ab.sh / ab2.sh, screen = scan + select): 7.1 ms with 343
+    // appended maxima per user; whole-tile appends (TAPP, variant 4) 7.4-7.5
+    // with 885 (the select reads 2.6x more); 4-wave workgroups 7.9-8.2, 4 / 6
+    // / 8 ring slots 7.3-7.4, alternating inserts (IE = 2) 8.1 (the lagging
+    // cut doubles the appends); without any append / insert work (DBG = 1)
+    // 4.9-6.4 ms
     constexpr int NW = (UG == 2) ? 8 : 4, NSL = (UG == 2) ? 3 : 4;
-    launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 1, MT == 16>(users, n_users, cat, n_items, dim, k, w, s);
+    launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s);
 }
 
 template <int DP>
@@ -1574,6 +1634,11 @@ static int ip_range(IpWs& w, int64_t n_items, int dim, int64_t blk_lo, int64_t b
     return NRK_OK;
 }
 
+static int sh_dbg() {  // dev timing knob (tools/ab_sh.sh): NRK_SH_DBG, 0 = off
+    static const int v = [] { const char* e = getenv("NRK_SH_DBG"); return e ? atoi(e) : 0; }();
+    return v;
+}
+
 // persistent grid of the shard kernels: SH_WG_PER_CU 4-wave workgroups per CU
 static int sh_grid(int64_t n_users) {
     static const int n_cu = [] {
@@ -1581,7 +1646,11 @@ static int sh_grid(int64_t n_users) {
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
         return cu > 0 ? cu : 256;
     }();
-    return (int)std::max<int64_t>(1, std::min<int64_t>((n_users + 3) / 4, (int64_t)n_cu * SH_WG_PER_CU));
+    static const int per_cu = [] {  // dev A/B knob (tools/ab2.sh): NRK_SH_WG
+        const char* e = getenv("NRK_SH_WG");
+        return e && atoi(e) > 0 ? atoi(e) : SH_WG_PER_CU;
+    }();
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n_users + 3) / 4, (int64_t)n_cu * per_cu));
 }
 
 // empty shard range: no appends, uinfo.z = 0 (shard_band: no band, no cut)
@@ -1684,7 +1753,7 @@ int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* ca
         ip_all_exact_kernel<<<grid, 256, 0, s>>>(n_users, w.cnt, w.ovf_flag, w.ovf_list, w.ovf_count);
     } else {
         scan_dispatch(users, (int)n_users, cat, (int)n_items, dim, k, w, s);
-        ip_select_kernel<<<(int)((n_users + 3) / 4), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt,
+        ip_select_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt,
                                                                  w.uinfo, w.cand, w.cnt, w.ucut, w.ovf_flag,
                                                                  w.ovf_list, w.ovf_count);
 
@@ -1852,15 +1921,16 @@ int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* ca
         scan_dispatch(users, (int)n_users, reinterpret_cast<const uint8_t*>(catalog), (int)n_items, dim, k, w, s);
     }
     ip_shard_bound_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, w.m2, w.app, w.acnt, w.uinfo, m, out_bound,
-                                                           w.ovf_flag);
+                                                           w.ovf_flag, w.bandcap, w.cand, w.cnt);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
 
 int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, const float* bounds, int n_lists,
-                           int m, void* workspace, size_t workspace_bytes, void* out_ent, int32_t* out_cnt,
-                           nrk_stream_t stream) {
+                           int m, int x_cap, void* workspace, size_t workspace_bytes, void* out_ent,
+                           int32_t* out_cnt, nrk_stream_t stream) {
     clear_error();
+    NRK_REQUIRE(x_cap >= 1 && x_cap <= IP_BQ, "x_cap must be in [1, 288]");
     NRK_REQUIRE(n_users >= 0 && n_users < (1ll << 30) && n_items >= 0 && dim > 0 && dim <= 256, "bad sizes");
     NRK_REQUIRE(k >= 1 && k <= IP_KFAST, "k must be in [1, 128]");
     NRK_REQUIRE(bounds == nullptr || (n_lists >= 1 && m >= 1 && n_lists * m <= 512),
@@ -1871,7 +1941,7 @@ int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, con
     const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
     ip_shard_band_kernel<<<sh_grid(n_users), 256, 0, as_stream(stream)>>>(
         n_users, k, w.m2, w.app, w.acnt, w.uinfo, bounds, bounds ? n_lists : 0, bounds ? m : 1, w.bandcap,
-        w.ovf_flag, w.ucut, reinterpret_cast<uint2*>(out_ent), out_cnt);
+        w.ovf_flag, w.cand, w.cnt, w.ucut, reinterpret_cast<uint2*>(out_ent), out_cnt, x_cap, sh_dbg());
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -1904,6 +1974,56 @@ int nrk_ip_topk_refine_csr(const float* users, int64_t n_users, const float* ite
     ip_refine_kernel<DS4, SV><<<g2, 256, 0, s>>>(users, n_users, items, cat, n_items, dim, k, row_offset, bd, 0, \
                                                  nullptr, uc, w.ovf_flag, w.ovf_list, w.ovf_count, out_scores,   \
                                                  out_rows, out_exact, band_off)
+#define NRK_REFINE_SV(DS4)                 \
+    do {                                   \
+        if (k <= 64) NRK_REFINE(DS4, 128); \
+        else NRK_REFINE(DS4, 256);         \
+    } while (0)
+    if (dim == 32) NRK_REFINE_SV(8);
+    else if (dim == 16) NRK_REFINE_SV(4);
+    else if (dim == 64) NRK_REFINE_SV(16);
+    else NRK_REFINE_SV(0);
+#undef NRK_REFINE_SV
+#undef NRK_REFINE
+    if (n_items > 0) {
+        const int ns = next_pow2(std::max(k, 64));
+        const size_t lds = (size_t)ns * sizeof(Cand);
+        (void)hipFuncSetAttribute((const void*)ip_fallback_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        ip_fallback_kernel<<<(int)std::min<int64_t>(n_users, 256), 256, lds, s>>>(
+            users, items, n_items, dim, k, ns, row_offset, w.ovf_list, w.ovf_count, out_scores, out_rows, out_exact);
+    }
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
+int nrk_ip_topk_refine_x(const float* users, int64_t n_users, const float* items, const void* catalog,
+                         int64_t n_items, int dim, int k, int64_t row_offset, const void* band, int n_src,
+                         int64_t src_users, int x_cap, const int32_t* src_cnt, const float* ucut,
+                         const int32_t* ovf_in, float* out_scores, int32_t* out_rows, double* out_exact,
+                         void* workspace, size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    int rc = ip_check(users, n_users, items, items, n_items, dim, k, workspace, workspace_bytes);
+    if (rc != NRK_OK || n_users == 0) return rc;
+    NRK_REQUIRE(out_scores && out_rows && band && src_cnt && ucut, "null pointer");
+    NRK_REQUIRE(n_src >= 1 && x_cap >= 1 && src_users >= n_users, "need n_src >= 1, x_cap >= 1, src_users >= n_users");
+    if (k > IP_KFAST) NRK_UNSUPPORTED("the band refine needs k <= 128 (larger k: exact path, ovf_in = 1)");
+    const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
+        set_error("nrk_ip_topk_refine_x: hipMemsetAsync failed");
+        return NRK_EHIP;
+    }
+    ip_ovf_collect_kernel<<<(int)std::min<int64_t>((n_users + 255) / 256, 4096), 256, 0, s>>>(
+        n_users, ovf_in, w.ovf_flag, w.ovf_list, w.ovf_count);
+    const int g2 = (int)((n_users + 3) / 4);
+    const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
+    const uint2* bd = reinterpret_cast<const uint2*>(band);
+    const float2* uc = reinterpret_cast<const float2*>(ucut);
+#define NRK_REFINE(DS4, SV)                                                                                   \
+    ip_refine_kernel<DS4, SV><<<g2, 256, 0, s>>>(users, n_users, items, cat, n_items, dim, k, row_offset, bd, 0, \
+                                                 nullptr, uc, w.ovf_flag, w.ovf_list, w.ovf_count, out_scores,   \
+                                                 out_rows, out_exact, nullptr, n_src, src_users, x_cap, src_cnt)
 #define NRK_REFINE_SV(DS4)                 \
     do {                                   \
         if (k <= 64) NRK_REFINE(DS4, 128); \

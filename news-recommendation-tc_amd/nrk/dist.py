@@ -170,22 +170,24 @@ class HipRangeShard:
         self.blk_lo, self.blk_hi, self.n_users = int(blk_lo), int(blk_hi), int(n_users)
         self.ws = ops.ip_topk_workspace(n_users, catalog, k, catalog.items.device)
         self.rws = None
+        self.x_cap = ops.IP_X_CAP
 
     def screen(self, users, m: int):
         # scan + the m largest appended maxima as bounds (no per-shard select)
         return self.ops.ip_topk_shard_screen(users, self.cat, self.k, self.blk_lo, self.blk_hi, m, self.ws)
 
     def band(self, bounds=None):
-        # cut = max(own list bound - 2 eps, global bound - eps); entries >= cut
-        return self.ops.ip_topk_shard_band(self.n_users, self.cat, self.k, bounds, self.ws)
+        # cut = max(own list bound - 2 eps, global bound - eps); entries >= cut,
+        # x_cap slots per user for the fixed-size exchange
+        return self.ops.ip_topk_shard_band(self.n_users, self.cat, self.k, bounds, self.ws, self.x_cap)
 
     def ucut(self, lo: int, hi: int):
         return self.ops.ip_topk_ucut(self.ws, self.n_users)[lo:hi].contiguous()
 
-    def refine(self, users, band_off, band, ucut, ovf):
+    def refine(self, users, src_cnt, src_ent, ucut, ovf):
         if self.rws is None:
             self.rws = self.ops.ip_topk_workspace(users.shape[0], self.cat, self.k, users.device)
-        return self.ops.ip_topk_refine_csr(users, self.cat, self.k, band_off, band, ucut, ovf, workspace=self.rws)
+        return self.ops.ip_topk_refine_x(users, self.cat, self.k, src_cnt, src_ent, ucut, ovf, workspace=self.rws)
 
 
 def shard_blocks(n_items: int, world: int, rank: int, tile_blocks: int):
@@ -198,44 +200,28 @@ def shard_blocks(n_items: int, world: int, rank: int, tile_blocks: int):
 
 
 def exchange_bands(cnt, ent, n_users: int, group=None):
-    """The owner exchange: rank r sends, for the users of every owner block
-    shard_range(n_users, world, o), its band entries (cnt [U] int32, -1 =
-    overflowed; ent [U, cap] int64) to owner o.  Returns this rank's users'
-    (band_off int64 [n_own + 1], band int64 [nnz] (sources in rank order per
-    user), ovf int32 [n_own])."""
+    """The owner exchange, fixed size (no host-side sizes, so no sync): rank
+    r holds, per user, cnt [U] int32 (-1 = overflowed) and ent [U, X] int64
+    (X slots); user block o (rows [o * per, (o + 1) * per), per = ceil(U /
+    world), = shard_range) goes to owner o with one all_to_all of counts and
+    one of entries.  Returns this rank's (src_cnt int32 [world, per],
+    src_ent int64 [world, per, X]): source s's band of the owner's users."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    dev = cnt.device
-    lo, hi = shard_range(n_users, world, rank)
-    n_own = hi - lo
-    c = cnt.to(torch.int64)
-    take = (torch.arange(ent.shape[1], device=dev)[None, :] < c.clamp(min=0)[:, None])
+    U, X = ent.shape
     if world == 1:
-        band = ent[take]
-        off = torch.zeros(n_users + 1, dtype=torch.int64, device=dev)
-        off[1:] = torch.cumsum(c.clamp(min=0), 0)
-        return off, band, (c < 0).to(torch.int32)
+        return cnt.view(1, U), ent.view(1, U, X)
     per = -(-n_users // world)
-    cpad = torch.full((per * world,), 0, dtype=torch.int64, device=dev)
-    cpad[:n_users] = c
-    rc = torch.empty_like(cpad)
-    dist.all_to_all_single(rc, cpad, group=group)  # block s = source s's counts for my users
-    rc = rc.view(world, per)[:, :n_own]
-    flat = ent[take]  # user-major, so each owner's entries are one contiguous run
-    send = torch.stack([c.clamp(min=0)[slice(*shard_range(n_users, world, o))].sum() for o in range(world)])
-    recv = rc.clamp(min=0).sum(1)
-    sc, rcv = send.tolist(), recv.tolist()
-    buf = torch.empty(int(sum(rcv)), dtype=torch.int64, device=dev)
-    dist.all_to_all_single(buf, flat.contiguous(), rcv, sc, group=group)
-    # regroup by user (stable: sources stay in rank order inside a user)
-    who = torch.repeat_interleave(torch.arange(n_own, device=dev).repeat(world), rc.clamp(min=0).reshape(-1))
-    order = torch.sort(who, stable=True).indices
-    band = buf[order]
-    per_user = rc.clamp(min=0).sum(0)
-    off = torch.zeros(n_own + 1, dtype=torch.int64, device=dev)
-    off[1:] = torch.cumsum(per_user, 0)
-    ovf = (rc < 0).any(0).to(torch.int32)
-    return off, band, ovf
+    if per * world != U:  # pad to whole blocks
+        cp = torch.full((per * world,), 0, dtype=cnt.dtype, device=cnt.device)
+        cp[:U] = cnt
+        ep = torch.zeros((per * world, X), dtype=ent.dtype, device=ent.device)
+        ep[:U] = ent
+        cnt, ent = cp, ep
+    rc = torch.empty_like(cnt)
+    dist.all_to_all_single(rc, cnt.contiguous(), group=group)
+    re = torch.empty_like(ent)
+    dist.all_to_all_single(re, ent.contiguous(), group=group)
+    return rc.view(world, per), re.view(world, per, X)
 
 
 def catalog_sharded_owner(users, shard, k: int, group=None, exchange_bound: bool = True, mark=None):
@@ -259,19 +245,20 @@ def catalog_sharded_owner(users, shard, k: int, group=None, exchange_bound: bool
     if mark is not None:
         mark("screen")
     cnt, ent = shard.band(bounds)
-    off, band, ovf = exchange_bands(cnt, ent, U, group)
+    rc, re = exchange_bands(cnt, ent, U, group)
     if mark is not None:
         mark("exchange")
     lo, hi = shard_range(U, world, rank)
-    return shard.refine(users[lo:hi].contiguous(), off, band, shard.ucut(lo, hi), ovf)
+    ovf = (rc[:, :hi - lo] < 0).any(0).to(torch.int32)
+    return shard.refine(users[lo:hi].contiguous(), rc, re, shard.ucut(lo, hi), ovf)
 
 
 def owner_replay(users, shards, k: int, timer=None):
     """One-process replay of catalog_sharded_owner over ``shards`` (one
     HipRangeShard per emulated rank, all on this device): the two exchanges
-    become stacks / concatenations.  ``timer(phase, rank, fn)`` may wrap each
-    rank's steps (tools/catalog_replay.py times them).  Returns the full
-    (scores f32 [U, k], rows i32 [U, k], exact f64 [U, k])."""
+    become stacks.  ``timer(phase, rank, fn)`` may wrap each rank's steps
+    (tools/catalog_replay.py times them).  Returns the full (scores f32
+    [U, k], rows i32 [U, k], exact f64 [U, k])."""
     run = timer or (lambda phase, r, fn: fn())
     world = len(shards)
     U = users.shape[0]
@@ -279,25 +266,19 @@ def owner_replay(users, shards, k: int, timer=None):
     bs = [run("screen", r, lambda sh=sh: sh.screen(users, max(m, 1))) for r, sh in enumerate(shards)]
     bounds = torch.stack(bs).contiguous() if m else None
     packs = [run("band", r, lambda sh=sh: sh.band(bounds)) for r, sh in enumerate(shards)]
+    per = -(-U // world)
     outs = []
     for o in range(world):
         lo, hi = shard_range(U, world, o)
-        n_own = hi - lo
-        cnts = torch.stack([c[lo:hi].to(torch.int64) for c, _ in packs])  # [world, n_own]
-        parts, whos = [], []
+        rc = torch.zeros((world, per), dtype=torch.int32, device=users.device)
+        re = torch.zeros((world, per, packs[0][1].shape[1]), dtype=torch.int64, device=users.device)
         for src, (c, ent) in enumerate(packs):
-            cc = c[lo:hi].to(torch.int64).clamp(min=0)
-            take = torch.arange(ent.shape[1], device=ent.device)[None, :] < cc[:, None]
-            parts.append(ent[lo:hi][take])
-            whos.append(torch.repeat_interleave(torch.arange(n_own, device=ent.device), cc))
-        order = torch.sort(torch.cat(whos), stable=True).indices
-        band = torch.cat(parts)[order].contiguous()
-        off = torch.zeros(n_own + 1, dtype=torch.int64, device=users.device)
-        off[1:] = torch.cumsum(cnts.clamp(min=0).sum(0), 0)
-        ovf = (cnts < 0).any(0).to(torch.int32)
+            rc[src, :hi - lo] = c[lo:hi]
+            re[src, :hi - lo] = ent[lo:hi]
+        ovf = (rc[:, :hi - lo] < 0).any(0).to(torch.int32)
         sh = shards[o]
-        outs.append(run("refine", o, lambda sh=sh, lo=lo, hi=hi, off=off, band=band, ovf=ovf: sh.refine(
-            users[lo:hi].contiguous(), off, band, sh.ucut(lo, hi), ovf)))
+        outs.append(run("refine", o, lambda sh=sh, lo=lo, hi=hi, rc=rc, re=re, ovf=ovf: sh.refine(
+            users[lo:hi].contiguous(), rc, re, sh.ucut(lo, hi), ovf)))
     return tuple(torch.cat([x[i] for x in outs]) for i in range(3))
 
 

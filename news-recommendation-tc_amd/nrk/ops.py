@@ -270,12 +270,16 @@ def ip_topk_shard_screen(users, catalog: Catalog, k: int, blk_lo: int, blk_hi: i
     return out
 
 
-def ip_topk_shard_band(n_users, catalog: Catalog, k: int, bounds, workspace):
+IP_X_CAP = 16  # band entries per user and shard in the fixed-slot exchange
+
+
+def ip_topk_shard_band(n_users, catalog: Catalog, k: int, bounds, workspace, x_cap: int = IP_X_CAP):
     """After ip_topk_shard_screen and the all_gather of every shard's bounds
     (``bounds`` [n_lists, n_users, m] f32, or None): cut = max(own list bound
     - 2 eps, k-th largest bound - eps), the entries >= cut packed: (cnt int32
-    [n] (-1 = exact path), ent int64 [n, cap]); the cut goes to ucut."""
-    cap = _lib.lib().nrk_ip_topk_band_cap(int(k))
+    [n] (-1 = more than x_cap: exact path), ent int64 [n, x_cap]); the cut
+    goes to ucut."""
+    cap = int(x_cap)
     dev = workspace.device
     cnt = torch.empty(n_users, dtype=torch.int32, device=dev)
     ent = torch.empty((n_users, cap), dtype=torch.int64, device=dev)
@@ -283,9 +287,35 @@ def ip_topk_shard_band(n_users, catalog: Catalog, k: int, bounds, workspace):
     if bounds is not None:
         _dev(bounds, workspace)
         _need(bounds, torch.float32, (nl, n_users, m), "bounds")
-    _lib.call("nrk_ip_topk_shard_band", n_users, catalog.n, catalog.d, int(k), _ptr(bounds), nl, m,
+    _lib.call("nrk_ip_topk_shard_band", n_users, catalog.n, catalog.d, int(k), _ptr(bounds), nl, m, cap,
               _ptr(workspace), workspace.numel(), _ptr(ent), _ptr(cnt), _stream())
     return cnt, ent
+
+
+def ip_topk_refine_x(users, catalog: Catalog, k: int, src_cnt, src_ent, ucut, ovf=None, row_offset: int = 0,
+                     workspace=None):
+    """The config-4 owner's exact refine over the fixed-slot exchange:
+    ``src_ent`` int64 [n_src, src_users, x_cap] (source s's band entries of
+    user u), ``src_cnt`` int32 [n_src, src_users] (-1: exact path), users
+    [n <= src_users, D].  Returns (scores f32 [n, k], rows i32 [n, k],
+    exact f64 [n, k])."""
+    _dev(users, src_cnt, src_ent, ucut, ovf)
+    n = users.shape[0]
+    ns, su, x = src_ent.shape
+    _need(src_cnt, torch.int32, (ns, su), "src_cnt")
+    if su < n:
+        raise ValueError("src_users must cover the users")
+    dev = users.device
+    s = torch.empty((n, k), dtype=torch.float32, device=dev)
+    r = torch.empty((n, k), dtype=torch.int32, device=dev)
+    e = torch.empty((n, k), dtype=torch.float64, device=dev)
+    nb = _lib.lib().nrk_ip_topk_workspace_bytes(n, catalog.n, catalog.d, k)
+    if workspace is None or workspace.numel() < nb:
+        workspace = torch.empty(nb, dtype=torch.uint8, device=dev)
+    _lib.call("nrk_ip_topk_refine_x", _ptr(users), n, _ptr(catalog.items), _ptr(catalog.packed), catalog.n,
+              catalog.d, int(k), int(row_offset), _ptr(src_ent), ns, su, x, _ptr(src_cnt), _ptr(ucut), _ptr(ovf),
+              _ptr(s), _ptr(r), _ptr(e), _ptr(workspace), workspace.numel(), _stream())
+    return s, r, e
 
 
 def ip_topk_ucut(workspace, n_users):

@@ -128,8 +128,8 @@ class _OwnerShard:
     refine = exact top-k over the received rows ((score desc, row asc)),
     the whole catalog for users flagged overflowed (one user is forced)."""
 
-    def __init__(self, items, lo, hi, k, force_ovf=None):
-        self.items, self.lo, self.hi, self.k, self.force = items, lo, hi, k, force_ovf
+    def __init__(self, items, lo, hi, k, force_ovf=None, x_cap=64):
+        self.items, self.lo, self.hi, self.k, self.force, self.x_cap = items, lo, hi, k, force_ovf, x_cap
 
     def screen(self, users, m):
         self.users = users.double().numpy()
@@ -150,12 +150,12 @@ class _OwnerShard:
         sc = self.users @ self.items[self.lo:self.hi].astype(np.float64).T
         keep = sc >= (g[:, None] - 1e-6)
         cnt = keep.sum(1)
-        cap = max(1, int(cnt.max(initial=0)))
+        cap = self.x_cap  # fixed exchange slots; more -> -1 (exact path on the owner)
         ent = np.zeros((U, cap), np.int64)
         for u in range(U):
             rows = np.nonzero(keep[u])[0] + self.lo
-            ent[u, :len(rows)] = rows
-        cnt = cnt.astype(np.int32)
+            ent[u, :min(cap, len(rows))] = rows[:cap]
+        cnt = np.where(cnt > cap, -1, cnt).astype(np.int32)
         if self.force is not None:
             cnt[self.force] = -1
         self.g = g
@@ -164,15 +164,16 @@ class _OwnerShard:
     def ucut(self, lo, hi):
         return torch.from_numpy(np.stack([self.g[lo:hi], np.zeros(hi - lo)], 1).astype(np.float32))
 
-    def refine(self, users, off, band, ucut, ovf):
+    def refine(self, users, src_cnt, src_ent, ucut, ovf):
         u = users.double().numpy()
-        off, band, ovf = off.numpy(), band.numpy(), ovf.numpy()
+        rc, re, ovf = src_cnt.numpy(), src_ent.numpy(), ovf.numpy()
         n, k = len(u), self.k
         s = np.full((n, k), -np.finfo(np.float32).max, np.float32)
         r = np.full((n, k), -1, np.int32)
         e = np.full((n, k), -np.inf)
         for i in range(n):
-            rows = np.arange(len(self.items)) if ovf[i] else np.unique(band[off[i]:off[i + 1]])
+            got = [re[w, i, :max(0, rc[w, i])] for w in range(rc.shape[0])]
+            rows = np.arange(len(self.items)) if ovf[i] else np.unique(np.concatenate(got))
             sc = (u[i] @ self.items[rows].astype(np.float64).T) if len(rows) else np.zeros(0)
             order = np.lexsort((rows, -sc))[:k]
             m = len(order)
@@ -180,7 +181,7 @@ class _OwnerShard:
         return torch.from_numpy(s), torch.from_numpy(r), torch.from_numpy(e)
 
 
-def _owner_worker(rank, world, port, U, I, D, k, q):
+def _owner_worker(rank, world, port, U, I, D, k, q, x_cap=64):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -191,7 +192,7 @@ def _owner_worker(rank, world, port, U, I, D, k, q):
         items = rng.standard_normal((I, D)).astype(np.float32)
         items[I // 2 + 1] = items[3]  # cross-shard exact tie -> lower row must win
         lo, hi = shard_range(I, world, rank)
-        shard = _OwnerShard(items, lo, hi, k, force_ovf=2 if rank == world - 1 else None)
+        shard = _OwnerShard(items, lo, hi, k, force_ovf=2 if rank == world - 1 else None, x_cap=x_cap)
         s, r, e = catalog_sharded_owner(torch.from_numpy(users), shard, k)
         ulo, uhi = shard_range(U, world, rank)
         q.put((rank, ulo, uhi, s.numpy(), r.numpy()))
@@ -199,18 +200,20 @@ def _owner_worker(rank, world, port, U, I, D, k, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,U,I,k", [(2, 37, 101, 31), (3, 50, 400, 8), (2, 64, 40, 31), (3, 5, 7, 10)])
-def test_catalog_sharded_owner_refine_matches_single(world, U, I, k):
-    """Config 4 with owner refine: bound all_gather, band all_to_all (CSR
-    regrouping by user, sources in rank order), overflowed users on the exact
-    path -- the merged result equals one GPU's."""
+@pytest.mark.parametrize("world,U,I,k,x_cap", [(2, 37, 101, 31, 64), (3, 50, 400, 8, 64), (2, 64, 40, 31, 64),
+                                                (3, 5, 7, 10, 64), (3, 50, 400, 8, 3)])
+def test_catalog_sharded_owner_refine_matches_single(world, U, I, k, x_cap):
+    """Config 4 with owner refine: bound all_gather, the fixed-slot band
+    all_to_all (counts + x_cap entries per user and shard; users padded to
+    whole blocks), overflowed users (forced, or more than x_cap entries from
+    one shard) on the exact path -- the merged result equals one GPU's."""
     from oracle import oracle
 
     D = 16
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, U, I, D, k, q)) for r in range(world)]
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, U, I, D, k, q, x_cap)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]
