@@ -159,8 +159,9 @@ int nrk_ip_topk_band_pack(int64_t n_users, int64_t n_items, int dim, int k, cons
  * nrk_ip_topk_shard_band, after the all_gather of every shard's bounds
  * (bounds [n_lists][n_users][m], n_lists * m <= 512, or NULL): cut =
  * max(the scan's own list bound - 2 eps, k-th largest bound - eps), the
- * appended entries >= cut packed to out_ent[u * x_cap + j] (x_cap in
- * [1, 288]; out_cnt -1 when more), and ucut written for the refine. */
+ * appended half-blocks >= cut packed as uint32 global half-block ids to
+ * out_ent[u * x_cap + j] (x_cap in [1, 288]; out_cnt -1 when more), and
+ * ucut written for the refine. */
 int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
                              int k, int64_t blk_lo, int64_t blk_hi, int m, float* out_bound, void* workspace,
                              size_t workspace_bytes, nrk_stream_t stream);
@@ -168,8 +169,8 @@ int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, con
                            int m, int x_cap, void* workspace, size_t workspace_bytes, void* out_ent,
                            int32_t* out_cnt, nrk_stream_t stream);
 /* The owner's refine over the fixed-slot exchange (what nrk.dist sends: one
- * all_to_all of [n_src][src_users][x_cap] entries + one of [n_src][src_users]
- * counts, no host-side sizes): source s's entries for user u at
+ * all_to_all of [n_src][src_users][x_cap] uint32 half-block ids + one of
+ * [n_src][src_users] counts, no host-side sizes): source s's ids for user u at
  * band[(s * src_users + u) * x_cap + j], j < src_cnt[s * src_users + u]
  * (shard_band wrote at most x_cap per user, -1 when it had more: the user is
  * then in ovf_in).  Otherwise as nrk_ip_topk_refine_csr. */

@@ -187,8 +187,10 @@ __device__ __forceinline__ float partner32f(float v, int h) {
 // (jk + 1)-th largest inserted value (no run-time index into the list).
 template <int MT>
 __device__ __forceinline__ void top_insert(float (&t)[MT], float v) {
+    // t[i - 1] >= t[i], so max(t[i], min(t[i - 1], v)) is their median: one
+    // v_med3_f32 per slot instead of a max + min pair
 #pragma unroll
-    for (int i = MT - 1; i >= 1; --i) t[i] = fmaxf(t[i], fminf(t[i - 1], v));
+    for (int i = MT - 1; i >= 1; --i) t[i] = __builtin_amdgcn_fmed3f(t[i], t[i - 1], v);
     t[0] = fmaxf(t[0], v);
 }
 
@@ -818,9 +820,17 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         }
     };
     if (n_src > 0) {
+        // the exchange carries bare half-block ids (each source already
+        // filtered at its own cut, >= the global bound - eps)
+        const uint32_t* ids = reinterpret_cast<const uint32_t*>(cand);
         for (int s2 = 0; s2 < n_src; ++s2) {
             const int c2 = s2 < WAVE ? __shfl(src_n, s2, WAVE) : max(0, src_cnt[(int64_t)s2 * src_users + u]);
-            if (c2 > 0) take(cand + ((size_t)s2 * src_users + u) * x_cap, c2);
+            const uint32_t* src = ids + ((size_t)s2 * src_users + u) * x_cap;
+            for (int b0 = 0; b0 < c2; b0 += WAVE) {
+                const int e = b0 + lane;
+                if (e < c2) bandq[wave][nband + e] = src[e];
+                nband += min(WAVE, c2 - b0);
+            }
         }
     } else {
         take(bd, nbd);
@@ -1377,9 +1387,9 @@ __global__ __launch_bounds__(256) void ip_shard_bound_kernel(int64_t n_users, in
 // (-inf with fewer than k values; none without bounds), cut = max(lb - 2 eps,
 // G - eps) in the scan's scaled units (both valid: k items have exact >= G,
 // and k items have exact >= lb - eps), then the appended entries >= cut
-// compacted to out_ent[u * bandcap + j] (-1: overflowed -> the owner's exact
-// path) and the cut written to ucut for the owner's refine.  Entries keep the
-// scaled fp16 max and the GLOBAL half-block id.  uinfo.z == 0 marks an empty
+// compacted to out_ent[u * x_cap + j] as GLOBAL half-block ids (-1: more
+// than x_cap -> the owner's exact path) and the cut written to ucut for the
+// owner's refine.  uinfo.z == 0 marks an empty
 // shard: no band, no cut.
 __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int k, int m2,
                                                             const uint2* __restrict__ app,
@@ -1389,7 +1399,7 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
                                                             int bandcap, const int32_t* __restrict__ ovf_flag,
                                                             const uint2* __restrict__ pre,
                                                             const int32_t* __restrict__ pre_cnt,
-                                                            float2* __restrict__ ucut, uint2* __restrict__ out_ent,
+                                                            float2* __restrict__ ucut, uint32_t* __restrict__ out_ent,
                                                             int32_t* __restrict__ out_cnt, int x_cap, int dbg) {
     __shared__ __attribute__((aligned(16))) uint32_t pool[4][2 * IP_SEL + 4];  // n_lists * m <= 512
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1444,7 +1454,7 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
             cut = fmaxf(cut, f * inf.z);  // exact power-of-two rescale
         }
         int c = 0;
-        uint2* dst = out_ent + (size_t)u * x_cap;
+        uint32_t* dst = out_ent + (size_t)u * x_cap;
         for (int b0 = 0; b0 < (dbg == 2 ? 0 : n); b0 += SH_ENT * WAVE) {
             if (b0 > 0) sh_load(s0, s1, a0, n, b0, lane, ent);
 #pragma unroll
@@ -1453,7 +1463,7 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
                 const bool kp = e < n && !(__uint_as_float(ent[j].x) < cut);
                 const unsigned long long bal = __ballot(kp);
                 const int pos = c + __popcll(bal & lt);
-                if (kp && pos < x_cap) dst[pos] = ent[j];
+                if (kp && pos < x_cap) dst[pos] = ent[j].y;
                 c += __popcll(bal);
             }
         }
@@ -1588,6 +1598,7 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
             case 2: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 3: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 4: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 5: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 2, false>(users, n_users, cat, n_items, dim, k, w, s); return;
             default: break;
         }
     }
@@ -1941,7 +1952,7 @@ int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, con
     const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
     ip_shard_band_kernel<<<sh_grid(n_users), 256, 0, as_stream(stream)>>>(
         n_users, k, w.m2, w.app, w.acnt, w.uinfo, bounds, bounds ? n_lists : 0, bounds ? m : 1, w.bandcap,
-        w.ovf_flag, w.cand, w.cnt, w.ucut, reinterpret_cast<uint2*>(out_ent), out_cnt, x_cap, sh_dbg());
+        w.ovf_flag, w.cand, w.cnt, w.ucut, reinterpret_cast<uint32_t*>(out_ent), out_cnt, x_cap, sh_dbg());
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

@@ -201,11 +201,11 @@ def shard_blocks(n_items: int, world: int, rank: int, tile_blocks: int):
 
 def exchange_bands(cnt, ent, n_users: int, group=None):
     """The owner exchange, fixed size (no host-side sizes, so no sync): rank
-    r holds, per user, cnt [U] int32 (-1 = overflowed) and ent [U, X] int64
-    (X slots); user block o (rows [o * per, (o + 1) * per), per = ceil(U /
+    r holds, per user, cnt [U] int32 (-1 = overflowed) and ent [U, X] (X
+    slots of int32 half-block ids on the HIP path); user block o (rows [o * per, (o + 1) * per), per = ceil(U /
     world), = shard_range) goes to owner o with one all_to_all of counts and
     one of entries.  Returns this rank's (src_cnt int32 [world, per],
-    src_ent int64 [world, per, X]): source s's band of the owner's users."""
+    src_ent [world, per, X]): source s's band of the owner's users."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     U, X = ent.shape
     if world == 1:
@@ -271,7 +271,7 @@ def owner_replay(users, shards, k: int, timer=None):
     for o in range(world):
         lo, hi = shard_range(U, world, o)
         rc = torch.zeros((world, per), dtype=torch.int32, device=users.device)
-        re = torch.zeros((world, per, packs[0][1].shape[1]), dtype=torch.int64, device=users.device)
+        re = torch.zeros((world, per, packs[0][1].shape[1]), dtype=packs[0][1].dtype, device=users.device)
         for src, (c, ent) in enumerate(packs):
             rc[src, :hi - lo] = c[lo:hi]
             re[src, :hi - lo] = ent[lo:hi]

@@ -270,19 +270,19 @@ def ip_topk_shard_screen(users, catalog: Catalog, k: int, blk_lo: int, blk_hi: i
     return out
 
 
-IP_X_CAP = 16  # band entries per user and shard in the fixed-slot exchange
+IP_X_CAP = 32  # band half-block ids per user and shard in the fixed-slot exchange (4 B each)
 
 
 def ip_topk_shard_band(n_users, catalog: Catalog, k: int, bounds, workspace, x_cap: int = IP_X_CAP):
     """After ip_topk_shard_screen and the all_gather of every shard's bounds
     (``bounds`` [n_lists, n_users, m] f32, or None): cut = max(own list bound
-    - 2 eps, k-th largest bound - eps), the entries >= cut packed: (cnt int32
-    [n] (-1 = more than x_cap: exact path), ent int64 [n, x_cap]); the cut
-    goes to ucut."""
+    - 2 eps, k-th largest bound - eps), the half-blocks >= cut packed: (cnt
+    int32 [n] (-1 = more than x_cap: exact path), ids int32 [n, x_cap]
+    (global half-block ids)); the cut goes to ucut."""
     cap = int(x_cap)
     dev = workspace.device
     cnt = torch.empty(n_users, dtype=torch.int32, device=dev)
-    ent = torch.empty((n_users, cap), dtype=torch.int64, device=dev)
+    ent = torch.empty((n_users, cap), dtype=torch.int32, device=dev)
     nl, m = (0, 1) if bounds is None else (bounds.shape[0], bounds.shape[2])
     if bounds is not None:
         _dev(bounds, workspace)
@@ -295,13 +295,14 @@ def ip_topk_shard_band(n_users, catalog: Catalog, k: int, bounds, workspace, x_c
 def ip_topk_refine_x(users, catalog: Catalog, k: int, src_cnt, src_ent, ucut, ovf=None, row_offset: int = 0,
                      workspace=None):
     """The config-4 owner's exact refine over the fixed-slot exchange:
-    ``src_ent`` int64 [n_src, src_users, x_cap] (source s's band entries of
-    user u), ``src_cnt`` int32 [n_src, src_users] (-1: exact path), users
+    ``src_ent`` int32 [n_src, src_users, x_cap] (source s's band half-block
+    ids of user u), ``src_cnt`` int32 [n_src, src_users] (-1: exact path), users
     [n <= src_users, D].  Returns (scores f32 [n, k], rows i32 [n, k],
     exact f64 [n, k])."""
     _dev(users, src_cnt, src_ent, ucut, ovf)
     n = users.shape[0]
     ns, su, x = src_ent.shape
+    _need(src_ent, torch.int32, name="src_ent")
     _need(src_cnt, torch.int32, (ns, su), "src_cnt")
     if su < n:
         raise ValueError("src_users must cover the users")
