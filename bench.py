@@ -132,6 +132,17 @@ def pmc_din_pass(default_config):
     return tf["din_pass"]["traffic_bytes"]
 
 
+def max_over_ranks(x, device):
+    """The max of a host float over the ranks (the slowest rank's time); gloo
+    reduces a host tensor."""
+    import torch.distributed as dist
+
+    on_host = dist.get_backend() == "gloo"
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if on_host else device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def log(*a):
     # one write per line: ranks share the parent's stderr and run with -u, so
     # print's separate text / newline writes could interleave between ranks
@@ -509,9 +520,7 @@ def run_fused(args, device, rank, world, dist):
         dist.barrier()
     el = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([el], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el, device)
     rec_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     din_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     pairs = U * k * world
@@ -640,9 +649,7 @@ def run_din(args, device, rank, world):
         dist.barrier()
     dt = (time.perf_counter() - t0) / steps
     if dist is not None:  # whole-job rate: every rank's pass / the slowest rank's time
-        tt = torch.tensor([dt], device=device, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+        dt = max_over_ranks(dt, device)
     pass_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     value = n / dt  # every sample of the job once / the slowest rank's pass
     achieved = DIN_BYTES_PER_PAIR * n_loc / (pass_ms * 1e-3) / 1e9
@@ -956,9 +963,7 @@ def main(argv=None):
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, device)
     ms_step = elapsed / args.steps * 1e3
     tower_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     screen_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))

@@ -1005,6 +1005,128 @@ __device__ __forceinline__ uint64_t okey(double s) {
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 
+// The exact path (k > 128, overflowed bands, zero-band shards): one
+// workgroup per listed user, FB_GRID workgroups, each with its own scratch
+// row of n_items keys.  Every exact fp64 score is computed ONCE and stored
+// as the ordered key of its fp32 rounding (monotone: a larger fp32 key means
+// a larger exact score); a 3-pass radix select (11 / 11 / 10 bits, LDS
+// histograms, wave-aggregated counts) finds the kk-th largest key T; every
+// item with key >= T is a candidate (the top kk are among them), its exact
+// score is recomputed and an LDS bitonic sort on (score desc, row asc)
+// picks the kk.  Users with more candidates than the sort holds (many fp32
+// ties, e.g. an all-zero user) go to slow_list for ip_fallback_kernel.
+constexpr int FB_GRID = 256;
+
+__global__ __launch_bounds__(256) void ip_exact_kernel(
+    const float* __restrict__ users, const float* __restrict__ items, int64_t n_items, int dim, int k, int ns,
+    int64_t row_offset, const int32_t* __restrict__ ovf_list, const int32_t* __restrict__ ovf_count,
+    float* __restrict__ out_s, int32_t* __restrict__ out_r, double* __restrict__ out_e,
+    uint32_t* __restrict__ scratch, int32_t* __restrict__ slow_list, int32_t* __restrict__ slow_count) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    Cand* sel = reinterpret_cast<Cand*>(dyn);
+    __shared__ unsigned int hist[2048];
+    __shared__ unsigned int part[256];
+    __shared__ int s_bin, s_krem, s_eq, sel_n;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int cnt = *ovf_count;
+    const int kk = (int)(n_items < k ? n_items : k);
+    uint32_t* key = scratch + (size_t)blockIdx.x * n_items;
+    for (int qi = blockIdx.x; qi < cnt; qi += gridDim.x) {
+        const int64_t u = ovf_list[qi];
+        const float* uv = users + u * dim;
+        for (int64_t r = tid; r < n_items; r += 256) key[r] = fkey((float)exact_dot(uv, items + r * dim, dim));
+        __syncthreads();
+        uint32_t prefix = 0, mask = 0;
+        int krem = kk;
+        for (int p = 0; p < 3; ++p) {
+            const int wbits = p < 2 ? 11 : 10, sh = p == 0 ? 21 : (p == 1 ? 10 : 0);
+            const uint32_t nbm = (1u << wbits) - 1u;
+            for (int i = tid; i < 2048; i += 256) hist[i] = 0u;
+            __syncthreads();
+            for (int64_t r0 = 0; r0 < n_items; r0 += 256) {
+                const int64_t r = r0 + tid;
+                const uint32_t kv = r < n_items ? key[r] : 0u;
+                const bool act = r < n_items && (kv & mask) == prefix;
+                const uint32_t b = (kv >> sh) & nbm;
+                unsigned long long pend = __ballot(act);
+                while (pend) {  // one LDS atomic per distinct bin of the wave
+                    const int l = __ffsll((long long)pend) - 1;
+                    const uint32_t bl = (uint32_t)__shfl((int)b, l, WAVE);
+                    const unsigned long long same = __ballot(act && b == bl) & pend;
+                    if (lane == l) atomicAdd(&hist[bl], (unsigned int)__popcll(same));
+                    pend &= ~same;
+                }
+            }
+            __syncthreads();
+            {
+                unsigned int sum = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sum += hist[8 * tid + j];
+                part[tid] = sum;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int cum = 0, t = 255;
+                for (; t > 0; --t) {
+                    if (cum + (int)part[t] >= krem) break;
+                    cum += part[t];
+                }
+                int b = 8 * t + 7;
+                for (; b > 8 * t; --b) {
+                    if (cum + (int)hist[b] >= krem) break;
+                    cum += hist[b];
+                }
+                s_bin = b;
+                s_krem = krem - cum;
+                s_eq = (int)hist[b];
+            }
+            __syncthreads();
+            prefix |= (uint32_t)s_bin << sh;
+            mask |= nbm << sh;
+            krem = s_krem;
+        }
+        // prefix = T, the kk-th largest key; s_eq = #(key == T)
+        const int n_cand = (kk - krem) + s_eq;
+        if (n_cand > ns) {
+            if (tid == 0) slow_list[atomicAdd(slow_count, 1)] = (int32_t)u;
+            __syncthreads();
+            continue;
+        }
+        if (tid == 0) sel_n = 0;
+        __syncthreads();
+        for (int64_t r = tid; r < n_items; r += 256) {
+            if (key[r] >= prefix) {
+                const int pos = atomicAdd(&sel_n, 1);
+                sel[pos] = Cand{exact_dot(uv, items + r * dim, dim), (int32_t)r};
+            }
+        }
+        __syncthreads();
+        for (int i = n_cand + tid; i < ns; i += 256) sel[i] = Cand{-INFINITY, INT32_MAX};
+        __syncthreads();
+        for (int sz = 2; sz <= ns; sz <<= 1) {
+            for (int st = sz >> 1; st > 0; st >>= 1) {
+                for (int i = tid; i < ns / 2; i += 256) {
+                    const int lo = 2 * st * (i / st) + (i % st), hi = lo + st;
+                    const bool up = (lo & sz) == 0;
+                    const Cand a = sel[lo], b = sel[hi];
+                    if (up ? better(b, a) : better(a, b)) {
+                        sel[lo] = b;
+                        sel[hi] = a;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int i = tid; i < k; i += 256) {
+            const bool ok = i < kk;
+            out_s[u * k + i] = ok ? (float)sel[i].s : -FLT_MAX;
+            out_r[u * k + i] = ok ? (int32_t)(sel[i].row + row_offset) : -1;
+            if (out_e) out_e[u * k + i] = ok ? sel[i].s : -INFINITY;
+        }
+        __syncthreads();
+    }
+}
+
 // One workgroup per listed user: the k-th largest exact key by an 8-bit
 // radix select over the whole catalog (8 histogram passes), then the items
 // above it plus the first ties in row order (k winners in all), ordered by
@@ -1500,6 +1622,8 @@ struct IpWs {
     int32_t* acnt;
     uint2* cand;
     uint2* app;
+    uint32_t* fbk;      // exact path: FB_GRID scratch rows of n_items keys
+    int32_t* slow_list;  // exact path: users with too many fp32 ties (count at ovf_count[1])
     int bandcap, m2;
     int blk_lo, blk_hi;  // block range screened (config-4 shards), set by the caller
     size_t bytes;
@@ -1562,6 +1686,10 @@ static IpWs ip_ws_layout(void* base, int64_t n_users, int64_t n_items, int k, in
     off += align256((size_t)n_users * w.bandcap * sizeof(uint2));
     w.app = reinterpret_cast<uint2*>(p + off);
     off += align256((size_t)n_users * 2 * (size_t)w.m2 * sizeof(uint2));
+    w.fbk = reinterpret_cast<uint32_t*>(p + off);
+    off += align256((size_t)std::min<int64_t>(n_users, FB_GRID) * (size_t)n_items * sizeof(uint32_t));
+    w.slow_list = reinterpret_cast<int32_t*>(p + off);
+    off += align256((size_t)n_users * sizeof(int32_t));
     w.bytes = off;
     return w;
 }
@@ -1672,6 +1800,21 @@ __global__ void ip_empty_range_kernel(int64_t n_users, int32_t* __restrict__ acn
         acnt[2 * u + 1] = 0;
         uinfo[u] = make_float4(-INFINITY, 0.0f, 0.0f, 0.0f);
     }
+}
+
+// the exact path of the users in ovf_list (see ip_exact_kernel)
+static void launch_exact(const float* users, int64_t n_users, const float* items, int64_t n_items, int dim, int k,
+                         int64_t row_offset, const IpWs& w, float* out_s, int32_t* out_r, double* out_e,
+                         hipStream_t s) {
+    const int ns = next_pow2(std::max(k, 64));
+    const size_t lds = (size_t)ns * sizeof(Cand);
+    (void)hipFuncSetAttribute((const void*)ip_exact_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)ip_fallback_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const int grid = (int)std::min<int64_t>(n_users, FB_GRID);
+    ip_exact_kernel<<<grid, 256, lds, s>>>(users, items, n_items, dim, k, ns, row_offset, w.ovf_list, w.ovf_count,
+                                           out_s, out_r, out_e, w.fbk, w.slow_list, w.ovf_count + 1);
+    ip_fallback_kernel<<<grid, 256, lds, s>>>(users, items, n_items, dim, k, ns, row_offset, w.slow_list,
+                                              w.ovf_count + 1, out_s, out_r, out_e);
 }
 
 }  // namespace nrk
@@ -1810,17 +1953,7 @@ int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
     }
 #undef NRK_REFINE_SV
 #undef NRK_REFINE
-    if (n_items > 0) {
-        const int ns = next_pow2(std::max(k, 64));
-        const size_t lds = (size_t)ns * sizeof(Cand);
-        (void)hipFuncSetAttribute((const void*)ip_fallback_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        const int grid = (int)std::min<int64_t>(n_users, k > IP_KFAST ? 2048 : 256);
-
-        ip_fallback_kernel<<<grid, 256, lds, s>>>(users, items, n_items, dim, k, ns, row_offset, w.ovf_list,
-                                                  w.ovf_count, out_scores, out_rows, out_exact);
-
-    }
+    if (n_items > 0) launch_exact(users, n_users, items, n_items, dim, k, row_offset, w, out_scores, out_rows, out_exact, s);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -1996,14 +2129,7 @@ int nrk_ip_topk_refine_csr(const float* users, int64_t n_users, const float* ite
     else NRK_REFINE_SV(0);
 #undef NRK_REFINE_SV
 #undef NRK_REFINE
-    if (n_items > 0) {
-        const int ns = next_pow2(std::max(k, 64));
-        const size_t lds = (size_t)ns * sizeof(Cand);
-        (void)hipFuncSetAttribute((const void*)ip_fallback_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        ip_fallback_kernel<<<(int)std::min<int64_t>(n_users, 256), 256, lds, s>>>(
-            users, items, n_items, dim, k, ns, row_offset, w.ovf_list, w.ovf_count, out_scores, out_rows, out_exact);
-    }
+    if (n_items > 0) launch_exact(users, n_users, items, n_items, dim, k, row_offset, w, out_scores, out_rows, out_exact, s);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -2046,14 +2172,7 @@ int nrk_ip_topk_refine_x(const float* users, int64_t n_users, const float* items
     else NRK_REFINE_SV(0);
 #undef NRK_REFINE_SV
 #undef NRK_REFINE
-    if (n_items > 0) {
-        const int ns = next_pow2(std::max(k, 64));
-        const size_t lds = (size_t)ns * sizeof(Cand);
-        (void)hipFuncSetAttribute((const void*)ip_fallback_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        ip_fallback_kernel<<<(int)std::min<int64_t>(n_users, 256), 256, lds, s>>>(
-            users, items, n_items, dim, k, ns, row_offset, w.ovf_list, w.ovf_count, out_scores, out_rows, out_exact);
-    }
+    if (n_items > 0) launch_exact(users, n_users, items, n_items, dim, k, row_offset, w, out_scores, out_rows, out_exact, s);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

@@ -33,6 +33,30 @@ import torch
 import torch.distributed as dist
 
 
+def _staged(t, group=None):
+    """gloo with device tensors: collectives staged through host memory (the
+    one-GPU rehearsals of the N-rank layouts; RCCL takes device tensors)."""
+    return t.is_cuda and dist.is_initialized() and dist.get_backend(group) == "gloo"
+
+
+def all_gather_into(out, inp, group=None):
+    if _staged(out, group):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def all_to_all(out, inp, out_splits=None, in_splits=None, group=None):
+    if _staged(out, group):
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
 def shard_range(n: int, world: int, rank: int):
     """Contiguous split, ceil(n / world) per rank (the last ranks may be short)."""
     per = -(-n // world)
@@ -102,7 +126,7 @@ def gather_users(u_local, n_users: int, group=None):
     if u_local.shape[0] < per:
         send = torch.zeros((per,) + tuple(u_local.shape[1:]), dtype=u_local.dtype, device=u_local.device)
         send[: u_local.shape[0]] = u_local
-    dist.all_gather_into_tensor(buf, send.contiguous(), group=group)
+    all_gather_into(buf, send.contiguous(), group=group)
     if per * world == n_users:
         return buf
     parts = [buf[r * per: r * per + (shard_range(n_users, world, r)[1] - shard_range(n_users, world, r)[0])]
@@ -136,7 +160,7 @@ def catalog_sharded_topk(users, shard, k: int, group=None, merge=None, exchange_
     bounds = None
     if m:
         bounds = torch.empty((world * b.shape[0], b.shape[1]), dtype=b.dtype, device=b.device)
-        dist.all_gather_into_tensor(bounds, b.contiguous(), group=group)
+        all_gather_into(bounds, b.contiguous(), group=group)
         bounds = bounds.view(world, b.shape[0], b.shape[1])
     e, r = shard.finish(users, bounds)  # [U, k] each
     if world == 1:
@@ -150,8 +174,8 @@ def catalog_sharded_topk(users, shard, k: int, group=None, merge=None, exchange_
     rr = torch.empty_like(r)
     # block s of the send buffer = users of rank s; block s of the receive
     # buffer = shard s's lists for this rank's users
-    dist.all_to_all_single(re, e.contiguous(), group=group)
-    dist.all_to_all_single(rr, r.contiguous(), group=group)
+    all_to_all(re, e.contiguous(), group=group)
+    all_to_all(rr, r.contiguous(), group=group)
     s_, r_, x_ = merge(re.view(world, per, k), rr.view(world, per, k), k)
     lo, hi = shard_range(U, world, rank)
     return s_[: hi - lo], r_[: hi - lo], x_[: hi - lo]
@@ -218,9 +242,9 @@ def exchange_bands(cnt, ent, n_users: int, group=None):
         ep[:U] = ent
         cnt, ent = cp, ep
     rc = torch.empty_like(cnt)
-    dist.all_to_all_single(rc, cnt.contiguous(), group=group)
+    all_to_all(rc, cnt.contiguous(), group=group)
     re = torch.empty_like(ent)
-    dist.all_to_all_single(re, ent.contiguous(), group=group)
+    all_to_all(re, ent.contiguous(), group=group)
     return rc.view(world, per), re.view(world, per, X)
 
 
@@ -240,7 +264,7 @@ def catalog_sharded_owner(users, shard, k: int, group=None, exchange_bound: bool
     bounds = None
     if m:
         bounds = torch.empty((world * b.shape[0], b.shape[1]), dtype=b.dtype, device=b.device)
-        dist.all_gather_into_tensor(bounds, b.contiguous(), group=group)
+        all_gather_into(bounds, b.contiguous(), group=group)
         bounds = bounds.view(world, b.shape[0], b.shape[1])
     if mark is not None:
         mark("screen")
