@@ -939,7 +939,11 @@ def main(argv=None):
                             wl["hist_len"], wl["w0"], wl["b0"], wl["w1"], wl["b1"])
         if ev is not None:
             ev[1].record()
-        ops.ip_topk_screen(u, cat, K, ws)
+        # the screen as its two launches, so the roofline times the MFMA scan alone
+        ops.ip_topk_scan(u, cat, K, ws)
+        if ev is not None:
+            ev[5].record()
+        ops.ip_topk_select(u, cat, K, ws)
         if ev is not None:
             ev[2].record()
         ops.ip_topk_finish(u, cat, K, ws, out_s, out_r)
@@ -951,7 +955,7 @@ def main(argv=None):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -969,13 +973,16 @@ def main(argv=None):
     screen_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     finish_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
     refine_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
+    scan_ms = None if catalog_mode else float(np.mean([e[1].elapsed_time(e[5]) for e in evs]))
+    select_ms = None if catalog_mode else float(np.mean([e[5].elapsed_time(e[2]) for e in evs]))
     pairs = U * args.topk * (1 if catalog_mode else world)
     value = pairs / (elapsed / args.steps)
 
     # catalog mode: this rank's screen covers its own item blocks
     n_scr = (min(I, bhi * 32) - blo * 32) if catalog_mode else cat.n
     flops = 2.0 * U * n_scr * D
-    achieved = flops / (screen_ms * 1e-3) / 1e12
+    kernel_ms = screen_ms if catalog_mode else scan_ms
+    achieved = flops / (kernel_ms * 1e-3) / 1e12
     default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and world == 1
     traffic = pmc_traffic(["nrk::ip_scan_kernel<"], default_cfg)
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
@@ -983,10 +990,10 @@ def main(argv=None):
                 "traffic": round(traffic) if traffic else None,
                 "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r03_traffic.json; "
                                 "null when absent or measured on other kernel sources)",
-                "kernel": ("ip_scan_kernel (fp16 MFMA 32x32x16 screen) + ip_select + bound all_gather, this "
-                           "rank's item blocks" if catalog_mode else
-                           "ip_scan_kernel (fp16 MFMA 32x32x16 screen) + ip_select_kernel"),
-                "kernel_ms": round(screen_ms, 4),
+                "kernel": ("ip_scan_kernel (fp16 MFMA 32x32x16 screen) + ip_shard_bound_kernel + bound all_gather, "
+                           "this rank's item blocks" if catalog_mode else
+                           "ip_scan_kernel (fp16 MFMA 32x32x16 screen), HIP events around its launch"),
+                "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_flop_per_launch": flops,
                 "busy": pmc_busy(["nrk::ip_scan_kernel", "nrk::ip_select_kernel", "nrk::ip_refine_kernel",
                                   "nrk::tt_user_kernel"], default_cfg),
@@ -1057,8 +1064,8 @@ def main(argv=None):
             "phase_ms": ({"tower_and_gather": round(tower_ms, 4), "screen_and_bound_exchange": round(screen_ms, 4),
                           "band_pack_and_all_to_all": round(finish_ms, 4), "owner_refine": round(refine_ms, 4)}
                          if catalog_mode else
-                         {"tower": round(tower_ms, 4), "screen": round(screen_ms, 4),
-                          "finish": round(finish_ms, 4)}),
+                         {"tower": round(tower_ms, 4), "screen": round(screen_ms, 4), "scan": round(scan_ms, 4),
+                          "select": round(select_ms, 4), "finish": round(finish_ms, 4)}),
             "roofline": roofline, "cpu_baseline": cpu, "din": din, "itemcf": itemcf, "plugins": plugins,
             "host": host_info(),
         }

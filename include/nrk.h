@@ -104,6 +104,12 @@ int nrk_ip_topk(const float* users, int64_t n_users, const float* items, const v
 int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
                        int dim, int k, void* workspace, size_t workspace_bytes,
                        nrk_stream_t stream);
+/* nrk_ip_topk_screen in its two launches (timing / profiling of the MFMA
+ * scan alone): nrk_ip_topk_scan, then nrk_ip_topk_select, same arguments. */
+int nrk_ip_topk_scan(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim, int k,
+                     void* workspace, size_t workspace_bytes, nrk_stream_t stream);
+int nrk_ip_topk_select(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim, int k,
+                       void* workspace, size_t workspace_bytes, nrk_stream_t stream);
 int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
                        const void* catalog, int64_t n_items,
                        int dim, int k, int64_t row_offset, float* out_scores, int32_t* out_rows,

@@ -1880,10 +1880,11 @@ static int ip_check(const float* users, int64_t n_users, const float* items, con
     return NRK_OK;
 }
 
-int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
-                             int dim, int k, int64_t blk_lo, int64_t blk_hi, void* workspace,
-                             size_t workspace_bytes, nrk_stream_t stream) {
-    clear_error();
+// phases: 1 = the MFMA scan, 2 = the select (or the exact-path / empty
+// marking), 3 = both
+static int screen_phases(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim, int k,
+                         int64_t blk_lo, int64_t blk_hi, void* workspace, size_t workspace_bytes,
+                         nrk_stream_t stream, int phases) {
     int rc = ip_check(users, n_users, (const float*)catalog, catalog, n_items, dim, k, workspace,
                       workspace_bytes);
     if (rc != NRK_OK || n_users == 0) return rc;
@@ -1892,28 +1893,51 @@ int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* ca
     if (rc != NRK_OK) return rc;
     if (blk_hi == blk_lo) n_items = 0;  // empty range: every output row is padding
     hipStream_t s = as_stream(stream);
-    if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
-        set_error("nrk_ip_topk_screen: hipMemsetAsync failed");
-        return NRK_EHIP;
-    }
     const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
-    if (n_items == 0) {
-        // nothing to search: every output row is padding
-        (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * sizeof(int32_t), s);
-        (void)hipMemsetAsync(w.ovf_flag, 0, (size_t)n_users * sizeof(int32_t), s);
-        (void)hipMemsetAsync(w.ucut, 0xFF, (size_t)n_users * sizeof(float2), s);  // NaN cut: no band
-    } else if (k > IP_KFAST) {
-        const int grid = (int)std::min<int64_t>((n_users + 255) / 256, 4096);
-        ip_all_exact_kernel<<<grid, 256, 0, s>>>(n_users, w.cnt, w.ovf_flag, w.ovf_list, w.ovf_count);
-    } else {
-        scan_dispatch(users, (int)n_users, cat, (int)n_items, dim, k, w, s);
-        ip_select_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt,
-                                                                 w.uinfo, w.cand, w.cnt, w.ucut, w.ovf_flag,
-                                                                 w.ovf_list, w.ovf_count);
-
+    if ((phases & 1) && n_items > 0 && k <= IP_KFAST) scan_dispatch(users, (int)n_users, cat, (int)n_items, dim, k, w, s);
+    if (phases & 2) {
+        if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
+            set_error("nrk_ip_topk_screen: hipMemsetAsync failed");
+            return NRK_EHIP;
+        }
+        if (n_items == 0) {
+            // nothing to search: every output row is padding
+            (void)hipMemsetAsync(w.cnt, 0, (size_t)n_users * sizeof(int32_t), s);
+            (void)hipMemsetAsync(w.ovf_flag, 0, (size_t)n_users * sizeof(int32_t), s);
+            (void)hipMemsetAsync(w.ucut, 0xFF, (size_t)n_users * sizeof(float2), s);  // NaN cut: no band
+        } else if (k > IP_KFAST) {
+            const int grid = (int)std::min<int64_t>((n_users + 255) / 256, 4096);
+            ip_all_exact_kernel<<<grid, 256, 0, s>>>(n_users, w.cnt, w.ovf_flag, w.ovf_list, w.ovf_count);
+        } else {
+            ip_select_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt, w.uinfo,
+                                                              w.cand, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,
+                                                              w.ovf_count);
+        }
     }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
+}
+
+int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
+                             int dim, int k, int64_t blk_lo, int64_t blk_hi, void* workspace,
+                             size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    return screen_phases(users, n_users, catalog, n_items, dim, k, blk_lo, blk_hi, workspace, workspace_bytes, stream,
+                         3);
+}
+
+int nrk_ip_topk_scan(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim, int k,
+                     void* workspace, size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    return screen_phases(users, n_users, catalog, n_items, dim, k, 0, n_blocks_of(n_items), workspace,
+                         workspace_bytes, stream, 1);
+}
+
+int nrk_ip_topk_select(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim, int k,
+                       void* workspace, size_t workspace_bytes, nrk_stream_t stream) {
+    clear_error();
+    return screen_phases(users, n_users, catalog, n_items, dim, k, 0, n_blocks_of(n_items), workspace,
+                         workspace_bytes, stream, 2);
 }
 
 int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items,

@@ -41,6 +41,8 @@ SIGNATURES = {
     "nrk_ip_topk_screen_range": (INT, [P, I64, P, I64, INT, INT, I64, I64, P, SZ, P]),
     "nrk_ip_topk_band_cap": (INT, [INT]),
     "nrk_ip_topk_band_pack": (INT, [I64, I64, INT, INT, P, SZ, P, P, P]),
+    "nrk_ip_topk_scan": (INT, [P, I64, P, I64, INT, INT, P, SZ, P]),
+    "nrk_ip_topk_select": (INT, [P, I64, P, I64, INT, INT, P, SZ, P]),
     "nrk_ip_topk_shard_screen": (INT, [P, I64, P, I64, INT, INT, I64, I64, INT, P, P, SZ, P]),
     "nrk_ip_topk_shard_band": (INT, [I64, I64, INT, INT, P, INT, INT, INT, P, SZ, P, P, P]),
     "nrk_ip_topk_refine_x": (INT, [P, I64, P, P, I64, INT, INT, I64, P, INT, I64, INT, P, P, P, P, P, P, P, SZ,

@@ -208,6 +208,20 @@ def ip_topk_screen(users, catalog: Catalog, k: int, workspace):
               _ptr(workspace), workspace.numel(), _stream())
 
 
+def ip_topk_scan(users, catalog: Catalog, k: int, workspace):
+    """ip_topk_screen's first launch alone: the fp16 MFMA scan (appends)."""
+    _dev(users, workspace)
+    _lib.call("nrk_ip_topk_scan", _ptr(users), users.shape[0], _ptr(catalog.packed), catalog.n, catalog.d, k,
+              _ptr(workspace), workspace.numel(), _stream())
+
+
+def ip_topk_select(users, catalog: Catalog, k: int, workspace):
+    """ip_topk_screen's second launch alone: the per-user select (band)."""
+    _dev(users, workspace)
+    _lib.call("nrk_ip_topk_select", _ptr(users), users.shape[0], _ptr(catalog.packed), catalog.n, catalog.d, k,
+              _ptr(workspace), workspace.numel(), _stream())
+
+
 def ip_topk_finish(users, catalog: Catalog, k: int, workspace, out_scores, out_rows,
                    out_exact=None, row_offset: int = 0):
     """Phase 2 of ip_topk (exact rescoring + ordering) into preallocated outputs."""
