@@ -486,6 +486,31 @@ typedef struct {
 int nrk_ctx_features(const nrk_ctx_tables* tables, const nrk_ctx_spec* spec, double* out_raw, int32_t* out_codes,
                      nrk_stream_t stream);
 
+/* ---- multi-GPU exchanges over RCCL --------
+ * For a caller binding the C ABI without torch.distributed: one process per
+ * GPU; rank 0 makes a unique id (nrk_rccl_unique_id_bytes() bytes), the
+ * caller sends it to every rank, each rank calls nrk_rccl_comm_init with its
+ * device current.  Communicators are opaque (void*).
+ * nrk_rccl_topk_allgather: the merge protocol -- all-gather every shard's
+ *   top-k_in of every user (fp64 + global row) into the caller's
+ *   gather_exact / gather_rows [n_ranks][n_users][k_in], then nrk_topk_merge.
+ *   Replaces: nothing (a Faiss search is single-index).
+ * nrk_rccl_bound_allgather / nrk_rccl_band_alltoall: the owner protocol's
+ *   two exchanges (bounds [n_users, m] f32; counts [n_ranks * per] and
+ *   x_cap ids per user, user block o to rank o), around
+ *   nrk_ip_topk_shard_screen / _shard_band / _refine_x. */
+int nrk_rccl_unique_id_bytes(void);
+int nrk_rccl_get_unique_id(void* out_id);
+int nrk_rccl_comm_init(void** out_comm, int n_ranks, const void* id, int rank);
+int nrk_rccl_comm_destroy(void* comm);
+int nrk_rccl_topk_allgather(void* comm, const double* in_exact, const int32_t* in_rows, int64_t n_users, int k_in,
+                            int k_out, double* gather_exact, int32_t* gather_rows, float* out_scores,
+                            int32_t* out_rows, double* out_exact, nrk_stream_t stream);
+int nrk_rccl_bound_allgather(void* comm, const float* bounds, int64_t n_users, int m, float* out,
+                             nrk_stream_t stream);
+int nrk_rccl_band_alltoall(void* comm, const int32_t* cnt, const int32_t* ids, int64_t per, int x_cap,
+                           int32_t* out_cnt, int32_t* out_ids, nrk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -736,6 +736,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
     constexpr int RS = DS4 + 1;  // staged row stride in float4 (one float4 of padding)
     __shared__ float4 stage[DS4 > 0 ? 4 : 1][DS4 > 0 ? 64 * RS : 1];
     __shared__ uint32_t bandq[4][SV + 32 > IP_BQ ? SV + 32 : IP_BQ];
+    __shared__ __attribute__((aligned(16))) float ushl[4][DS4 > 0 ? 1 : 256];  // DS4 == 0: the user's fp16 values
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users || ovf_flag[u]) return;
@@ -955,6 +956,18 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
         }
         while (kc > ko) exact_round(kc - ko < WAVE ? kc - ko : WAVE);
     } else {
+        // any dim: the fp16 prefilter reads each band item's packed pieces
+        // (pad_dim / 16 k-steps of two 16-B pieces) against the user's fp16
+        // values held in LDS, and only items reaching the cut get the exact
+        // fp64 dot (per lane, the oracle's sequential order)
+        const int dpc = pad_dim(dim), dskc = dpc / 16;
+        if (pre) {
+            float ua = 0.0f;
+            for (int d = 0; d < dim; ++d) ua = fmaxf(ua, fabsf(uv[d]));
+            const float s2 = pow2_scale(ua);
+            for (int d = lane; d < dpc; d += WAVE) ushl[wave][d] = d < dim ? (float)(_Float16)(uv[d] * s2) : 0.0f;
+            wave_sync_lds();
+        }
         for (int base = 0; base < nitem; base += WAVE) {
             const int idx = base + lane;
             bool keep = false;
@@ -966,6 +979,22 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
                 const int64_t rr = (int64_t)(qv >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (qv & 1);
                 if (rr < n_items) row = (int32_t)rr;
                 keep = rr < n_items;
+                if (keep && pre) {
+                    const uint8_t* bp = catalog + (size_t)(rr >> 5) * (64 * dpc);
+                    const int il = (int)(rr & 31);
+                    float acc = 0.0f;
+                    for (int st = 0; st < dskc; ++st) {
+                        const f16x8 h0 = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(bp + st * 1024 + il * 16));
+                        const f16x8 h1 =
+                            __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(bp + st * 1024 + (il + 32) * 16));
+                        const float* us = &ushl[wave][16 * st];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) acc = fmaf((float)h0[e], us[e], acc);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) acc = fmaf((float)h1[e], us[8 + e], acc);
+                    }
+                    keep = acc >= pcut;
+                }
                 if (keep) {
                     sd = exact_dot(uv, items + (int64_t)row * dim, dim);
                     keep = sd >= thr;

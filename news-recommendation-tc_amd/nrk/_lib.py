@@ -42,6 +42,13 @@ SIGNATURES = {
     "nrk_ip_topk_band_cap": (INT, [INT]),
     "nrk_ip_topk_band_pack": (INT, [I64, I64, INT, INT, P, SZ, P, P, P]),
     "nrk_ip_topk_scan": (INT, [P, I64, P, I64, INT, INT, P, SZ, P]),
+    "nrk_rccl_unique_id_bytes": (INT, []),
+    "nrk_rccl_get_unique_id": (INT, [P]),
+    "nrk_rccl_comm_init": (INT, [P, INT, P, INT]),
+    "nrk_rccl_comm_destroy": (INT, [P]),
+    "nrk_rccl_topk_allgather": (INT, [P, P, P, I64, INT, INT, P, P, P, P, P, P]),
+    "nrk_rccl_bound_allgather": (INT, [P, P, I64, INT, P, P]),
+    "nrk_rccl_band_alltoall": (INT, [P, P, P, I64, INT, P, P, P]),
     "nrk_ip_topk_select": (INT, [P, I64, P, I64, INT, INT, P, SZ, P]),
     "nrk_ip_topk_shard_screen": (INT, [P, I64, P, I64, INT, INT, I64, I64, INT, P, P, SZ, P]),
     "nrk_ip_topk_shard_band": (INT, [I64, I64, INT, INT, P, INT, INT, INT, P, SZ, P, P, P]),

@@ -436,6 +436,9 @@ class DinParams:
         self.mlp_w1, self.mlp_b1 = d("mlp.2.weight"), d("mlp.2.bias")
         self.mlp_w2 = d("mlp.4.weight").reshape(-1).contiguous()
         self.mlp_b2 = d("mlp.4.bias")
+        for name in ("att_w0", "att_b0", "att_w1", "att_b1", "mlp_w0", "mlp_b0", "mlp_w1", "mlp_b1", "mlp_w2",
+                     "mlp_b2"):
+            _finite(getattr(self, name), f"DIN weight {name}")
         self.h1, self.h2 = self.mlp_w0.shape[0], self.mlp_w1.shape[0]
         in_dim = 32 * (self.n_user + self.n_ctx + 2 * self.n_item)
         if self.att_w0.shape != (36, 4 * 32 * self.n_item) or self.mlp_w0.shape[1] != in_dim:
