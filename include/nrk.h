@@ -72,8 +72,10 @@ int nrk_tt_item_fwd(const float* item_table, int64_t n_item_rows, int dim, const
 /* Brute-force inner-product top-K (replaces faiss.IndexFlatIP)           */
 /* ---------------------------------------------------------------------- */
 
-/* Catalog = the "index": a bf16 copy of the item rows in MFMA-fragment
- * order plus the max row norm.  Replaces faiss.IndexFlatIP(d).add(items)
+/* Catalog = the "index": an fp16 copy of the item rows (power-of-two scaled)
+ * in MFMA-fragment order, a header (max row norm, scale, max rounding error)
+ * and, for dim <= 64, a half-block-major fp16 copy read by the refine's
+ * prefilter.  Replaces faiss.IndexFlatIP(d).add(items)
  * (youtubednn_recaller.py:493-494).  items stays the fp32 source of truth
  * for exact rescoring and must outlive the catalog. */
 size_t nrk_ip_catalog_bytes(int64_t n_items, int dim);

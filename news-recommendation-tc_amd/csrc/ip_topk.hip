@@ -78,6 +78,15 @@ __device__ __forceinline__ float pow2_scale(float maxabs) {
 static inline size_t catalog_body_bytes(int64_t n_items, int dp) {
     return (size_t)n_blocks_of(n_items) * 64u * (size_t)dp;
 }
+// dims <= 64: a second fp16 copy after the header, half-block major (the
+// refine's prefilter): half-block q = 2 b + h holds the 16 items
+// 32 b + (r & 3) + 8 (r >> 2) + 4 h, r = 0..15, each as dp contiguous fp16 --
+// one 16 dp-B run per half-block instead of half of every 128-B line of the
+// fragment-ordered body
+__host__ __device__ static inline bool catalog_has_hb(int dp) { return dp <= 64; }
+__host__ __device__ static inline size_t catalog_hb_offset(int64_t n_items, int dp) {
+    return (size_t)n_blocks_of(n_items) * 64u * (size_t)dp + CATALOG_HDR;
+}
 
 // --------------------------------------------------------- catalog build --
 // Thread -> one 16-byte fragment: block b, k-step s, lane l:
@@ -108,6 +117,32 @@ __global__ void catalog_pack_kernel(const float* __restrict__ items, int64_t n_i
         o.z = v[4] | ((uint32_t)v[5] << 16);
         o.w = v[6] | ((uint32_t)v[7] << 16);
         out[t] = o;
+    }
+}
+
+// Thread -> one 16-byte piece of the half-block-major copy: half-block q,
+// item r, dims 8p + [0, 8).
+__global__ void catalog_pack_hb_kernel(const float* __restrict__ items, int64_t n_items, int dim,
+                                       int dp, const CatalogHdr* __restrict__ hdr,
+                                       uint4* __restrict__ out) {
+    const int ppr = dp / 8;  // pieces per item row
+    const float scale = hdr->scale;
+    const int64_t total = n_blocks_of(n_items) * 2 * 16 * ppr;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(t % ppr);
+        const int r = (int)((t / ppr) & 15);
+        const int64_t q = t / ppr / 16;
+        const int64_t item = (q >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (q & 1);
+        uint16_t v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int d = 8 * p + e;
+            const float f = (item < n_items && d < dim) ? items[item * dim + d] : 0.0f;
+            v[e] = __builtin_bit_cast(uint16_t, (_Float16)(f * scale));
+        }
+        out[t] = make_uint4(v[0] | ((uint32_t)v[1] << 16), v[2] | ((uint32_t)v[3] << 16),
+                            v[4] | ((uint32_t)v[5] << 16), v[6] | ((uint32_t)v[7] << 16));
     }
 }
 
@@ -859,21 +894,26 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
             idx = idx < nitem ? idx : nitem - 1;
             return bandq[wave][idx > 0 ? idx >> 4 : 0];
         };
+        // the prefilter reads the half-block-major copy: item r of band
+        // entry qv is the 8 DS4-B row at ((qv * 16 + r) * 8 DS4), the 16
+        // items of a half-block one contiguous run
+        const uint8_t* hbc = catalog ? catalog + catalog_hb_offset(n_items, 4 * DS4) : nullptr;
+        int64_t hoff = 0;
         auto item_row = [&](int base, uint32_t qv, int32_t& row, bool& inb) {
             const int idx = base + lane, r = idx & 15;
             const int64_t rr = (int64_t)(qv >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (qv & 1);
             inb = idx < nitem && rr < n_items;
             row = inb ? (int32_t)rr : 0;
+            hoff = inb ? ((int64_t)qv * 16 + r) * (8 * DS4) : 0;
         };
-        auto pieces = [&](int32_t row) {
+        auto pieces = [&](int32_t) {
             if (pre) {
-                const int blk = row >> 5, il = row & 31;
-                const uint8_t* bp = catalog + (size_t)blk * (64 * 4 * DS4);
+                const uint8_t* bp = hbc + hoff;
 #pragma unroll
                 for (int st = 0; st < DSK; ++st)
 #pragma unroll
                     for (int hh = 0; hh < 2; ++hh)
-                        pc[2 * st + hh] = *reinterpret_cast<const uint4*>(bp + st * 1024 + (il + 32 * hh) * 16);
+                        pc[2 * st + hh] = *reinterpret_cast<const uint4*>(bp + 32 * st + 16 * hh);
             }
         };
         int kc = 0, ko = 0;  // ring fill / read positions (wave-uniform)
@@ -1756,8 +1796,18 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
             case 3: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 4: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
             case 5: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 2, false>(users, n_users, cat, n_items, dim, k, w, s); return;
+            // 128 users per wave (half the LDS fragment reads and barriers per MFMA), 2 waves / SIMD
+            case 6: launch_scan_v<DP, 4, 3, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 7: launch_scan_v<DP, 4, 4, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
+            case 9: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
             default: break;
         }
+        // default at D = 32, k <= 32 (BASELINE config 2): 8 waves x 128 users
+        // (UG = 4) per workgroup at 2 waves / SIMD -- every LDS fragment read
+        // and tile barrier serves twice the MFMAs of the 64-user waves
+        // (variant 9): config-2 screen 6.8-7.0 vs 7.0-7.2 ms
+        launch_scan_v<DP, 8, 3, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s);
+        return;
     }
     // 8 waves share a 3-slot ring, 2 workgroups (4 waves / SIMD) per CU; every
     // tile inserts (IE = 1), appends per half-block max >= tau.  Config 2
@@ -1854,7 +1904,8 @@ extern "C" {
 
 size_t nrk_ip_catalog_bytes(int64_t n_items, int dim) {
     if (n_items < 0 || dim <= 0 || dim > 256) return 0;
-    return catalog_body_bytes(n_items, pad_dim(dim)) + CATALOG_HDR;
+    const int dp = pad_dim(dim);
+    return catalog_body_bytes(n_items, dp) + CATALOG_HDR + (catalog_has_hb(dp) ? catalog_body_bytes(n_items, dp) : 0);
 }
 
 int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* catalog,
@@ -1884,6 +1935,10 @@ int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* cat
         const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
         catalog_pack_kernel<<<grid, 256, 0, s>>>(items, n_items, dim, dp, hdr,
                                                  reinterpret_cast<uint4*>(catalog));
+        if (catalog_has_hb(dp))
+            catalog_pack_hb_kernel<<<grid, 256, 0, s>>>(
+                items, n_items, dim, dp, hdr,
+                reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(catalog) + catalog_hb_offset(n_items, dp)));
     }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
