@@ -327,6 +327,221 @@ __global__ __launch_bounds__(256) void din_att_h_kernel(
             }
 }
 
+// din_att_h2: the T <= 64 path (one t-tile per wave) of din_att_h with a
+// two-deep gather pipeline.  gfx9 retires vector memory operations in issue
+// order and the compiler can only count them statically when none is
+// conditional: one conditional load or store between a prefetch and its use
+// makes the wait for ANY older load a vmcnt(0), which drains the prefetch
+// (din_att_h pays this at the end of every sample).  Here every vector memory
+// operation of the loop is unconditional --
+//   * indices and rows are read at clamped addresses (sample min(b, b_end-1),
+//     slot 0 for t >= T): real, finite rows whose h lands in padding rows
+//     that are never stored;
+//   * h is written with buffer stores whose out-of-range offsets the hardware
+//     drops (t >= T, j >= 36);
+//   * statistics accumulate every (t, j) of the tile; only real ones are
+//     written --
+// and the k rows / q bits of sample b + 2G are issued into the registers
+// sample b just converted (two register sets, the loop unrolled by two: no
+// copy of an in-flight register), after the indices of b + 3G.
+template <typename TT, int NI>
+__global__ __launch_bounds__(256, 2) void din_att_h2_kernel(
+    const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
+    const int32_t* __restrict__ item_idx, const int32_t* __restrict__ hist_idx, int64_t N,
+    int64_t S, int G, int T, const float* __restrict__ prep, const float* __restrict__ att_b0,
+    float* __restrict__ h_out, double* __restrict__ partial) {
+    constexpr int ID = NI * DIN_E;
+    constexpr bool F32 = sizeof(TT) == 4;
+    constexpr int NSLOT = DIN_JT * NI * 64;
+    constexpr int SPT = (NSLOT + 255) / 256;
+    constexpr int RW = F32 ? 2 : 1;
+    typedef uint32_t u4n __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) din_half8 mf[2][DIN_JT][NI][64];
+    __shared__ float qs[ID];
+    __shared__ float cs[48];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const float* A = prep;
+    const float* Bq = prep + DIN_H * ID;
+    const float* P = prep + 2 * DIN_H * ID;
+    const DinScales sc = *reinterpret_cast<const DinScales*>(prep + 3 * DIN_H * ID);
+
+    float ra[SPT][8], rp[SPT][8];
+#pragma unroll
+    for (int m = 0; m < SPT; ++m) {
+        const int q = tid + 256 * m;
+        const int jt = q / (NI * 64), s = (q / 64) % NI, l = q % 64;
+        const int j = 16 * jt + (l & 15), k = 32 * s + 8 * (l >> 4);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const bool ok = q < NSLOT && j < DIN_H;
+            ra[m][e] = ok ? A[j * ID + k + e] : 0.0f;
+            rp[m][e] = ok ? P[j * ID + k + e] : 0.0f;
+        }
+    }
+    constexpr int CQ = ID / 4;
+    float rbq[CQ];
+    {
+        const int j = tid >> 2, k0 = (tid & 3) * CQ;
+#pragma unroll
+        for (int e = 0; e < CQ; ++e) rbq[e] = j < DIN_H ? Bq[j * ID + k0 + e] : 0.0f;
+    }
+    double ssum[DIN_JT][4], ssq[DIN_JT][4];
+#pragma unroll
+    for (int b = 0; b < DIN_JT; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ssum[b][r] = ssq[b][r] = 0.0;
+
+    const int64_t seg = blockIdx.x / G;
+    const int64_t b_end = (seg + 1) * S < N ? (seg + 1) * S : N;
+    const int64_t b0 = seg * S + blockIdx.x % G;
+    int64_t rbs[NI];
+#pragma unroll
+    for (int s = 0; s < NI; ++s) rbs[s] = row_base[n_user + s];
+    const int qf = tid < ID ? tid / DIN_E : 0;
+    const int64_t qbase = row_base[n_user + qf];
+    const float b0j = (tid >> 2) < DIN_H ? att_b0[tid >> 2] : 0.0f;
+    const int trow = 16 * wv + (lane & 15);
+    const int tg = trow < T ? trow : 0;  // gather slot (padding rows read slot 0)
+    auto clampb = [&](int64_t bb) { return bb < b_end ? bb : b_end - 1; };
+    auto hidx_of = [&](int64_t bb, int32_t (&hi)[NI]) {
+        const int32_t* p = hist_idx + (clampb(bb) * T + tg) * NI;
+#pragma unroll
+        for (int s = 0; s < NI; ++s) hi[s] = p[s];
+    };
+    auto qi_of = [&](int64_t bb) -> int32_t { return item_idx[clampb(bb) * NI + qf]; };
+    auto rows_of = [&](const int32_t (&hi)[NI], u4n (&raw)[NI][RW]) {
+#pragma unroll
+        for (int s = 0; s < NI; ++s) {
+            const u4n* p = reinterpret_cast<const u4n*>(table + (rbs[s] + hi[s]) * DIN_E + 8 * (lane >> 4));
+#pragma unroll
+            for (int w = 0; w < RW; ++w) raw[s][w] = p[w];
+        }
+    };
+    auto qbits_of = [&](int32_t qi) -> uint32_t { return table_bits(table + (qbase + qi) * DIN_E + tid % DIN_E); };
+
+    // prologue: every index first, then rows / q of b0 (set A) and b0 + G (set B)
+    u4n rawA[NI][RW], rawB[NI][RW];
+    uint32_t qvA, qvB;
+    int32_t hiA[NI], hiB[NI], qiA, qiB;
+    {
+        int32_t h0[NI], h1[NI];
+        hidx_of(b0, h0);
+        const int32_t q0 = qi_of(b0);
+        hidx_of(b0 + G, h1);
+        const int32_t q1 = qi_of(b0 + G);
+        rows_of(h0, rawA);
+        qvA = qbits_of(q0);
+        rows_of(h1, rawB);
+        qvB = qbits_of(q1);
+    }
+    hidx_of(b0 + 2 * G, hiA);
+    qiA = qi_of(b0 + 2 * G);
+
+    // sample b from (raw, qv); then issue b + 3G's indices into (hn, qn) and
+    // b + 2G's rows / q (indices hc, qc) into (raw, qv)
+    auto step = [&](int64_t b, u4n (&raw)[NI][RW], uint32_t& qv, const int32_t (&hc)[NI], const int32_t& qc,
+                    int32_t (&hn)[NI], int32_t& qn) {
+        // (1) this wave's k rows -> A fragments; q -> LDS
+        din_half8 ahi[NI], alo[NI];
+#pragma unroll
+        for (int s = 0; s < NI; ++s) {
+            float v[8];
+            if (F32) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = __uint_as_float(raw[s][0][e]);
+                    v[4 + e] = __uint_as_float(raw[s][RW - 1][e]);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    v[2 * i] = __uint_as_float(raw[s][0][i] << 16);
+                    v[2 * i + 1] = __uint_as_float(raw[s][0][i] & 0xFFFF0000u);
+                }
+            }
+            split8(v, sc.s_k, ahi[s], alo[s]);
+        }
+        if (tid < ID) qs[tid] = F32 ? __uint_as_float(qv) : __uint_as_float(qv << 16);
+        // (2) prefetch: indices of b + 3G, then rows / q of b + 2G into the
+        // registers just consumed
+        hidx_of(b + 3 * G, hn);
+        qn = qi_of(b + 3 * G);
+        rows_of(hc, raw);
+        qv = qbits_of(qc);
+        lds_barrier();
+        // (3) M_b fragments and c_b
+#pragma unroll
+        for (int m = 0; m < SPT; ++m) {
+            const int q = tid + 256 * m;
+            if (q < NSLOT) {
+                const int jt = q / (NI * 64), s = (q / 64) % NI, l = q % 64;
+                const int k = 32 * s + 8 * (l >> 4);
+                float mv[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) mv[e] = fmaf(rp[m][e], qs[k + e], ra[m][e]);
+                din_half8 hi, lo;
+                split8(mv, sc.s_m, hi, lo);
+                mf[0][jt][s][l] = hi;
+                mf[1][jt][s][l] = lo;
+            }
+        }
+        {
+            const int k0 = (tid & 3) * CQ;
+            float c = 0.0f;
+#pragma unroll
+            for (int e = 0; e < CQ; ++e) c = fmaf(rbq[e], qs[k0 + e], c);
+            c += __shfl_xor(c, 1, WAVE);
+            c += __shfl_xor(c, 2, WAVE);
+            const int j = tid >> 2;
+            if ((tid & 3) == 0 && j < DIN_H) cs[j] = c + b0j;
+        }
+        lds_barrier();
+        // (4) MFMAs + epilogue: unconditional buffer stores (dropped out of
+        // range), statistics of every (t, j) of the tile
+        if (16 * wv < T) {
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(h_out + b * T * DIN_H, 0, T * DIN_H * 4, 0x00020000);
+#pragma unroll
+            for (int jt = 0; jt < DIN_JT; ++jt) {
+                din_f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int s = 0; s < NI; ++s) {
+                    const din_half8 bh = mf[0][jt][s][lane];
+                    const din_half8 bl = mf[1][jt][s][lane];
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[s], bh, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[s], bl, acc, 0, 0, 0);
+                    if (F32) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[s], bh, acc, 0, 0, 0);
+                }
+                const int j = 16 * jt + (lane & 15);
+                const float cj = j < DIN_H ? cs[j] : 0.0f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int t = 16 * wv + 4 * (lane >> 4) + r;
+                    const float v = acc[r] * sc.inv + cj;
+                    const int off = (t < T && j < DIN_H) ? (t * DIN_H + j) * 4 : 0x7FFFFFF0;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, off, 0, 0);
+                    ssum[jt][r] += (double)v;
+                    ssq[jt][r] += (double)v * (double)v;
+                }
+            }
+        }
+    };
+    for (int64_t b = b0; b < b_end; b += 2 * G) {
+        step(b, rawA, qvA, hiA, qiA, hiB, qiB);
+        if (b + G >= b_end) break;
+        step(b + G, rawB, qvB, hiB, qiB, hiA, qiA);
+    }
+    // per-workgroup partial column sums (every real (t, j) is owned by one lane)
+    double2* dst = reinterpret_cast<double2*>(partial) + (size_t)blockIdx.x * T * DIN_H;
+#pragma unroll
+    for (int jt = 0; jt < DIN_JT; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int t = 16 * wv + 4 * (lane >> 4) + r;
+            const int j = 16 * jt + (lane & 15);
+            if (t < T && j < DIN_H) dst[t * DIN_H + j] = make_double2(ssum[jt][r], ssq[jt][r]);
+        }
+}
+
 // Scales for the split-fp16 products: s_k puts max|table| at <= 2^14, s_m
 // puts max|M_b| <= max(|A| + |P| max|q|) at <= 2^14 (powers of two, so
 // inv = 1 / (s_k s_m) is exact).
@@ -1187,6 +1402,15 @@ __global__ void din_prepare_kernel(const float* __restrict__ w0, int ID, float* 
 // din_att_h workgroups per segment: about 6144 in the whole grid (24 per CU,
 // measured best of 1024...32768 at config 3), at most 512 per segment and
 // never more than the segment has samples
+// att_h variant (dev A/B knob NRK_DIN_ATT: 0 = din_att_h, 1 = din_att_h2, the default)
+static int din_att_v() {
+    static int v = [] {
+        const char* e = getenv("NRK_DIN_ATT");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 static inline int din_att_groups(int64_t N, int64_t S) {
     const int64_t n_seg = (N + S - 1) / S;
     int64_t g = (6144 + n_seg - 1) / n_seg;
@@ -1349,7 +1573,11 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     const float* pf = reinterpret_cast<const float*>(prep);
 #define NRK_ATT_H(TT, NI)                                                                              \
     do {                                                                                               \
-        if (T <= 64)                                                                                   \
+        if (T <= 64 && din_att_v() == 1 && (sizeof(TT) == 2 || NI < 4))                                \
+            din_att_h2_kernel<TT, NI><<<(unsigned)nb_att, 256, 0, s>>>(                                \
+                reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G,    \
+                T, pf, att_b0, w.h, w.hpart);                                                       \
+        else if (T <= 64)                                                                              \
             din_att_h_kernel<TT, NI, 1><<<(unsigned)nb_att, 256, 0, s>>>(                              \
                 reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G,    \
                 T, pf, att_b0, w.h, w.hpart);                                                       \
