@@ -757,7 +757,7 @@ __device__ __forceinline__ double exact_dot(const float* __restrict__ a, const f
 // DS4 = 0: the generic per-lane gather.  SV = exact survivors held per user
 // (SV / 64 per lane in the final sort).
 template <int DS4, int SV>
-__global__ __launch_bounds__(256) void ip_refine_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ip_refine_kernel(
     const float* __restrict__ users, int64_t n_users, const float* __restrict__ items,
     const uint8_t* __restrict__ catalog, int64_t n_items, int dim, int k, int64_t row_offset,
     const uint2* __restrict__ cand, int bandcap, const int32_t* __restrict__ cand_cnt,
@@ -769,7 +769,7 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
     __shared__ Cand surv[4][SV];
     __shared__ int32_t krow[DS4 > 0 ? 4 : 1][DS4 > 0 ? IP_KRING : 1];
     constexpr int RS = DS4 + 1;  // staged row stride in float4 (one float4 of padding)
-    __shared__ float4 stage[DS4 > 0 ? 4 : 1][DS4 > 0 ? 64 * RS : 1];
+    __shared__ float4 stage[DS4 > 0 ? 4 : 1][DS4 > 0 ? 32 * RS : 1];  // half a round (32 rows) at a time
     __shared__ uint32_t bandq[4][SV + 32 > IP_BQ ? SV + 32 : IP_BQ];
     __shared__ __attribute__((aligned(16))) float ushl[4][DS4 > 0 ? 1 : 256];  // DS4 == 0: the user's fp16 values
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -917,41 +917,46 @@ __global__ __launch_bounds__(256) void ip_refine_kernel(
             }
         };
         int kc = 0, ko = 0;  // ring fill / read positions (wave-uniform)
+        // rows staged 32 at a time (half the LDS of a whole round: four
+        // workgroups per CU instead of three)
         auto exact_round = [&](int m) {
             const int32_t rl = lane < m ? krow[wave][(ko + lane) & (IP_KRING - 1)] : -1;
-            float4 v[DS4];
-            bool okv[DS4];
-#pragma unroll
-            for (int it = 0; it < DS4; ++it) {
-                const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
-                const int r_item = __shfl(rl, item, WAVE);
-                okv[it] = r_item >= 0;
-                v[it] = reinterpret_cast<const float4*>(items + (int64_t)(okv[it] ? r_item : 0) * dim)[part];
-            }
-#pragma unroll
-            for (int it = 0; it < DS4; ++it) {
-                const int g = it * 64 + lane, item = g / DS4, part = g % DS4;
-                stage[wave][item * RS + part] = okv[it] ? v[it] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            wave_sync_lds();
             double sd = 0.0;
             bool keep = false;
-            if (rl >= 0) {
-                const float4* a4 = reinterpret_cast<const float4*>(uv);
-                const float4* b4 = &stage[wave][lane * RS];
-                double acc = 0.0;
 #pragma unroll
-                for (int t = 0; t < DS4; ++t) {
-                    const float4 x = a4[t], y = b4[t];
-                    acc += (double)x.x * (double)y.x;
-                    acc += (double)x.y * (double)y.y;
-                    acc += (double)x.z * (double)y.z;
-                    acc += (double)x.w * (double)y.w;
+            for (int hp = 0; hp < 2; ++hp) {
+                float4 v[DS4 / 2];
+                bool okv[DS4 / 2];
+#pragma unroll
+                for (int it = 0; it < DS4 / 2; ++it) {
+                    const int g = it * 64 + lane, item = 32 * hp + g / DS4, part = g % DS4;
+                    const int r_item = __shfl(rl, item, WAVE);
+                    okv[it] = r_item >= 0;
+                    v[it] = reinterpret_cast<const float4*>(items + (int64_t)(okv[it] ? r_item : 0) * dim)[part];
                 }
-                sd = acc + 0.0;
-                keep = sd >= thr;
+#pragma unroll
+                for (int it = 0; it < DS4 / 2; ++it) {
+                    const int g = it * 64 + lane, part = g % DS4;
+                    stage[wave][(g / DS4) * RS + part] = okv[it] ? v[it] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                wave_sync_lds();
+                if ((lane >> 5) == hp && rl >= 0) {
+                    const float4* a4 = reinterpret_cast<const float4*>(uv);
+                    const float4* b4 = &stage[wave][(lane & 31) * RS];
+                    double acc = 0.0;
+#pragma unroll
+                    for (int t = 0; t < DS4; ++t) {
+                        const float4 x = a4[t], y = b4[t];
+                        acc += (double)x.x * (double)y.x;
+                        acc += (double)x.y * (double)y.y;
+                        acc += (double)x.z * (double)y.z;
+                        acc += (double)x.w * (double)y.w;
+                    }
+                    sd = acc + 0.0;
+                    keep = sd >= thr;
+                }
+                wave_sync_lds();  // the stage is rewritten next
             }
-            __builtin_amdgcn_wave_barrier();  // the stage is rewritten next round
             push(keep, sd, rl);
             ko += m;
         };
