@@ -886,6 +886,174 @@ __global__ __launch_bounds__(256, 2) void din_wh_kernel(
     flush();
 }
 
+// din_wh2: din_wh with the Dice statistics in LDS instead of registers.
+// Workgroup (seg, g) takes a contiguous run of ONE Dice batch (segment), so
+// its four waves share the segment's (mean, 1 / (std + 1e-8)) table, loaded
+// once into LDS; the per-wave Dice stage holds T rows (dynamic LDS).  That
+// frees 64 VGPRs per lane: 3 waves / SIMD at T <= 50 (48 KB of LDS per
+// workgroup) instead of 2, for this latency-bound gather kernel.  Same
+// arithmetic, same order (bit-identical wh).
+template <typename TT, int NI, int NCH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void din_wh2_kernel(
+    const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
+    const int32_t* __restrict__ hist_idx, const float* __restrict__ mask, int64_t B, int64_t S,
+    int T, int GW, const float* __restrict__ h, const float2* __restrict__ hinv_all,
+    const float* __restrict__ att_w1, const float* __restrict__ att_b1, float* __restrict__ wh,
+    unsigned int* __restrict__ segmax) {
+    constexpr int ID = NI * DIN_E;
+    typedef float f4n __attribute__((ext_vector_type(4)));
+    typedef uint32_t u4n __attribute__((ext_vector_type(4)));
+    constexpr int EPP = 16 / (int)sizeof(TT);
+    constexpr int PPR = DIN_E / EPP;
+    constexpr int LPT = NI * PPR;
+    constexpr int TG = 64 / LPT;
+    constexpr int R = 64 / TG < 6 ? 64 / TG : 6;  // loads per lane in flight per round (VGPRs: 3 waves / SIMD)
+    constexpr int HQ = DIN_H / 4;
+    extern __shared__ __attribute__((aligned(16))) float wh2_lds[];
+    const int nq = T * HQ;
+    f4n* smean = reinterpret_cast<f4n*>(wh2_lds);       // [nq]
+    f4n* sinv = smean + nq;                             // [nq]
+    float* dscb = reinterpret_cast<float*>(sinv + nq);  // [4][T * DIN_H]
+    int32_t* rrb = reinterpret_cast<int32_t*>(dscb + 4 * T * DIN_H);  // [4][64 * NI]
+    float* wsb = reinterpret_cast<float*>(rrb + 4 * 64 * NI);         // [4][64]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float* dsc = dscb + wv * T * DIN_H;
+    int32_t* rr_s = rrb + wv * 64 * NI;
+    float* w_s = wsb + wv * 64;
+    const int tg = lane / LPT, gf = (lane / PPR) % NI, gc = lane % PPR;
+    const int64_t seg = blockIdx.x / GW, g = blockIdx.x % GW;
+    const int64_t s0 = seg * S, s1 = (seg + 1) * S < B ? (seg + 1) * S : B;
+    const int64_t cw = (s1 - s0 + GW - 1) / GW;          // samples per workgroup
+    const int64_t pw = (cw + 3) / 4;                      // per wave
+    const int64_t wb = s0 + g * cw + wv * pw;
+    const int64_t wg_end = s0 + (g + 1) * cw < s1 ? s0 + (g + 1) * cw : s1;
+    const int64_t b0 = wb;
+    const int64_t b1e = wb + pw < wg_end ? wb + pw : wg_end;
+    // this segment's statistics -> LDS (chunk q = columns 4q .. 4q + 3)
+    {
+        const f4n* st = reinterpret_cast<const f4n*>(hinv_all + (size_t)seg * T * DIN_H);
+        for (int q = threadIdx.x; q < nq; q += 256) {
+            const f4n a = st[2 * q], b = st[2 * q + 1];
+            smean[q] = f4n{a.x, a.z, b.x, b.z};
+            sinv[q] = f4n{a.y, a.w, b.y, b.w};
+        }
+    }
+    __syncthreads();
+    const float ab1 = att_b1[0];
+    const bool act = lane < T;
+    int64_t rbs[NI];
+#pragma unroll
+    for (int f = 0; f < NI; ++f) rbs[f] = row_base[n_user + f];
+    float mx = 0.0f;
+    f4n hq[NCH];
+    int32_t ix[NI];
+    float mk;
+    const f4n* hdummy = reinterpret_cast<const f4n*>(hinv_all);
+    auto load_mask = [&](int64_t bb) -> float { return (bb < b1e && act) ? mask[bb * T + lane] : 0.0f; };
+    auto fetch = [&](int64_t bb, float mbb) {
+        const bool ok = bb < b1e;
+        const f4n* hr = reinterpret_cast<const f4n*>(h + (size_t)(ok ? bb : 0) * T * DIN_H);
+        const uint64_t live = __builtin_amdgcn_ballot_w64(mbb != 0.0f);
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int q = 64 * i + lane;
+            const bool on = ok && q < nq && ((live >> (q / HQ)) & 1ull);
+            hq[i] = *(on ? hr + q : hdummy);
+        }
+#pragma unroll
+        for (int f = 0; f < NI; ++f) ix[f] = ok && act ? hist_idx[((size_t)bb * T + lane) * NI + f] : 0;
+        mk = mbb;
+    };
+    float mk_n = load_mask(b0);
+    fetch(b0, mk_n);
+    mk_n = load_mask(b0 + 1);
+    for (int64_t b = b0; b < b1e; ++b) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int q = 64 * i + lane;
+            if (q < nq) {
+                const f4n m4 = smean[q], i4 = sinv[q];
+                f4n d;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) d[e] = dice_fast(hq[i][e], m4[e], i4[e]);
+                *reinterpret_cast<f4n*>(&dsc[4 * q]) = d;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float w = 0.0f;
+        if (act) {
+            const f4n* dr = reinterpret_cast<const f4n*>(&dsc[lane * DIN_H]);
+            float sacc = 0.0f;
+#pragma unroll
+            for (int c = 0; c < HQ; ++c) {
+                const f4n d = dr[c];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sacc += att_w1[4 * c + e] * d[e];
+            }
+            w = (sacc + ab1) * mk;
+        }
+        w_s[lane] = w;
+#pragma unroll
+        for (int f = 0; f < NI; ++f) rr_s[lane * NI + f] = act ? (int32_t)(rbs[f] + ix[f]) : 0;
+        const uint64_t nz = __builtin_amdgcn_ballot_w64(w != 0.0f);
+        const int te = nz ? 64 - __builtin_clzll(nz) : 0;
+        asm volatile("" ::: "memory");
+        fetch(b + 1, mk_n);
+        mk_n = load_mask(b + 2);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float acc[EPP];
+#pragma unroll
+        for (int e = 0; e < EPP; ++e) acc[e] = 0.0f;
+        for (int t0 = 0; t0 < te; t0 += TG * R) {
+            u4n raw[R];
+            float wt[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int t = t0 + TG * u + tg;
+                const int tc = t < te ? t : te - 1;
+                wt[u] = t < te ? w_s[tc] : 0.0f;
+                const int32_t r = rr_s[tc * NI + gf];
+                raw[u] = *reinterpret_cast<const u4n*>(table + (int64_t)r * DIN_E + gc * EPP);
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                if constexpr (sizeof(TT) == 4) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[e] = fmaf(wt[u], __uint_as_float(raw[u][e]), acc[e]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc[2 * i] = fmaf(wt[u], __uint_as_float(raw[u][i] << 16), acc[2 * i]);
+                        acc[2 * i + 1] = fmaf(wt[u], __uint_as_float(raw[u][i] & 0xFFFF0000u), acc[2 * i + 1]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int off = LPT; off < 64; off <<= 1)
+#pragma unroll
+            for (int e = 0; e < EPP; ++e) acc[e] += __shfl_xor(acc[e], off, WAVE);
+        if (tg == 0) {
+            f4n* o = reinterpret_cast<f4n*>(wh + (size_t)b * ID + gf * DIN_E + gc * EPP);
+#pragma unroll
+            for (int v = 0; v < EPP / 4; ++v) o[v] = f4n{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
+        }
+#pragma unroll
+        for (int e = 0; e < EPP; ++e) mx = fmaxf(mx, fabsf(acc[e]));
+    }
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) mx = fmaxf(mx, __shfl_xor(mx, k, WAVE));
+    if (lane == 0 && b0 < b1e) atomicMax(segmax + seg, __float_as_uint(mx));
+}
+
+static inline size_t din_wh2_lds(int T, int NI) {
+    return (size_t)2 * T * (DIN_H / 4) * 16 + (size_t)4 * T * DIN_H * 4 + (size_t)4 * 64 * NI * 4 + 4 * 64 * 4;
+}
+
 // ----------------------------------------------------- 4'. mlp1 (fast) --
 // z1 = [user | ctx | cand | wh] W0^T + b0 (DIN.py:279-282, Linear(IN -> h1))
 // without materialising the MLP input: every 32-wide feature is one k-step
@@ -1403,6 +1571,15 @@ __global__ void din_prepare_kernel(const float* __restrict__ w0, int ID, float* 
 // measured best of 1024...32768 at config 3), at most 512 per segment and
 // never more than the segment has samples
 // att_h variant (dev A/B knob NRK_DIN_ATT: 0 = din_att_h, 1 = din_att_h2, the default)
+// wh variant (dev A/B knob NRK_DIN_WH: 0 = din_wh, 1 = din_wh2, the default)
+static int din_wh_v() {
+    static int v = [] {
+        const char* e = getenv("NRK_DIN_WH");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 static int din_att_v() {
     static int v = [] {
         const char* e = getenv("NRK_DIN_ATT");
@@ -1619,13 +1796,24 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         const int64_t per_wave = (batch + waves - 1) / waves;
         const unsigned gw = (unsigned)((((batch + per_wave - 1) / per_wave) + 3) / 4);
         const int nch = (T * (DIN_H / 4) + 63) / 64;
+        // din_wh2: workgroups per Dice batch, about the same 8,192 in all
+        const int gw_seg = (int)std::max<int64_t>(1, std::min<int64_t>(S, (8192 + n_seg - 1) / n_seg));
+        const unsigned gw2 = (unsigned)(n_seg * gw_seg);
 #define NRK_WH_K(TT, NI, NCH)                                                                                \
     din_wh_kernel<TT, NI, NCH><<<gw, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,      \
                                                   hist_idx, mask, batch, S, T, per_wave, w.h, w.hinv,      \
                                                   att_w1, att_b1, w.wh, w.whmax)
+#define NRK_WH2_K(TT, NI, NCH)                                                                               \
+    din_wh2_kernel<TT, NI, NCH><<<gw2, 256, din_wh2_lds(T, NI), s>>>(                                        \
+        reinterpret_cast<const TT*>(table), row_base, n_user, hist_idx, mask, batch, S, T, gw_seg, w.h, w.hinv, \
+        att_w1, att_b1, w.wh, w.whmax)
 #define NRK_WH(TT, NI)                                                                                  \
     do {                                                                                                \
-        if (nch <= 4) NRK_WH_K(TT, NI, 4); else if (nch <= 8) NRK_WH_K(TT, NI, 8); else NRK_WH_K(TT, NI, 9); \
+        if (din_wh_v() == 1) {                                                                          \
+            if (nch <= 4) NRK_WH2_K(TT, NI, 4); else if (nch <= 8) NRK_WH2_K(TT, NI, 8); else NRK_WH2_K(TT, NI, 9); \
+        } else {                                                                                        \
+            if (nch <= 4) NRK_WH_K(TT, NI, 4); else if (nch <= 8) NRK_WH_K(TT, NI, 8); else NRK_WH_K(TT, NI, 9); \
+        }                                                                                               \
     } while (0)
         if (table_dtype == 0) {
             if (n_item == 4) NRK_WH(float, 4); else if (n_item == 2) NRK_WH(float, 2); else NRK_WH(float, 1);

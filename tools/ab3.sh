@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_recall.py tests/te
 tail -1 $O/pytest.log
 for rep in 1 2; do
   for v in ${DVARS:-0 1}; do
-    echo -n "att=$v "; NRK_DIN_ATT=$v timeout -k 10 120 python3 tools/din_time.py 10 2>&1 | tail -1 || exit 1
+    echo -n "din=$v "; NRK_DIN_WH=$v timeout -k 10 120 python3 tools/din_time.py 10 2>&1 | tail -1 || exit 1
   done
   for v in ${SVARS:-0 6 7 8}; do
     NRK_SCAN_VARIANT=$v timeout -k 10 120 python3 tools/screen_time.py 2>&1 | tail -1 || exit 1
