@@ -10,7 +10,7 @@
 namespace nrk {
 
 template <int D>
-__global__ __launch_bounds__(256) void tt_user_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tt_user_kernel(
     const float* __restrict__ user_table, const float* __restrict__ item_table,
     const int32_t* __restrict__ uid, const int32_t* __restrict__ hist,
     const int32_t* __restrict__ hist_len, int64_t n, int T, const float* __restrict__ w0,
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void tt_user_kernel(
             float z1 = lane + WAVE < h0 ? sb0[lane + WAVE] : 0.0f;
             const float* wr0 = sw0 + (lane < h0 ? lane : 0) * S0;
             const float* wr1 = sw0 + (lane + WAVE < h0 ? lane + WAVE : 0) * S0;
-#pragma unroll
+#pragma unroll 16
             for (int q = 0; q < 2 * D; ++q) {
                 const float xq = sx[q];
                 z0 += wr0[q] * xq;
