@@ -774,7 +774,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     __shared__ __attribute__((aligned(16))) float ushl[4][DS4 > 0 ? 1 : 256];  // DS4 == 0: the user's fp16 values
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
-    if (u >= n_users || ovf_flag[u]) return;
+    if (u >= n_users) return;
+    // one round trip for the per-user state: the overflow flag, the band
+    // count and cut, the user's row and (select slots) the first 64 band
+    // entries are loaded together before anything branches on them
+    const bool slots = n_src == 0 && !band_off;  // kernel arguments: uniform
+    const float* uv = users + u * dim;
+    const int32_t ovf_u = ovf_flag[u];
+    const int nbd_slots = slots ? cand_cnt[u] : 0;
+    const float2 ce = ucut[u];
+    const float uv_r = uv[lane < dim ? lane : 0];  // unconditional (a branch around a load serialises the batch)
+    const uint2 ent0 = slots ? cand[(size_t)u * bandcap + lane] : make_uint2(0u, 0u);  // bandcap >= 64
+    if (ovf_u) return;
     // band: per-user slots of the select (band_off == nullptr, n_src == 0), a
     // CSR of every catalog shard's entries for this user (band_off), or the
     // fixed-slot exchange (n_src > 0): source s's entries at
@@ -794,10 +805,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
         if ((threadIdx.x & 63) == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
         return;
     }
-    const float* uv = users + u * dim;
     // zero user: every score is exactly 0 -> the lowest rows win the ties
-    float nz = 0.0f;
-    for (int d = lane; d < dim; d += WAVE) nz += fabsf(uv[d]);
+    const float uv_l = lane < dim ? uv_r : 0.0f;
+    float nz = fabsf(uv_l), uam = fabsf(uv_l);
+    for (int d = lane + WAVE; d < dim; d += WAVE) {
+        nz += fabsf(uv[d]);
+        uam = fmaxf(uam, fabsf(uv[d]));
+    }
     nz = wave_sum_f32(nz);
     if (nz == 0.0f) {
         for (int i = lane; i < k; i += WAVE) {
@@ -808,9 +822,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
         }
         return;
     }
-    const int nbd = n_src > 0 ? 0 : band_off ? (int)(band_off[u + 1] - band_off[u]) : cand_cnt[u];
+    const int nbd = n_src > 0 ? 0 : band_off ? (int)(band_off[u + 1] - band_off[u]) : nbd_slots;
     const uint2* bd = band_off ? cand + band_off[u] : cand + (size_t)u * bandcap;
-    const float2 ce = ucut[u];
     double thr = -INFINITY;
     if (ce.x != -INFINITY) {
         thr = (double)ce.x + (double)ce.y;
@@ -827,32 +840,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     // for the exact score.
     constexpr int DSK = DS4 / 4;  // 16-dim k-steps of the packed layout
     const bool pre = catalog != nullptr && ce.x != -INFINITY;
-    float ush[DS4 > 0 ? 4 * DS4 : 1];
+    _Float16 ush[DS4 > 0 ? 4 * DS4 : 1];  // the user's fp16 values (packed: half the VGPRs)
     float pcut = 0.0f;
     if (pre) {
         const int dpc = pad_dim(dim);
         const int64_t nblk_c = (n_items + 31) >> 5;
         const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk_c * 64 * dpc);
-        float ua = 0.0f;
-        for (int d = 0; d < dim; ++d) ua = fmaxf(ua, fabsf(uv[d]));
+        float ua = uam;  // max |u_d| (order-free: the same value as a sequential max)
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) ua = fmaxf(ua, __shfl_xor(ua, m, WAVE));
         const float su = pow2_scale(ua);
         if constexpr (DS4 > 0) {
 #pragma unroll
-            for (int d = 0; d < 4 * DS4; ++d) ush[d] = (float)(_Float16)(uv[d] * su);
+            for (int d = 0; d < 4 * DS4; ++d) ush[d] = (_Float16)(uv[d] * su);
         }
         pcut = ce.x * (su * hdr->scale);
     }
     // (a) compact the band into LDS (list order kept; sources in rank order)
     int nband = 0;
+    auto take_one = [&](uint2 ent, int e, int cnt) {
+        const bool kp = e < cnt && (!pre || __uint_as_float(ent.x) >= pcut);
+        const unsigned long long bal = __ballot(kp);
+        if (kp) bandq[wave][nband + __popcll(bal & ((1ull << lane) - 1ull))] = ent.y;
+        nband += __popcll(bal);
+    };
     auto take = [&](const uint2* __restrict__ src, int cnt) {
-        for (int b0 = 0; b0 < cnt; b0 += WAVE) {
+        int b0 = 0;
+        if (slots) {  // the first 64 entries were loaded with the user's state
+            take_one(ent0, lane, cnt);
+            b0 = WAVE;
+        }
+        for (; b0 < cnt; b0 += WAVE) {
             const int e = b0 + lane;
-            uint2 ent = make_uint2(0u, 0u);
-            if (e < cnt) ent = src[e];
-            const bool kp = e < cnt && (!pre || __uint_as_float(ent.x) >= pcut);
-            const unsigned long long bal = __ballot(kp);
-            if (kp) bandq[wave][nband + __popcll(bal & ((1ull << lane) - 1ull))] = ent.y;
-            nband += __popcll(bal);
+            take_one(e < cnt ? src[e] : make_uint2(0u, 0u), e, cnt);
         }
     };
     if (n_src > 0) {
@@ -979,7 +999,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
                         const f16x8 hv = __builtin_bit_cast(f16x8, pc[2 * st + hh]);
 #pragma unroll
                         for (int e = 0; e < 8; ++e)
-                            acc = fmaf((float)hv[e], ush[16 * st + 8 * hh + e], acc);
+                            acc = fmaf((float)hv[e], (float)ush[16 * st + 8 * hh + e], acc);  // exact product: fma_mix
                     }
                 keep = acc >= pcut;
             }
