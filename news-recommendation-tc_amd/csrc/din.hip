@@ -1105,10 +1105,20 @@ __device__ __forceinline__ void mlp_epilogue(const din_f4 (&acc)[2][NT], float i
                                              unsigned int* __restrict__ zmax) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4;
     float mx = 0.0f;
+    // every bias load before the first store: stores count in vmcnt, so a
+    // load issued between (conditional) stores would make its wait a
+    // vmcnt(0) that drains the stores already issued -- one store round trip
+    // per column tile
+    float bns[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         const int n = 16 * j + (lane & 15);
-        const float bn = n < N ? bias[n] : 0.0f;
+        bns[j] = bias[n < N ? n : N - 1];
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int n = 16 * j + (lane & 15);
+        const float bn = n < N ? bns[j] : 0.0f;
         double su = 0.0, sq = 0.0;
 #pragma unroll
         for (int a = 0; a < 2; ++a)
