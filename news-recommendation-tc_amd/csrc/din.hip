@@ -967,6 +967,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
     float mk_n = load_mask(b0);
     fetch(b0, mk_n);
     mk_n = load_mask(b0 + 1);
+    // sample b's wh is stored during sample b + 1, right before its gathers:
+    // a store counts in vmcnt, so one issued at the end of a sample made the
+    // next sample's first wait a full store round trip; issued before the
+    // gathers its acknowledgement overlaps their latency
+    float pacc[EPP];
+    int64_t pb = -1;
+    auto store_wh = [&]() {
+        if (pb >= 0 && tg == 0) {
+            f4n* o = reinterpret_cast<f4n*>(wh + (size_t)pb * ID + gf * DIN_E + gc * EPP);
+#pragma unroll
+            for (int v = 0; v < EPP / 4; ++v) o[v] = f4n{pacc[4 * v], pacc[4 * v + 1], pacc[4 * v + 2], pacc[4 * v + 3]};
+        }
+    };
     for (int64_t b = b0; b < b1e; ++b) {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
@@ -1002,6 +1015,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         asm volatile("" ::: "memory");
         fetch(b + 1, mk_n);
         mk_n = load_mask(b + 2);
+        store_wh();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1037,14 +1051,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         for (int off = LPT; off < 64; off <<= 1)
 #pragma unroll
             for (int e = 0; e < EPP; ++e) acc[e] += __shfl_xor(acc[e], off, WAVE);
-        if (tg == 0) {
-            f4n* o = reinterpret_cast<f4n*>(wh + (size_t)b * ID + gf * DIN_E + gc * EPP);
 #pragma unroll
-            for (int v = 0; v < EPP / 4; ++v) o[v] = f4n{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
+        for (int e = 0; e < EPP; ++e) {
+            pacc[e] = acc[e];
+            mx = fmaxf(mx, fabsf(acc[e]));
         }
-#pragma unroll
-        for (int e = 0; e < EPP; ++e) mx = fmaxf(mx, fabsf(acc[e]));
+        pb = b;
     }
+    store_wh();
 #pragma unroll
     for (int k = 32; k > 0; k >>= 1) mx = fmaxf(mx, __shfl_xor(mx, k, WAVE));
     if (lane == 0 && b0 < b1e) atomicMax(segmax + seg, __float_as_uint(mx));
