@@ -776,7 +776,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
     if (u >= n_users) return;
     // one round trip for the per-user state: the overflow flag, the band
-    // count and cut, the user's row and (select slots) the first 64 band
+    // count and cut, the user's row and (select slots) the first 32 band
     // entries are loaded together before anything branches on them
     const bool slots = n_src == 0 && !band_off;  // kernel arguments: uniform
     const float* uv = users + u * dim;
@@ -784,7 +784,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     const int nbd_slots = slots ? cand_cnt[u] : 0;
     const float2 ce = ucut[u];
     const float uv_r = uv[lane < dim ? lane : 0];  // unconditional (a branch around a load serialises the batch)
-    const uint2 ent0 = slots ? cand[(size_t)u * bandcap + lane] : make_uint2(0u, 0u);  // bandcap >= 64
+    // first 32 band slots (lanes 32-63 re-read slot 0: same line, no traffic)
+    const uint2 ent0 = slots ? cand[(size_t)u * bandcap + (lane < 32 ? lane : 0)] : make_uint2(0u, 0u);
     if (ovf_u) return;
     // band: per-user slots of the select (band_off == nullptr, n_src == 0), a
     // CSR of every catalog shard's entries for this user (band_off), or the
@@ -866,9 +867,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     };
     auto take = [&](const uint2* __restrict__ src, int cnt) {
         int b0 = 0;
-        if (slots) {  // the first 64 entries were loaded with the user's state
-            take_one(ent0, lane, cnt);
-            b0 = WAVE;
+        if (slots) {  // the first 32 entries were loaded with the user's state
+            take_one(ent0, lane < 32 ? lane : cnt, cnt);
+            b0 = 32;
         }
         for (; b0 < cnt; b0 += WAVE) {
             const int e = b0 + lane;

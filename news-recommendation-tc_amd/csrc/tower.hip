@@ -53,6 +53,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
     int len, uidv;
     int32_t hv;
     meta(u, len, uidv, hv);
+    // user u's output row is stored during user u + wstride, after that
+    // user's first gathers are issued: a store counts in vmcnt, so one issued
+    // at the end of a user made the next user's first wait a full store round
+    // trip; issued behind the gathers its acknowledgement overlaps them
+    float pout = 0.0f;
+    int64_t pu = -1;
     for (; u < n; u += wstride) {
         int nlen, nuid;
         int32_t nhv;
@@ -67,6 +73,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
                 const int t = ph + P * (i0 + e);
                 const int32_t r = __shfl(hv, t < T ? t : 0, WAVE);
                 v[e] = item_table[(int64_t)(t < len ? r : 0) * D + d];
+            }
+            if (i0 == 0 && pu >= 0) {
+                if (lane < h1) out[pu * h1 + lane] = pout;
+                pu = -1;
             }
 #pragma unroll
             for (int e = 0; e < CH; ++e)
@@ -115,11 +125,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
         v = v / fmaxf(nn, 1e-12f);
         float n2 = sqrtf(wave_sum_f32(v * v));
         if (n2 == 0.0f) n2 = 1.0f;
-        if (lane < h1) out[u * h1 + lane] = v / n2;
+        if (pu >= 0 && lane < h1) out[pu * h1 + lane] = pout;  // no gathers this user (len == 0)
+        pout = v / n2;
+        pu = u;
         len = nlen;
         uidv = nuid;
         hv = nhv;
     }
+    if (pu >= 0 && lane < h1) out[pu * h1 + lane] = pout;
 }
 
 // Any depth (youtubednn_hidden_units is a list, youtubednn_recaller.py:105-112):
