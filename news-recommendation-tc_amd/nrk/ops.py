@@ -53,8 +53,11 @@ def _finite(t, name):
 
 
 # ------------------------------------------------------------------ tower --
-def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1):
-    """YoutubeDNN user tower + re-normalisation (youtubednn_recaller.py:129-178, :467-470)."""
+def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1, validate: bool = True):
+    """YoutubeDNN user tower + re-normalisation (youtubednn_recaller.py:129-178, :467-470).
+    ``validate`` checks hist_len against [0, T] (two device syncs); a caller
+    that re-runs the tower on inputs it already validated (the bench's timed
+    steps) may pass False."""
     _dev(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1)
     n, T = hist.shape
     D = user_table.shape[1]
@@ -68,7 +71,7 @@ def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1):
     _need(b0, torch.float32, (h0,), "b0")
     _need(w1, torch.float32, (h1, h0), "w1")
     _need(b1, torch.float32, (h1,), "b1")
-    if n and (int(hist_len.min()) < 0 or int(hist_len.max()) > T):
+    if validate and n and (int(hist_len.min()) < 0 or int(hist_len.max()) > T):
         raise ValueError("hist_len out of [0, T]")
     out = torch.empty((n, h1), dtype=torch.float32, device=uid.device)
     _lib.call("nrk_tt_user_fwd", _ptr(user_table), user_table.shape[0], _ptr(item_table),
