@@ -769,8 +769,10 @@ def layout_plan(args, world):
             per.append({"rank": r, "blocks": [0, -(-I // 32)], "items": [0, I], "users": [0, U]})
     rec = {"layout": layout, "tile_blocks": tb, "per_rank": per,
            "parallelism": {"single": "single",
-                           "catalog": f"catalog-sharded x{world} (BASELINE config 4: shard screen, bound "
-                                      f"all_gather, band all_to_all, owner refine)",
+                           "catalog": (f"catalog-sharded x{world} (BASELINE config 4: shard screen, bound "
+                                       f"all_gather, band all_to_all, owner refine)" if getattr(args, "topk", 30) + 1 <= 128 else
+                                       f"catalog-sharded x{world} (BASELINE config 4, k + 1 > 128: per-shard exact "
+                                       f"top-k, all_to_all to the owner, merge)"),
                            "users": f"users-sharded x{world} (independent replicas)"}[layout]}
     n, B = args.din_samples, 4096
     dper = []
@@ -899,12 +901,17 @@ def main(argv=None):
     wl = recall_workload(23 if catalog_mode else 23 + rank, U, I, D, device)
     item_vec = ops.tt_item_fwd(wl["item_table"], torch.arange(I, dtype=torch.int32, device=device))
     cat = ops.Catalog(item_vec)
+    owner = K <= ops.IP_KFAST  # the owner protocol's shard screen; larger k: the merge protocol
     if catalog_mode:
-        from nrk.dist import HipRangeShard, catalog_sharded_owner, gather_users
+        from nrk.dist import HipRangeShard, HipShard, catalog_sharded_owner, catalog_sharded_topk, gather_users
 
         me = plan["recall"]["per_rank"][rank]
         (blo, bhi), (ulo, uhi) = me["blocks"], me["users"]
-        shard = HipRangeShard(cat, blo, bhi, K, U)
+        if owner:
+            shard = HipRangeShard(cat, blo, bhi, K, U)
+        else:
+            i0, i1 = me["items"]
+            shard = HipShard(ops.Catalog(item_vec[i0:i1].contiguous()), i0, K, U)
     else:
         ws = ops.ip_topk_workspace(U, cat, K, device)
         out_s = torch.empty((U, K), dtype=torch.float32, device=device)
@@ -925,7 +932,13 @@ def main(argv=None):
         if ev is not None:
             ev[1].record()
         mark = None if ev is None else (lambda ph: ev[2 if ph == "screen" else 3].record())
-        res = catalog_sharded_owner(u, shard, K, mark=mark)
+        if owner:
+            res = catalog_sharded_owner(u, shard, K, mark=mark)
+        else:
+            res = catalog_sharded_topk(u, shard, K)
+            if mark is not None:
+                mark("screen")
+                mark("exchange")
         if ev is not None:
             ev[4].record()
         return res

@@ -34,6 +34,12 @@ typedef void* nrk_stream_t; /* hipStream_t */
 #define NRK_EUNSUPPORTED 3 /* configuration outside the compiled variants   */
 
 const char* nrk_last_error(void);
+/* ABI version 2 (round 4): nrk_ip_topk_bound takes k before m (the screen's
+ * k, so the bound pass knows the list length); the packed catalog carries a
+ * half-block-major fp16 copy after its header (nrk_ip_catalog_bytes grew);
+ * nrk_din_remap_index added; DIN item features 1, 2, 4 or 8.  A caller built
+ * against version 1 must be rebuilt. */
+#define NRK_ABI_VERSION 2
 int nrk_abi_version(void);
 
 /* ---------------------------------------------------------------------- */
@@ -329,6 +335,20 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
  * once per weight load into prep (nrk_din_prep_bytes); call it again if
  * the table changes.  B >= 2 (B = 1 is NaN in the
  * reference too). */
+/* Embedding widths other than 32 (din_embedding_dim, src/utils/config.py:115,
+ * read back by DINRanker.load_model, DIN.py:1371-1379): the kernels read
+ * 32-wide VIRTUAL features.  The host zero-pads every table to
+ * m = ceil(D / 32) * 32 columns, views it as [m * vocab, 32] (feature f's
+ * index i -> virtual indices m i + h, h < m), expands att_w0 / mlp_w0 with
+ * zero columns at the padded positions, and pads the item features with a
+ * shared all-zero row up to 1, 2, 4 or 8.  nrk_din_remap_index maps caller
+ * index rows [n_rows, f_in] to the virtual layout [n_rows, f_out]:
+ * out[r, j] = map[j] < 0 ? map[2 f_out + j]
+ *                        : in[r, map[j]] * map[f_out + j] + map[2 f_out + j]
+ * (map: int32 device array, rows src | mul | add).  Identity when D = 32 and
+ * the item-feature count is 1, 2, 4 or 8 (no call needed). */
+int nrk_din_remap_index(const int32_t* in, int64_t n_rows, int f_in, const int32_t* map, int f_out,
+                        int32_t* out, nrk_stream_t stream);
 size_t nrk_din_prep_bytes(int n_item);
 int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int table_dtype,
                     int64_t n_table_rows, void* prep, nrk_stream_t stream);

@@ -712,187 +712,14 @@ __device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
     return p * x + ((1.0f - p) * 0.01f) * x;
 }
 
-template <typename TT, int NI, int NCH>
-__global__ __launch_bounds__(256, 2) void din_wh_kernel(
-    const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
-    const int32_t* __restrict__ hist_idx, const float* __restrict__ mask, int64_t B, int64_t S,
-    int T, int64_t per_wave, const float* __restrict__ h, const float2* __restrict__ hinv_all,
-    const float* __restrict__ att_w1, const float* __restrict__ att_b1, float* __restrict__ wh,
-    unsigned int* __restrict__ segmax) {
-    constexpr int ID = NI * DIN_E;
-    typedef float f4n __attribute__((ext_vector_type(4)));
-    typedef uint32_t u4n __attribute__((ext_vector_type(4)));
-    // gather layout: 16-B pieces of EPP elements, PPR pieces per row; lane =
-    // tg * LPT + f * PPR + c gathers piece c of feature f for slots
-    // t = tg, tg + TG, ... (a round's R loads in flight at once), and the TG
-    // partial sums are combined by an xor tree
-    constexpr int EPP = 16 / (int)sizeof(TT);
-    constexpr int PPR = DIN_E / EPP;
-    constexpr int LPT = NI * PPR;
-    constexpr int TG = 64 / LPT;
-    constexpr int R = 64 / TG < 8 ? 64 / TG : 8;
-    constexpr int HQ = DIN_H / 4;                      // 4-column chunks per h row
-    __shared__ __attribute__((aligned(16))) float dsc[4][64 * DIN_H];  // Dice(h) of the sample
-    __shared__ int32_t rr_s[4][64 * NI];
-    __shared__ float w_s[4][64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int tg = lane / LPT, gf = (lane / PPR) % NI, gc = lane % PPR;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
-    const int64_t b0 = wave * per_wave;
-    const int64_t b1e = b0 + per_wave < B ? b0 + per_wave : B;
-    const float ab1 = att_b1[0];
-    const bool act = lane < T;
-    const int nq = T * HQ;
-    int64_t rbs[NI];
-#pragma unroll
-    for (int f = 0; f < NI; ++f) rbs[f] = row_base[n_user + f];
-    int64_t cur = -1;
-    float mx = 0.0f;
-    auto flush = [&]() {
-        float m = mx;
-#pragma unroll
-        for (int k = 32; k > 0; k >>= 1) m = fmaxf(m, __shfl_xor(m, k, WAVE));
-        if (lane == 0 && cur >= 0) atomicMax(segmax + cur, __float_as_uint(m));
-    };
-    // sample bb's h block [T x DIN_H] read as consecutive 16-B chunks (chunk
-    // q = 64 i + lane: one coalesced 1-KB load per i), plus lane t's history
-    // indices and mask
-    // masked rows' weights are multiplied by 0, so their h is never needed:
-    // their chunks read one shared, always-finite chunk instead --
-    // unconditional loads, no traffic.  The mask of the fetched
-    // sample was loaded one sample earlier (mk_n), so the chunk addresses do
-    // not wait on a load in flight.
-    f4n hq[NCH];
-    int32_t ix[NI];
-    float mk;
-    const f4n* hdummy = reinterpret_cast<const f4n*>(hinv_all);
-    auto load_mask = [&](int64_t bb) -> float { return (bb < b1e && act) ? mask[bb * T + lane] : 0.0f; };
-    auto fetch = [&](int64_t bb, float mbb) {
-        const bool ok = bb < b1e;
-        const f4n* hr = reinterpret_cast<const f4n*>(h + (size_t)(ok ? bb : 0) * T * DIN_H);
-        const uint64_t live = __builtin_amdgcn_ballot_w64(mbb != 0.0f);  // unmasked rows (wave-uniform)
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-            const int q = 64 * i + lane;
-            const bool on = ok && q < nq && ((live >> (q / HQ)) & 1ull);
-            hq[i] = *(on ? hr + q : hdummy);
-        }
-#pragma unroll
-        for (int f = 0; f < NI; ++f) ix[f] = ok && act ? hist_idx[((size_t)bb * T + lane) * NI + f] : 0;
-        mk = mbb;
-    };
-    // this segment's Dice statistics for the same chunks, kept in registers
-    f4n sm[NCH], si[NCH];
-    auto stats = [&](int64_t seg) {
-        const f4n* st = reinterpret_cast<const f4n*>(hinv_all + (size_t)seg * T * DIN_H);
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-            const int q = 64 * i + lane;
-            const f4n s0 = q < nq ? st[2 * q] : f4n{0.0f, 1.0f, 0.0f, 1.0f};
-            const f4n s1 = q < nq ? st[2 * q + 1] : f4n{0.0f, 1.0f, 0.0f, 1.0f};
-            sm[i] = f4n{s0.x, s0.z, s1.x, s1.z};
-            si[i] = f4n{s0.y, s0.w, s1.y, s1.w};
-        }
-    };
-    float mk_n = load_mask(b0);
-    fetch(b0, mk_n);
-    mk_n = load_mask(b0 + 1);
-    for (int64_t b = b0; b < b1e; ++b) {
-        const int64_t seg = b / S;
-        if (seg != cur) {
-            flush();
-            cur = seg;
-            mx = 0.0f;
-            stats(seg);
-        }
-        // Dice of every h element, chunk-parallel, staged in LDS; lane t then
-        // forms w_t = (sum_j w1_j Dice(h_tj) + b1) * mask_t over j ascending
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-            const int q = 64 * i + lane;
-            if (q < nq) {
-                f4n d;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) d[e] = dice_fast(hq[i][e], sm[i][e], si[i][e]);
-                *reinterpret_cast<f4n*>(&dsc[wv][4 * q]) = d;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        float w = 0.0f;
-        if (act) {
-            const f4n* dr = reinterpret_cast<const f4n*>(&dsc[wv][lane * DIN_H]);
-            float sacc = 0.0f;
-#pragma unroll
-            for (int c = 0; c < HQ; ++c) {
-                const f4n d = dr[c];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) sacc += att_w1[4 * c + e] * d[e];
-            }
-            w = (sacc + ab1) * mk;
-        }
-        w_s[wv][lane] = w;
-#pragma unroll
-        for (int f = 0; f < NI; ++f) rr_s[wv][lane * NI + f] = act ? (int32_t)(rbs[f] + ix[f]) : 0;
-        const uint64_t nz = __builtin_amdgcn_ballot_w64(w != 0.0f);
-        const int te = nz ? 64 - __builtin_clzll(nz) : 0;
-        asm volatile("" ::: "memory");
-        fetch(b + 1, mk_n);  // next sample, in flight during the gathers
-        mk_n = load_mask(b + 2);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        float acc[EPP];
-#pragma unroll
-        for (int e = 0; e < EPP; ++e) acc[e] = 0.0f;
-        for (int t0 = 0; t0 < te; t0 += TG * R) {
-            u4n raw[R];
-            float wt[R];
-#pragma unroll
-            for (int u = 0; u < R; ++u) {
-                const int t = t0 + TG * u + tg;
-                const int tc = t < te ? t : te - 1;  // past te: weight +0 on a valid row
-                wt[u] = t < te ? w_s[wv][tc] : 0.0f;
-                const int32_t r = rr_s[wv][tc * NI + gf];
-                raw[u] = *reinterpret_cast<const u4n*>(table + (int64_t)r * DIN_E + gc * EPP);
-            }
-#pragma unroll
-            for (int u = 0; u < R; ++u) {
-                if constexpr (sizeof(TT) == 4) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) acc[e] = fmaf(wt[u], __uint_as_float(raw[u][e]), acc[e]);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        acc[2 * i] = fmaf(wt[u], __uint_as_float(raw[u][i] << 16), acc[2 * i]);
-                        acc[2 * i + 1] = fmaf(wt[u], __uint_as_float(raw[u][i] & 0xFFFF0000u), acc[2 * i + 1]);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int off = LPT; off < 64; off <<= 1)
-#pragma unroll
-            for (int e = 0; e < EPP; ++e) acc[e] += __shfl_xor(acc[e], off, WAVE);
-        if (tg == 0) {
-            f4n* o = reinterpret_cast<f4n*>(wh + (size_t)b * ID + gf * DIN_E + gc * EPP);
-#pragma unroll
-            for (int v = 0; v < EPP / 4; ++v) o[v] = f4n{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
-        }
-#pragma unroll
-        for (int e = 0; e < EPP; ++e) mx = fmaxf(mx, fabsf(acc[e]));
-    }
-    flush();
-}
-
-// din_wh2: din_wh with the Dice statistics in LDS instead of registers.
-// Workgroup (seg, g) takes a contiguous run of ONE Dice batch (segment), so
-// its four waves share the segment's (mean, 1 / (std + 1e-8)) table, loaded
-// once into LDS; the per-wave Dice stage holds T rows (dynamic LDS).  That
-// frees 64 VGPRs per lane: 3 waves / SIMD at T <= 50 (48 KB of LDS per
-// workgroup) instead of 2, for this latency-bound gather kernel.  Same
-// arithmetic, same order (bit-identical wh).
+// din_wh2: the Dice statistics live in LDS, not registers.  Workgroup
+// (seg, g) takes a contiguous run of ONE Dice batch (segment), so its four
+// waves share the segment's (mean, 1 / (std + 1e-8)) table, loaded once into
+// LDS; the per-wave Dice stage holds T rows (dynamic LDS).  3 waves / SIMD at
+// T <= 50 (48 KB of LDS per workgroup) for this latency-bound gather kernel
+// (round 2's register-resident variant ran 2 with spills: 1.40 vs 1.10 ms).
+// Masked rows (mask_t = 0) never read their h row: the attention kernels may
+// leave it unwritten.
 template <typename TT, int NI, int NCH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void din_wh2_kernel(
     const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
@@ -1590,28 +1417,30 @@ __global__ void din_prepare_kernel(const float* __restrict__ w0, int ID, float* 
     }
 }
 
+// ---------------------------------------------------------- index remap --
+// The kernels read 32-wide features.  A model with another embedding width D
+// (din_embedding_dim, config.py:115) is served as 32-wide VIRTUAL features:
+// every table zero-padded to m = ceil(D / 32) * 32 columns and viewed as
+// [m * vocab, 32], feature f's index i becoming the m virtual indices
+// m i + h; padding features (a shared all-zero row) fill the item features up
+// to a supported count.  out[r, j] = map[j] < 0 ? map[2F + j]
+//                                                : in[r, map[j]] * map[F + j] + map[2F + j]
+// with F = f_out (map: src | mul | add rows).
+__global__ void din_remap_kernel(const int32_t* __restrict__ in, int64_t n_rows, int f_in, int f_out,
+                                 const int32_t* __restrict__ map, int32_t* __restrict__ out) {
+    const int64_t n = n_rows * f_out;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / f_out;
+        const int j = (int)(i - r * f_out);
+        const int src = map[j];
+        out[i] = src < 0 ? map[2 * f_out + j] : in[r * f_in + src] * map[f_out + j] + map[2 * f_out + j];
+    }
+}
+
 // ------------------------------------------------------------- workspace --
 // din_att_h workgroups per segment: about 6144 in the whole grid (24 per CU,
 // measured best of 1024...32768 at config 3), at most 512 per segment and
 // never more than the segment has samples
-// att_h variant (dev A/B knob NRK_DIN_ATT: 0 = din_att_h, 1 = din_att_h2, the default)
-// wh variant (dev A/B knob NRK_DIN_WH: 0 = din_wh, 1 = din_wh2, the default)
-static int din_wh_v() {
-    static int v = [] {
-        const char* e = getenv("NRK_DIN_WH");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
-
-static int din_att_v() {
-    static int v = [] {
-        const char* e = getenv("NRK_DIN_ATT");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
-
 static inline int din_att_groups(int64_t N, int64_t S) {
     const int64_t n_seg = (N + S - 1) / S;
     int64_t g = (6144 + n_seg - 1) / n_seg;
@@ -1692,6 +1521,20 @@ using namespace nrk;
 
 extern "C" {
 
+int nrk_din_remap_index(const int32_t* in, int64_t n_rows, int f_in, const int32_t* map, int f_out,
+                        int32_t* out, nrk_stream_t stream) {
+    clear_error();
+    NRK_REQUIRE(n_rows >= 0 && f_in >= 1 && f_out >= 1, "bad shape");
+    if (n_rows == 0) return NRK_OK;
+    NRK_REQUIRE(in && map && out, "null pointer");
+    hipStream_t s = as_stream(stream);
+    const int64_t n = n_rows * f_out;
+    din_remap_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 4096), 256, 0, s>>>(in, n_rows, f_in, f_out,
+                                                                                        map, out);
+    NRK_CHECK_LAUNCH();
+    return NRK_OK;
+}
+
 size_t nrk_din_prep_bytes(int n_item) {
     if (n_item <= 0) return 0;
     return (size_t)3 * DIN_H * n_item * DIN_E * sizeof(float) + 64;
@@ -1702,9 +1545,8 @@ int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int tabl
     clear_error();
     NRK_REQUIRE(att_w0 && prep && table, "null pointer");
     NRK_REQUIRE(n_item >= 1 && n_item <= 8, "n_item must be in [1, 8]");
-    // nrk_din_forward_segments is instantiated for 1, 2 and 4 item features only:
-    // refuse the others here rather than at the first forward call
-    if (n_item != 4 && n_item != 2 && n_item != 1) NRK_UNSUPPORTED("n_item must be 1, 2 or 4");
+    // instantiated for 1, 2, 4 and 8 (32-wide) item features (ops.DinParams pads other counts)
+    if (n_item != 8 && n_item != 4 && n_item != 2 && n_item != 1) NRK_UNSUPPORTED("n_item must be 1, 2, 4 or 8");
     NRK_REQUIRE(table_dtype == 0 || table_dtype == 1, "table_dtype must be 0 (f32) or 1 (bf16)");
     NRK_REQUIRE(n_table_rows >= 1, "n_table_rows must be >= 1");
     const int ID = n_item * DIN_E;
@@ -1755,7 +1597,8 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         NRK_REQUIRE(S % 64 == 0, "seg_len must be a multiple of 64 when the samples span several segments");
     NRK_REQUIRE(seq_len >= 1 && seq_len <= 128, "seq_len must be in [1, 128]");
     NRK_REQUIRE(n_user >= 1 && n_ctx >= 0 && n_item >= 1, "bad feature counts");
-    if (n_item != 4 && n_item != 2 && n_item != 1) NRK_UNSUPPORTED("n_item must be 1, 2 or 4");
+    // instantiated for 1, 2, 4 and 8 (32-wide) item features (ops.DinParams pads other counts)
+    if (n_item != 8 && n_item != 4 && n_item != 2 && n_item != 1) NRK_UNSUPPORTED("n_item must be 1, 2, 4 or 8");
     NRK_REQUIRE(h1 >= 1 && h1 <= 1024 && h2 >= 1 && h2 <= 1024, "hidden sizes out of range");
     NRK_REQUIRE(table && row_base && user_idx && item_idx && hist_idx && mask && prep && att_b0 &&
                     att_w1 && att_b1 && mlp_w0 && mlp_b0 && mlp_w1 && mlp_b1 && mlp_w2 && mlp_b2 &&
@@ -1774,7 +1617,7 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     const float* pf = reinterpret_cast<const float*>(prep);
 #define NRK_ATT_H(TT, NI)                                                                              \
     do {                                                                                               \
-        if (T <= 64 && din_att_v() == 1 && (sizeof(TT) == 2 || NI < 4))                                \
+        if (T <= 64 && NI <= 4 && (sizeof(TT) == 2 || NI < 4))                                         \
             din_att_h2_kernel<TT, NI><<<(unsigned)nb_att, 256, 0, s>>>(                                \
                 reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G,    \
                 T, pf, att_b0, w.h, w.hpart);                                                       \
@@ -1788,9 +1631,11 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
                 T, pf, att_b0, w.h, w.hpart);                                                       \
     } while (0)
     if (table_dtype == 0) {
-        if (n_item == 4) NRK_ATT_H(float, 4); else if (n_item == 2) NRK_ATT_H(float, 2); else NRK_ATT_H(float, 1);
+        if (n_item == 8) NRK_ATT_H(float, 8); else if (n_item == 4) NRK_ATT_H(float, 4);
+        else if (n_item == 2) NRK_ATT_H(float, 2); else NRK_ATT_H(float, 1);
     } else {
-        if (n_item == 4) NRK_ATT_H(uint16_t, 4); else if (n_item == 2) NRK_ATT_H(uint16_t, 2); else NRK_ATT_H(uint16_t, 1);
+        if (n_item == 8) NRK_ATT_H(uint16_t, 8); else if (n_item == 4) NRK_ATT_H(uint16_t, 4);
+        else if (n_item == 2) NRK_ATT_H(uint16_t, 2); else NRK_ATT_H(uint16_t, 1);
     }
 #undef NRK_ATT_H
     const int ncol_att = T * DIN_H;
@@ -1815,37 +1660,27 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
 #define NRK_PACK(NTV) din_w1_pack_kernel<NTV><<<gp, 256, 0, s>>>(mlp_w0, h1, IN, w1max, w.w1pack)
         if (NT == 4) NRK_PACK(4); else if (NT == 8) NRK_PACK(8); else if (NT == 13) NRK_PACK(13); else NRK_PACK(16);
 #undef NRK_PACK
-        // wh: one wave per sample, contiguous runs of samples per wave
-        const int64_t waves = std::min<int64_t>(batch, 32768);
-        const int64_t per_wave = (batch + waves - 1) / waves;
-        const unsigned gw = (unsigned)((((batch + per_wave - 1) / per_wave) + 3) / 4);
+        // din_wh2: one wave per sample; workgroups per Dice batch, about 8,192 in all
         const int nch = (T * (DIN_H / 4) + 63) / 64;
-        // din_wh2: workgroups per Dice batch, about the same 8,192 in all
         const int gw_seg = (int)std::max<int64_t>(1, std::min<int64_t>(S, (8192 + n_seg - 1) / n_seg));
         const unsigned gw2 = (unsigned)(n_seg * gw_seg);
-#define NRK_WH_K(TT, NI, NCH)                                                                                \
-    din_wh_kernel<TT, NI, NCH><<<gw, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,      \
-                                                  hist_idx, mask, batch, S, T, per_wave, w.h, w.hinv,      \
-                                                  att_w1, att_b1, w.wh, w.whmax)
 #define NRK_WH2_K(TT, NI, NCH)                                                                               \
     din_wh2_kernel<TT, NI, NCH><<<gw2, 256, din_wh2_lds(T, NI), s>>>(                                        \
         reinterpret_cast<const TT*>(table), row_base, n_user, hist_idx, mask, batch, S, T, gw_seg, w.h, w.hinv, \
         att_w1, att_b1, w.wh, w.whmax)
 #define NRK_WH(TT, NI)                                                                                  \
     do {                                                                                                \
-        if (din_wh_v() == 1) {                                                                          \
-            if (nch <= 4) NRK_WH2_K(TT, NI, 4); else if (nch <= 8) NRK_WH2_K(TT, NI, 8); else NRK_WH2_K(TT, NI, 9); \
-        } else {                                                                                        \
-            if (nch <= 4) NRK_WH_K(TT, NI, 4); else if (nch <= 8) NRK_WH_K(TT, NI, 8); else NRK_WH_K(TT, NI, 9); \
-        }                                                                                               \
+        if (nch <= 4) NRK_WH2_K(TT, NI, 4); else if (nch <= 8) NRK_WH2_K(TT, NI, 8); else NRK_WH2_K(TT, NI, 9); \
     } while (0)
         if (table_dtype == 0) {
-            if (n_item == 4) NRK_WH(float, 4); else if (n_item == 2) NRK_WH(float, 2); else NRK_WH(float, 1);
+            if (n_item == 8) NRK_WH(float, 8); else if (n_item == 4) NRK_WH(float, 4);
+            else if (n_item == 2) NRK_WH(float, 2); else NRK_WH(float, 1);
         } else {
-            if (n_item == 4) NRK_WH(uint16_t, 4); else if (n_item == 2) NRK_WH(uint16_t, 2); else NRK_WH(uint16_t, 1);
+            if (n_item == 8) NRK_WH(uint16_t, 8); else if (n_item == 4) NRK_WH(uint16_t, 4);
+            else if (n_item == 2) NRK_WH(uint16_t, 2); else NRK_WH(uint16_t, 1);
         }
 #undef NRK_WH
-#undef NRK_WH_K
+#undef NRK_WH2_K
         const unsigned gm = (unsigned)((batch + MLP1_ROWS - 1) / MLP1_ROWS);
 #define NRK_MLP1(TT, NTV)                                                                                 \
     din_mlp1_kernel<TT, NTV><<<gm, 256, 0, s>>>(reinterpret_cast<const TT*>(table), row_base, n_user,     \

@@ -235,8 +235,7 @@ __device__ __forceinline__ void top_insert(float (&t)[MT], float v) {
 // Scan: NW waves x UG x 32 users per workgroup share one NSL-slot LDS ring of
 // catalog tiles (8 KB, or one 16-KB block at dim 256).  Per tile every wave
 // reads the tile's A fragments once and runs TB x DS x UG MFMAs.
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false,
-          int DBG = 0>
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false>
 __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
     int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
@@ -434,11 +433,6 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
 #pragma unroll
             for (int b = 1; b < TB; ++b) vt[g] = fmaxf(vt[g], mx[g][b]);
         }
-        if constexpr (DBG == 1) {  // dev floor measurement: MFMA + max only
-#pragma unroll
-            for (int g = 0; g < UG; ++g) pend[g] = fmaxf(pend[g], vt[g]);
-            return;
-        }
         // appends: every half-block max >= tau reaches the user's HBM list
         // (the count runs past the capacity -- the select then sends the user
         // to the exact fallback -- and extra entries land on the last slots).
@@ -556,7 +550,6 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         if (user < n_users) {
             acnt[(size_t)user * 2 + h] = cnt[g];
             if (h == 0) uinfo[user] = make_float4(live[g] ? lb : -INFINITY, eps_s[g], scl[g], eps_u[g]);
-            if (DBG == 1 && pend[g] == 12345.0f) acnt[(size_t)user * 2 + h] = 7;
         }
     }
 }
@@ -1617,7 +1610,7 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
                                                             const uint2* __restrict__ pre,
                                                             const int32_t* __restrict__ pre_cnt,
                                                             float2* __restrict__ ucut, uint32_t* __restrict__ out_ent,
-                                                            int32_t* __restrict__ out_cnt, int x_cap, int dbg) {
+                                                            int32_t* __restrict__ out_cnt, int x_cap) {
     __shared__ __attribute__((aligned(16))) uint32_t pool[4][2 * IP_SEL + 4];  // n_lists * m <= 512
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * 4;
@@ -1656,7 +1649,7 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
         uint2 ent[SH_ENT];
         sh_load(s0, s1, a0, n, 0, lane, ent);  // in flight across the bound select
         float G = -INFINITY;
-        if (tot >= k && dbg != 1) {
+        if (tot >= k) {
             for (int i = lane; i < tot; i += WAVE)
                 pool[wave][i] = fkey(bounds[((int64_t)(i / m) * n_users + u) * m + (i % m)]);
             wave_sync_lds();
@@ -1672,7 +1665,7 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
         }
         int c = 0;
         uint32_t* dst = out_ent + (size_t)u * x_cap;
-        for (int b0 = 0; b0 < (dbg == 2 ? 0 : n); b0 += SH_ENT * WAVE) {
+        for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
             if (b0 > 0) sh_load(s0, s1, a0, n, b0, lane, ent);
 #pragma unroll
             for (int j = 0; j < SH_ENT; ++j) {
@@ -1797,14 +1790,14 @@ static inline int next_pow2(int x) {
 
 // scan variants: (DP, waves per workgroup, ring slots, user groups per wave,
 // register list length, waves per SIMD)
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false, int DBG = 0>
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false>
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
     const int per_wg = NW * 32 * UG;
     constexpr int TB = 64 * DP >= 8192 ? 1 : 8192 / (64 * DP);
     const int nblk = (n_items + 31) / 32;
     const int t_lo = w.blk_lo / TB, t_hi = (std::min(w.blk_hi, nblk) + TB - 1) / TB;
-    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP, DBG><<<(n_users + per_wg - 1) / per_wg, NW * 64, 0, s>>>(
+    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<(n_users + per_wg - 1) / per_wg, NW * 64, 0, s>>>(
         users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi);
 }
 
@@ -1814,24 +1807,10 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
     constexpr int UG = (DP <= 128 && MT <= 32) ? 2 : 1;
     constexpr int WPE = (DP >= 128 || MT >= 32) ? 2 : 4;
     if constexpr (DP == 32 && MT == 16) {
-        // dev A/B switch (tools/screen_time.py): NRK_SCAN_VARIANT
-        static const int var = [] { const char* e = getenv("NRK_SCAN_VARIANT"); return e ? atoi(e) : 0; }();
-        switch (var) {
-            case 1: launch_scan_v<DP, 4, 4, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 2: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 2, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 3: launch_scan_v<DP, 8, 4, 2, MT, 4, false, 1, true, 1>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 4: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, true>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 5: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 2, false>(users, n_users, cat, n_items, dim, k, w, s); return;
-            // 128 users per wave (half the LDS fragment reads and barriers per MFMA), 2 waves / SIMD
-            case 6: launch_scan_v<DP, 4, 3, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 7: launch_scan_v<DP, 4, 4, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
-            case 9: launch_scan_v<DP, 8, 3, 2, MT, 4, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s); return;
-            default: break;
-        }
         // default at D = 32, k <= 32 (BASELINE config 2): 8 waves x 128 users
         // (UG = 4) per workgroup at 2 waves / SIMD -- every LDS fragment read
         // and tile barrier serves twice the MFMAs of the 64-user waves
-        // (variant 9): config-2 screen 6.8-7.0 vs 7.0-7.2 ms
+        // (round 3): config-2 screen 6.8-7.0 vs 7.0-7.2 ms
         launch_scan_v<DP, 8, 3, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s);
         return;
     }
@@ -1841,8 +1820,8 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
     // appended maxima per user; whole-tile appends (TAPP, variant 4) 7.4-7.5
     // with 885 (the select reads 2.6x more); 4-wave workgroups 7.9-8.2, 4 / 6
     // / 8 ring slots 7.3-7.4, alternating inserts (IE = 2) 8.1 (the lagging
-    // cut doubles the appends); without any append / insert work (DBG = 1)
-    // 4.9-6.4 ms
+    // cut doubles the appends); a round-3 measurement build without any
+    // append / insert work ran 4.9-6.4 ms
     constexpr int NW = (UG == 2) ? 8 : 4, NSL = (UG == 2) ? 3 : 4;
     launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s);
 }
@@ -1878,11 +1857,6 @@ static int ip_range(IpWs& w, int64_t n_items, int dim, int64_t blk_lo, int64_t b
     return NRK_OK;
 }
 
-static int sh_dbg() {  // dev timing knob (tools/ab_sh.sh): NRK_SH_DBG, 0 = off
-    static const int v = [] { const char* e = getenv("NRK_SH_DBG"); return e ? atoi(e) : 0; }();
-    return v;
-}
-
 // persistent grid of the shard kernels: SH_WG_PER_CU 4-wave workgroups per CU
 static int sh_grid(int64_t n_users) {
     static const int n_cu = [] {
@@ -1890,11 +1864,7 @@ static int sh_grid(int64_t n_users) {
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
         return cu > 0 ? cu : 256;
     }();
-    static const int per_cu = [] {  // dev A/B knob (tools/ab2.sh): NRK_SH_WG
-        const char* e = getenv("NRK_SH_WG");
-        return e && atoi(e) > 0 ? atoi(e) : SH_WG_PER_CU;
-    }();
-    return (int)std::max<int64_t>(1, std::min<int64_t>((n_users + 3) / 4, (int64_t)n_cu * per_cu));
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n_users + 3) / 4, (int64_t)n_cu * SH_WG_PER_CU));
 }
 
 // empty shard range: no appends, uinfo.z = 0 (shard_band: no band, no cut)
@@ -2219,7 +2189,7 @@ int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, con
     const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
     ip_shard_band_kernel<<<sh_grid(n_users), 256, 0, as_stream(stream)>>>(
         n_users, k, w.m2, w.app, w.acnt, w.uinfo, bounds, bounds ? n_lists : 0, bounds ? m : 1, w.bandcap,
-        w.ovf_flag, w.cand, w.cnt, w.ucut, reinterpret_cast<uint32_t*>(out_ent), out_cnt, x_cap, sh_dbg());
+        w.ovf_flag, w.cand, w.cnt, w.ucut, reinterpret_cast<uint32_t*>(out_ent), out_cnt, x_cap);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

@@ -11,5 +11,5 @@ void clear_error() { g_last_error.clear(); }
 
 extern "C" {
 const char* nrk_last_error(void) { return nrk::g_last_error.c_str(); }
-int nrk_abi_version(void) { return 1; }
+int nrk_abi_version(void) { return NRK_ABI_VERSION; }
 }

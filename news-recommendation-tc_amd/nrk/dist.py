@@ -4,21 +4,25 @@ torch.distributed over RCCL ("nccl" on ROCm), 127.0.0.1 rendezvous.
 * users-sharded  -- every rank scores its own contiguous user block against
   the full (replicated) catalog.  No data-path collective (weak scaling).
 * catalog-sharded (BASELINE config 4), owner refine (catalog_sharded_owner,
-  the default) -- every rank holds the whole packed catalog and fp32 rows
-  (69 MB at config 2) and screens only its block range [lo_r, hi_r) for
-  ALL users (gather_users: each rank runs the user tower for its own user
-  block, all_gather).  Two exchanges: an all_gather of every shard's m
-  largest screen bounds per user, whose k-th largest bounds the user's
-  GLOBAL k-th score (nrk_ip_topk_apply_bound raises each shard's cut to
-  it), then an all_to_all of the band entries at or above the cut (8 B
-  each, global half-block ids) to the owner of each user block, which runs
-  the exact refine for its users only (nrk_ip_topk_refine_csr): the refine
-  shrinks 1/N with the screen and no merge is needed.  Same rows and
-  scores as one GPU.
-* catalog-sharded, merge (catalog_sharded_topk, round 2) -- each shard
-  refines every user against its own rows and an all_to_all of the
+  the default, k <= 128) -- every rank holds the whole packed catalog and
+  fp32 rows (69 MB at config 2) and screens only its tile-aligned block
+  range for ALL users (gather_users: each rank runs the user tower for its
+  own user block, all_gather).  Two exchanges, both fixed-size (no host-side
+  sizes, no sync): an all_gather of every shard's m largest screen lower
+  bounds per user (nrk_ip_topk_shard_screen), whose k-th largest bounds the
+  user's GLOBAL k-th score; each shard packs the half-block ids at or above
+  its cut (nrk_ip_topk_shard_band: IP_X_CAP = 32 slots of 4-byte int32
+  half-block ids per user, count -1 = more than 32 -> the owner takes that
+  user's exact path), and one all_to_all of counts and slots goes to the
+  owner of each user block, which runs the exact refine of its users only
+  from every shard's slots (nrk_ip_topk_refine_x): the refine shrinks 1/N
+  with the screen and no merge is needed.  Same rows and scores as one GPU.
+* catalog-sharded, merge (catalog_sharded_topk) -- each shard holds its own
+  rows and refines every user against them (k <= 128: after the bound
+  exchange; larger k: the exact path, no exchange) and an all_to_all of the
   shard-local top-k (fp64 exact + int32 global row) goes to the owner,
-  where nrk_topk_merge orders by (score desc, row asc).
+  where nrk_topk_merge orders by (score desc, row asc), pairwise in a tree
+  when the lists exceed one merge (k <= 512).
 * users-sharded ItemCF similarity (itemcf_sim_sharded) -- rank r holds the
   click lists of users [lo_r, hi_r) and owns items [ilo_r, ihi_r).  Every
   rank emits the pair tuples (key, GLOBAL slot, weight) of its users; one
@@ -67,12 +71,16 @@ def shard_range(n: int, world: int, rank: int):
 class HipShard:
     """This rank's catalog shard on the HIP path (nrk_ip_topk_screen ->
     nrk_ip_topk_bound / _apply_bound -> nrk_ip_topk_finish), with its
-    workspace and outputs allocated once for ``n_users`` queries."""
+    workspace and outputs allocated once for ``n_users`` queries.  For
+    k > ops.IP_KFAST (no MFMA screen; nrk_ip_topk's exact path) there are no
+    screen bounds: ``bounded`` is False, screen() returns -inf and finish()
+    runs the exact top-k of the shard."""
 
     def __init__(self, catalog, row_lo: int, k: int, n_users: int):
         from . import ops
 
         self.ops, self.cat, self.row_lo, self.k = ops, catalog, int(row_lo), int(k)
+        self.bounded = self.k <= ops.IP_KFAST
         dev = catalog.items.device
         self.ws = ops.ip_topk_workspace(n_users, catalog, k, dev)
         self.s = torch.empty((n_users, k), dtype=torch.float32, device=dev)
@@ -81,7 +89,9 @@ class HipShard:
 
     def screen(self, users, m: int):
         """fp16 MFMA screen; returns this shard's m largest exact lower
-        bounds per user (fp32 [U, m])."""
+        bounds per user (fp32 [U, m]; -inf without a screen)."""
+        if not self.bounded:
+            return torch.full((users.shape[0], m), float("-inf"), dtype=torch.float32, device=users.device)
         self.ops.ip_topk_screen(users, self.cat, self.k, self.ws)
         return self.ops.ip_topk_bound(users, self.cat, self.k, m, self.ws)
 
@@ -90,6 +100,10 @@ class HipShard:
         shard; with ``bounds`` ([n_lists, U, m], every shard's screen bounds)
         the cut is first raised to the k-th largest of each user's values."""
         n = users.shape[0]
+        if not self.bounded:
+            s, r, e = self.ops.ip_topk(users, self.cat, self.k, row_offset=self.row_lo, exact=True,
+                                       workspace=self.ws, check_finite=False)
+            return e, r
         if bounds is not None:
             self.ops.ip_topk_apply_bound(bounds, self.k, self.ws)
         self.ops.ip_topk_finish(users, self.cat, self.k, self.ws, self.s[:n], self.r[:n],
@@ -107,9 +121,30 @@ def bound_width(k: int, world: int) -> int:
     return m if world * m <= 512 and world * m >= k else 0
 
 
+MERGE_MAX = 1024  # entries one nrk_topk_merge call orders per user
+
+
 def _default_merge(exact_lists, row_lists, k):
+    """(score desc, row asc) merge of [G, n, k_in] lists; lists longer than
+    one merge call are merged pairwise in a tree (the order is total, so
+    the result is the same)."""
     from . import ops
 
+    G, n, k_in = exact_lists.shape
+    while G * k_in > MERGE_MAX:
+        if 2 * k_in > MERGE_MAX:
+            raise NotImplementedError(f"catalog-sharded merge supports k <= {MERGE_MAX // 2}, got {k_in}")
+        e_next, r_next = [], []
+        for g in range(0, G, 2):
+            if g + 1 == G:
+                e_next.append(exact_lists[g])
+                r_next.append(row_lists[g])
+                continue
+            _, r2, e2 = ops.topk_merge(exact_lists[g:g + 2].contiguous(), row_lists[g:g + 2].contiguous(), k_in)
+            e_next.append(e2)
+            r_next.append(r2)
+        exact_lists, row_lists = torch.stack(e_next).contiguous(), torch.stack(r_next).contiguous()
+        G = exact_lists.shape[0]
     return ops.topk_merge(exact_lists, row_lists, k)
 
 
@@ -155,7 +190,7 @@ def catalog_sharded_topk(users, shard, k: int, group=None, merge=None, exchange_
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     U = users.shape[0]
-    m = bound_width(k, world) if exchange_bound else 0
+    m = bound_width(k, world) if exchange_bound and getattr(shard, "bounded", True) else 0
     b = shard.screen(users, max(m, 1))
     bounds = None
     if m:
@@ -191,6 +226,10 @@ class HipRangeShard:
         from . import ops
 
         self.ops, self.cat, self.k = ops, catalog, int(k)
+        self.k_max = ops.IP_KFAST  # the shard screen's list (nrk_ip_topk_shard_screen)
+        if self.k > self.k_max:
+            raise NotImplementedError(f"HipRangeShard (owner protocol) handles k <= {self.k_max}, got {self.k}; "
+                                      "use HipShard + catalog_sharded_topk")
         self.blk_lo, self.blk_hi, self.n_users = int(blk_lo), int(blk_hi), int(n_users)
         self.ws = ops.ip_topk_workspace(n_users, catalog, k, catalog.items.device)
         self.rws = None
@@ -259,6 +298,9 @@ def catalog_sharded_owner(users, shard, k: int, group=None, exchange_bound: bool
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     U = users.shape[0]
+    if k > getattr(shard, "k_max", k):
+        raise NotImplementedError(f"the owner protocol's shard screen handles k <= {shard.k_max}; "
+                                  f"use catalog_sharded_topk (merge protocol) for k = {k}")
     m = bound_width(k, world) if exchange_bound else 0
     b = shard.screen(users, max(m, 1))
     bounds = None

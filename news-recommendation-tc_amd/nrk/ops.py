@@ -392,10 +392,24 @@ def row_normalize(x, norms=False):
 
 
 # -------------------------------------------------------------------- DIN --
+DIN_KERNEL_ITEM_FEATS = (1, 2, 4, 8)  # item-feature counts the attention kernels are instantiated for
+
+
 class DinParams:
     """Device-resident DIN weights in kernel layout (DINModel state_dict,
     DIN.py:133-212): concatenated embedding table (fp32 or bf16 storage),
-    per-feature row offsets, prepared attention matrices and the MLP."""
+    per-feature row offsets, prepared attention matrices and the MLP.
+
+    Any embedding width D (``din_embedding_dim``, config.py:115; the
+    state_dict's table width) and any item-feature count up to 8 32-wide
+    features: the kernels read 32-wide VIRTUAL features.  Every table is
+    zero-padded to m = ceil(D / 32) * 32 columns and viewed as [m * vocab, 32]
+    (feature f's index i -> virtual indices m i + h), att_w0 / mlp_w0 get
+    zero columns at the padded positions, and the item features are padded
+    with a shared all-zero row up to 1, 2, 4 or 8 -- every extra product is
+    an exact 0, so the results are those of the D-wide model.  ``n_user`` /
+    ``n_item`` / ``n_ctx`` / ``vocab`` describe the caller's features;
+    ``kn_*`` the kernel's (include/nrk.h, nrk_din_remap_index)."""
 
     def __init__(self, state_dict, user_feats, item_feats, ctx_feats, table_dtype="fp32",
                  device="cuda"):
@@ -406,15 +420,43 @@ class DinParams:
             v = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
             return np.ascontiguousarray(v, dtype=np.float32)
 
+        user_feats, item_feats, ctx_feats = list(user_feats), list(item_feats), list(ctx_feats)
         groups = ([("user_profile_embedding_dict", f) for f in user_feats]
                   + [("item_embedding_dict", f) for f in item_feats]
                   + [("context_embedding_dict", f) for f in ctx_feats])
         tabs = [arr(f"{g}.{f}.weight") for g, f in groups]
-        for t in tabs:
-            if t.shape[1] != 32:
-                raise NotImplementedError("the DIN kernels are compiled for embedding dim 32")
-        base = np.cumsum([0] + [t.shape[0] for t in tabs[:-1]]).astype(np.int64)
-        table = torch.from_numpy(np.concatenate(tabs, 0))
+        if not tabs or not item_feats or not user_feats:
+            raise ValueError("DIN needs at least one user and one item feature")
+        D = tabs[0].shape[1]
+        if any(t.ndim != 2 or t.shape[1] != D for t in tabs):
+            raise ValueError("every embedding table must have the same width (din_embedding_dim)")
+        m = -(-D // 32)
+        Fu, Fi, Fc = len(user_feats), len(item_feats), len(ctx_feats)
+        niv = m * Fi
+        kni = next((n for n in DIN_KERNEL_ITEM_FEATS if n >= niv), None)
+        if kni is None:
+            raise NotImplementedError(f"DIN item features x ceil(dim / 32) must be <= 8, got {Fi} x {m}")
+        self.dim, self.m = D, m
+        self.n_user, self.n_item, self.n_ctx = Fu, Fi, Fc
+        self.vocab = [t.shape[0] for t in tabs]
+        self.kn_user, self.kn_item, self.kn_ctx = m * Fu, kni, m * Fc
+
+        def virt(t):  # [v, D] -> [m v, 32], zero-padded columns
+            if D == 32 * m:
+                return t.reshape(-1, 32)
+            tp = np.zeros((t.shape[0], 32 * m), np.float32)
+            tp[:, :D] = t
+            return tp.reshape(-1, 32)
+
+        vt = [virt(t) for t in tabs]
+        pieces = vt[:Fu] + vt[Fu:Fu + Fi] + ([np.zeros((1, 32), np.float32)] if kni > niv else []) + vt[Fu + Fi:]
+        starts = np.cumsum([0] + [pc.shape[0] for pc in pieces[:-1]]).astype(np.int64)
+        fb = list(starts[:Fu + Fi]) + list(starts[Fu + Fi + (1 if kni > niv else 0):])  # per caller feature
+        zero_row = int(starts[Fu + Fi]) if kni > niv else 0
+        base = ([fb[f] for f in range(Fu) for _ in range(m)]
+                + [fb[Fu + f] for f in range(Fi) for _ in range(m)] + [zero_row] * (kni - niv)
+                + [fb[Fu + Fi + f] for f in range(Fc) for _ in range(m)])
+        table = torch.from_numpy(np.concatenate(pieces, 0))
         _finite(table, "DIN embedding tables")
         if table_dtype == "bf16":
             self.table = table.to(torch.bfloat16).to(device).contiguous()
@@ -424,32 +466,69 @@ class DinParams:
             self.table_code = 0
         else:
             raise ValueError("table_dtype must be 'fp32' or 'bf16'")
-        self.row_base = torch.from_numpy(base).to(device)
-        self.vocab = [t.shape[0] for t in tabs]
-        self.n_user, self.n_item, self.n_ctx = len(user_feats), len(item_feats), len(ctx_feats)
-        if self.n_item not in (1, 2, 4):
-            # the attention kernels are instantiated for 1, 2 or 4 item features
-            raise NotImplementedError("DIN supports 1, 2 or 4 item features, got %d" % self.n_item)
-        d = lambda k: torch.from_numpy(arr(k)).to(device).contiguous()  # noqa: E731
-        self.att_w0 = d("activation_unit.mlp.0.weight")
-        self.att_b0 = d("activation_unit.mlp.0.bias")
-        self.att_w1 = d("activation_unit.mlp.2.weight").reshape(-1).contiguous()
-        self.att_b1 = d("activation_unit.mlp.2.bias")
-        self.mlp_w0, self.mlp_b0 = d("mlp.0.weight"), d("mlp.0.bias")
-        self.mlp_w1, self.mlp_b1 = d("mlp.2.weight"), d("mlp.2.bias")
-        self.mlp_w2 = d("mlp.4.weight").reshape(-1).contiguous()
-        self.mlp_b2 = d("mlp.4.bias")
+        self.row_base = torch.from_numpy(np.asarray(base, np.int64)).to(device)
+
+        # index maps to the virtual layout (None: identity, no remap launch)
+        def idx_map(F, pad_to):
+            src = [f for f in range(F) for _ in range(m)] + [-1] * (pad_to - m * F)
+            mul = [m] * (m * F) + [0] * (pad_to - m * F)
+            add = [h for _ in range(F) for h in range(m)] + [0] * (pad_to - m * F)
+            return torch.tensor([src, mul, add], dtype=torch.int32).to(device).contiguous()
+
+        self.map_user = None if m == 1 else idx_map(Fu, m * Fu)
+        self.map_item = None if m == 1 and kni == Fi else idx_map(Fi, kni)
+        self.map_ctx = None if m == 1 or Fc == 0 else idx_map(Fc, m * Fc)
+
+        d = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(device).contiguous()  # noqa: E731
+        aw0 = arr("activation_unit.mlp.0.weight")
+        w0 = arr("mlp.0.weight")
+        if aw0.shape != (36, 4 * Fi * D) or w0.shape[1] != D * (Fu + Fc + 2 * Fi):
+            raise ValueError("state_dict shapes do not match the feature lists")
+
+        def expand(w, F, pad_to):  # [rows, F D] -> [rows, pad_to * 32]
+            x = np.zeros((w.shape[0], F, 32 * m), np.float32)
+            x[:, :, :D] = w.reshape(w.shape[0], F, D)
+            x = x.reshape(w.shape[0], F * m * 32)
+            if pad_to * 32 > x.shape[1]:
+                x = np.concatenate([x, np.zeros((w.shape[0], pad_to * 32 - x.shape[1]), np.float32)], 1)
+            return x
+
+        self.att_w0 = d(np.concatenate([expand(aw0[:, q * Fi * D:(q + 1) * Fi * D], Fi, kni) for q in range(4)], 1))
+        cuts = np.cumsum([0, Fu * D, Fc * D, Fi * D, Fi * D])
+        segs = [(0, Fu, m * Fu), (1, Fc, m * Fc), (2, Fi, kni), (3, Fi, kni)]
+        self.mlp_w0 = d(np.concatenate([expand(w0[:, cuts[i]:cuts[i + 1]], F, pt) for i, F, pt in segs], 1))
+        self.att_b0 = d(arr("activation_unit.mlp.0.bias"))
+        self.att_w1 = d(arr("activation_unit.mlp.2.weight").reshape(-1))
+        self.att_b1 = d(arr("activation_unit.mlp.2.bias"))
+        self.mlp_b0 = d(arr("mlp.0.bias"))
+        self.mlp_w1, self.mlp_b1 = d(arr("mlp.2.weight")), d(arr("mlp.2.bias"))
+        self.mlp_w2 = d(arr("mlp.4.weight").reshape(-1))
+        self.mlp_b2 = d(arr("mlp.4.bias"))
         for name in ("att_w0", "att_b0", "att_w1", "att_b1", "mlp_w0", "mlp_b0", "mlp_w1", "mlp_b1", "mlp_w2",
                      "mlp_b2"):
             _finite(getattr(self, name), f"DIN weight {name}")
         self.h1, self.h2 = self.mlp_w0.shape[0], self.mlp_w1.shape[0]
-        in_dim = 32 * (self.n_user + self.n_ctx + 2 * self.n_item)
-        if self.att_w0.shape != (36, 4 * 32 * self.n_item) or self.mlp_w0.shape[1] != in_dim:
+        if self.mlp_w1.shape[1] != self.h1 or self.mlp_w2.numel() != self.h2 or self.att_w1.numel() != 36:
             raise ValueError("state_dict shapes do not match the feature lists")
-        nb = _lib.lib().nrk_din_prep_bytes(self.n_item)
+        nb = _lib.lib().nrk_din_prep_bytes(self.kn_item)
         self.prep = torch.empty(nb, dtype=torch.uint8, device=device)
-        _lib.call("nrk_din_prepare", _ptr(self.att_w0), self.n_item, _ptr(self.table), self.table_code,
+        _lib.call("nrk_din_prepare", _ptr(self.att_w0), self.kn_item, _ptr(self.table), self.table_code,
                   self.table.shape[0], _ptr(self.prep), _stream())
+
+    def kernel_indices(self, user, item, hist, ctx):
+        """Caller index tensors -> the kernel's virtual-feature layout
+        (nrk_din_remap_index); identity for 32-wide models with 1/2/4/8 item
+        features."""
+        def remap(t, mp, f_in):
+            if mp is None:
+                return t
+            rows = t.numel() // f_in
+            out = torch.empty(t.shape[:-1] + (mp.shape[1],), dtype=torch.int32, device=t.device)
+            _lib.call("nrk_din_remap_index", _ptr(t), rows, f_in, _ptr(mp), mp.shape[1], _ptr(out), _stream())
+            return out
+
+        return (remap(user, self.map_user, self.n_user), remap(item, self.map_item, self.n_item),
+                remap(hist, self.map_item, self.n_item), remap(ctx, self.map_ctx, self.n_ctx))
 
 
 def din_validate(p: DinParams, user, item, hist, ctx):
@@ -497,17 +576,18 @@ def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspa
     _need(mask, torch.float32, (B, T), "mask")
     if validate:
         din_validate(p, user, item, hist, ctx)
+    user, item, hist, ctx = p.kernel_indices(user, item, hist, ctx)
     if out is not None:
         _need(out, torch.float32, (B,), "out")
         probs = out
     else:
         probs = torch.empty(B, dtype=torch.float32, device=mask.device)
     lg = torch.empty(B, dtype=torch.float32, device=mask.device) if logits else None
-    nb = _lib.lib().nrk_din_segments_workspace_bytes(B, S, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
+    nb = _lib.lib().nrk_din_segments_workspace_bytes(B, S, T, p.kn_user, p.kn_item, p.kn_ctx, p.h1, p.h2)
     if workspace is None or workspace.numel() < nb:
         workspace = torch.empty(nb, dtype=torch.uint8, device=mask.device)
-    _lib.call("nrk_din_forward_segments", _ptr(p.table), p.table_code, _ptr(p.row_base), p.n_user,
-              p.n_item, p.n_ctx, _ptr(user), _ptr(item), _ptr(hist), _ptr(ctx), _ptr(mask), B, S, T,
+    _lib.call("nrk_din_forward_segments", _ptr(p.table), p.table_code, _ptr(p.row_base), p.kn_user,
+              p.kn_item, p.kn_ctx, _ptr(user), _ptr(item), _ptr(hist), _ptr(ctx), _ptr(mask), B, S, T,
               _ptr(p.prep), _ptr(p.att_b0), _ptr(p.att_w1), _ptr(p.att_b1), _ptr(p.mlp_w0),
               _ptr(p.mlp_b0), p.h1, _ptr(p.mlp_w1), _ptr(p.mlp_b1), p.h2, _ptr(p.mlp_w2),
               _ptr(p.mlp_b2), _ptr(probs), _ptr(lg), _ptr(workspace), workspace.numel(), _stream())
@@ -520,7 +600,7 @@ def din_forward(p: DinParams, user, item, hist, ctx, mask, logits=False, workspa
 
 def din_workspace(p: DinParams, B, T, device, batch_size=None):
     S = _din_seg(B, batch_size)
-    nb = _lib.lib().nrk_din_segments_workspace_bytes(B, S, T, p.n_user, p.n_item, p.n_ctx, p.h1, p.h2)
+    nb = _lib.lib().nrk_din_segments_workspace_bytes(B, S, T, p.kn_user, p.kn_item, p.kn_ctx, p.h1, p.h2)
     return torch.empty(nb, dtype=torch.uint8, device=device)
 
 

@@ -11,9 +11,10 @@ into arrays and builds the output dict.
 
 Exactness: global / local min-max and every strategy run the reference's
 float64 operations in the reference's order (bit-identical scores, identical
-lists and tie order).  The z-score normalisation takes each method's mean /
-std from numpy on the host, exactly as the reference does (np.mean / np.std,
-:141-145); its sigmoid uses the device exp (within 1 ulp of numpy's).
+lists and tie order).  The z-score normalisation (:155-175) runs on the host
+exactly as the reference does -- numpy mean / std of the method's scores and
+numpy's exp for the sigmoid, so those scores are the reference's to the bit --
+and the device takes them as pre-normalised.
 """
 from __future__ import annotations
 

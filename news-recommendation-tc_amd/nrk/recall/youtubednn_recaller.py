@@ -118,7 +118,11 @@ class YoutubeDNNRecaller(BaseRecaller):
             raise ValueError("Model not trained. Call train() first.")
         n_users = self.user_embeddings.shape[0]
         arr = np.asarray(user_ids)
-        if arr.dtype.kind in "iu" and arr.ndim == 1 and self._user_index.is_unique:
+        # the int64 index path only where the cast is value-preserving: signed
+        # ids, or unsigned ids below 2^63 (a larger uint64 would wrap onto
+        # another user); everything else takes the dict lookup
+        fits = arr.dtype.kind == "i" or (arr.dtype.kind == "u" and (arr.size == 0 or int(arr.max()) < 2 ** 63))
+        if fits and arr.ndim == 1 and self._user_index.is_unique:
             idx = self._user_index.get_indexer(arr.astype(np.int64))
         else:  # str / float / mixed ids: the reference's own dict lookup (user_rawid_2_index.get, :511)
             idx = np.array([self.user_rawid_2_index.get(u, -1) for u in user_ids], np.int64)

@@ -544,6 +544,127 @@ def gen_din_encode(tmp):
 
 
 # --------------------------------------------------------------------------
+# Rank pipeline drop-in: DINRanker.load -> load_model(load_dir) -> predict
+# (DIN.py:529-558, :1328-1399, :1219-1283) on an artifact directory written
+# the way the reference's feature step and save_model lay it out
+# (config.py:141-161, DIN.py:1285-1326), then rank_and_recommend
+# (rank_pipeline.py:143-191).
+# --------------------------------------------------------------------------
+RP_USERS, RP_ITEMS, RP_ROWS = 70, 160, 400
+
+
+def rank_pipeline_data(seed):
+    """Feature-step outputs of one synthetic data set (plain Python / pandas
+    objects, the shapes FeatureExtractor saves): main_df with int context bins
+    (so ``main_df.iloc[i]`` is an int64 row and ``str(user_id)`` hits the
+    str-keyed dicts), user profiles (float values), item features (int
+    values), histories of str item ids (some unknown, some longer than
+    din_seq_max_len)."""
+    import pandas as pd
+
+    rng = np.random.default_rng(seed)
+    users = [str(u) for u in range(2000, 2000 + RP_USERS)]
+    items = [str(i) for i in range(7000, 7000 + RP_ITEMS)]
+    upd = {u: {f: float(np.round(rng.random() * 6, 1)) for f in USER_FEATS} for u in users[: RP_USERS - 4]}
+    ifd = {it: {f: int(rng.integers(0, 15)) for f in ITEM_FEATS} for it in items[: RP_ITEMS - 8]}
+    uhd = {}
+    for u in users[3:]:
+        L = int(rng.integers(0, 42))
+        uhd[u] = [items[int(x)] for x in rng.integers(0, RP_ITEMS, L)]
+    main = pd.DataFrame({"user_id": [int(users[x]) for x in rng.integers(0, RP_USERS, RP_ROWS)],
+                         "item_id": [int(items[x]) for x in rng.integers(0, RP_ITEMS, RP_ROWS)]})
+    for f in CTX_FEATS:
+        main[f] = rng.integers(0, 10, RP_ROWS)
+    main["label"] = rng.integers(0, 2, RP_ROWS)
+    lists = {"user_profile_features": list(USER_FEATS), "item_features": list(ITEM_FEATS),
+             "context_features": list(CTX_FEATS)}
+    return main, upd, ifd, uhd, lists
+
+
+def write_rank_artifacts(save_path, main, upd, ifd, uhd, lists):
+    import pickle
+
+    os.makedirs(save_path, exist_ok=True)
+    main.to_csv(os.path.join(save_path, "main_features.csv"), index=False)
+    for name, obj in (("user_profile_dict", upd), ("item_features_dict", ifd), ("user_history_dict", uhd),
+                      ("feature_lists", lists)):
+        with open(os.path.join(save_path, name + ".pkl"), "wb") as f:
+            pickle.dump(obj, f)
+
+
+def gen_rank_pipeline(tmp):
+    import pickle
+
+    import pandas as pd
+    import torch
+    from src.rank.DIN import DINModel, DINRanker
+    from src.utils.config import RankConfig
+
+    torch.set_num_threads(8)
+    out = {}
+    for dim in (32, 16, 64):
+        root = os.path.join(tmp, f"rank_{dim}")
+        main, upd, ifd, uhd, lists = rank_pipeline_data(41 + dim)
+        cfg = RankConfig(_project_root=root, din_embedding_dim=dim, batch_size=128, num_workers=0,
+                         pin_memory=False)
+        write_rank_artifacts(cfg.save_path, main, upd, ifd, uhd, lists)
+        # the trained model: reference vocabularies, reference init (seeded),
+        # saved with the reference's own save_model + the encoders train() pickles
+        r0 = DINRanker(cfg)
+        r0.load()
+        uv, iv, cv = r0._prepare_vocab_dicts()
+        seed_all(23 + dim)
+        r0.model = DINModel(uv, iv, cv, embedding_dim=dim, attention_hidden_units=[36],
+                            mlp_hidden_units=[200, 80], activation="dice")
+        with torch.no_grad():  # spread the attention weights so the history matters
+            r0.model.activation_unit.mlp[0].weight.mul_(4.0)
+        r0.save_model(cfg.save_path)
+        with open(os.path.join(cfg.save_path, "label_encoders.pkl"), "wb") as f:
+            pickle.dump(r0.label_encoders, f)
+        sd = torch.load(os.path.join(cfg.save_path, "din_model.pth"), weights_only=True)
+        # the reference's serving path, executed: RankPipeline.load_model
+        # (rank_pipeline.py:96-103) then predict() at two batch sizes
+        probs = {}
+        for bs in (128, 100):
+            r = DINRanker(RankConfig(_project_root=root, din_embedding_dim=dim, batch_size=bs, num_workers=0,
+                                     pin_memory=False))
+            r.load()
+            r.load_model(load_dir=cfg.save_path)
+            probs[bs] = r.predict().astype(np.float32)
+        # rank_and_recommend (rank_pipeline.py:162-174), top_k = 5 on the bs-128 scores
+        df = pd.read_csv(cfg.main_features_path)
+        df["rank_score"] = probs[128]
+        rec_u, rec_i, rec_s = [], [], []
+        for user_id, group in df.groupby("user_id"):
+            top = group.nlargest(5, "rank_score")[["item_id", "rank_score"]]
+            for _, row in top.iterrows():
+                rec_u.append(str(user_id))
+                rec_i.append(str(row["item_id"]))
+                rec_s.append(float(row["rank_score"]))
+        p = f"d{dim}_"
+        out.update({p + k: v for k, v in (
+            ("main", main[["user_id", "item_id"] + CTX_FEATS + ["label"]].to_numpy(np.int64)),
+            ("prof_users", np.array(list(upd), dtype=str)),
+            ("prof_vals", np.array([[upd[u][f] for f in USER_FEATS] for u in upd], np.float64)),
+            ("ifeat_items", np.array(list(ifd), dtype=str)),
+            ("ifeat_vals", np.array([[ifd[i][f] for f in ITEM_FEATS] for i in ifd], np.int64)),
+            ("hist_users", np.array(list(uhd), dtype=str)),
+            ("hist_offsets", np.cumsum([0] + [len(v) for v in uhd.values()]).astype(np.int64)),
+            ("hist_items", np.array([i for v in uhd.values() for i in v], dtype=str)),
+            ("probs_bs128", probs[128]), ("probs_bs100", probs[100]),
+            ("rec_user", np.array(rec_u, dtype=str)), ("rec_item", np.array(rec_i, dtype=str)),
+            ("rec_score", np.array(rec_s, np.float64)))})
+        out.update({f"{p}sd::{k}": v.numpy() for k, v in sd.items()})
+        for f, le in r0.label_encoders.items():  # object (str) classes stored as a unicode array
+            c = np.asarray(le.classes_)
+            out[f"{p}classes::{f}"] = c.astype(str) if c.dtype == object else c
+    out["user_feats"], out["item_feats"], out["ctx_feats"] = (np.array(USER_FEATS), np.array(ITEM_FEATS),
+                                                               np.array(CTX_FEATS))
+    np.savez_compressed(os.path.join(HERE, "rank_pipeline_small.npz"), **out)
+    print("rank_pipeline_small: DINRanker.load/load_model/predict at D in {32, 16, 64}, bs 128 / 100")
+
+
+# --------------------------------------------------------------------------
 # RecallFusion.fuse (fusion.py:67-342), every strategy x normalisation
 # --------------------------------------------------------------------------
 def fusion_inputs():
@@ -730,6 +851,7 @@ def main():
     gen_embsim(tmp)
     gen_fusion(tmp)
     gen_ctxfeat(tmp)
+    gen_rank_pipeline(tmp)
 
 
 if __name__ == "__main__":

@@ -31,7 +31,7 @@ def test_binding_covers_header():
 
 def test_host_queries_without_gpu():
     L = _lib.lib()
-    assert L.nrk_abi_version() == 1
+    assert L.nrk_abi_version() == 2
     assert L.nrk_ip_catalog_bytes(364047, 32) > 364047 * 32 * 2
     assert L.nrk_ip_topk_workspace_bytes(250000, 364047, 32, 31) > 0
 
@@ -59,10 +59,19 @@ def test_argument_errors_raise_valueerror():
 
 
 def test_din_prepare_refuses_unsupported_item_counts():
-    # the forward is instantiated for 1, 2 or 4 item features; prepare refuses
-    # the others before touching any pointer (fail at build time)
+    # the forward is instantiated for 1, 2, 4 or 8 (32-wide) item features
+    # (ops.DinParams pads other counts); prepare refuses the others before
+    # touching any pointer (fail at build time)
     L = _lib.lib()
-    for n_item in (3, 5, 8):
+    for n_item in (3, 5, 6, 7, 9):
         rc = L.nrk_din_prepare(1, n_item, 1, 1, 10, 1, None)
-        assert rc == _lib.NRK_EUNSUPPORTED, n_item
-        assert b"n_item must be 1, 2 or 4" in L.nrk_last_error()
+        assert rc in (_lib.NRK_EUNSUPPORTED, _lib.NRK_EINVAL), n_item
+        assert b"n_item must be" in L.nrk_last_error()
+
+
+def test_din_remap_index_arguments():
+    L = _lib.lib()
+    assert L.nrk_din_remap_index(None, 0, 4, None, 8, None, None) == _lib.NRK_OK  # nothing to do
+    assert L.nrk_din_remap_index(None, 10, 4, None, 8, None, None) == _lib.NRK_EINVAL
+    assert b"null pointer" in L.nrk_last_error()
+    assert L.nrk_din_remap_index(None, 10, 0, None, 8, None, None) == _lib.NRK_EINVAL

@@ -60,8 +60,9 @@ def test_din_bf16_tables_vs_oracle(golden, tag):
     np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
 
 
-def synth_model(rng, vocab_u, vocab_i, vocab_c, h1=200, h2=80, scale=0.05):
-    """Random DINModel-shaped state_dict (DIN.py:133-212 parameter names)."""
+def synth_model(rng, vocab_u, vocab_i, vocab_c, h1=200, h2=80, scale=0.05, dim=32):
+    """Random DINModel-shaped state_dict (DIN.py:133-212 parameter names)
+    at embedding width ``dim``."""
     f32 = np.float32
     uf = [f"u{n}" for n in range(len(vocab_u))]
     itf = [f"i{n}" for n in range(len(vocab_i))]
@@ -71,11 +72,11 @@ def synth_model(rng, vocab_u, vocab_i, vocab_c, h1=200, h2=80, scale=0.05):
                             ("item_embedding_dict", itf, vocab_i),
                             ("context_embedding_dict", cf, vocab_c)):
         for f, v in zip(names, voc):
-            sd[f"{grp}.{f}.weight"] = (rng.standard_normal((v, 32)) * 0.1).astype(f32)
+            sd[f"{grp}.{f}.weight"] = (rng.standard_normal((v, dim)) * 0.1).astype(f32)
     ni = len(itf)
-    in_dim = 32 * (len(uf) + len(cf) + 2 * ni)
+    in_dim = dim * (len(uf) + len(cf) + 2 * ni)
     lin = lambda o, i: (rng.standard_normal((o, i)) * (scale * 8 / np.sqrt(i))).astype(f32)  # noqa: E731
-    sd["activation_unit.mlp.0.weight"] = lin(36, 128 * ni)
+    sd["activation_unit.mlp.0.weight"] = lin(36, 4 * dim * ni)
     sd["activation_unit.mlp.0.bias"] = (rng.standard_normal(36) * 0.1).astype(f32)
     sd["activation_unit.mlp.2.weight"] = lin(1, 36)
     sd["activation_unit.mlp.2.bias"] = np.array([0.1], f32)
@@ -115,6 +116,34 @@ def test_din_vs_oracle(B, T, n_item, n_ctx, h1, h2, table_dtype):
     rng = np.random.default_rng(B * 131 + T)
     vu, vi, vc = [50, 300, 7, 2000, 90], [60, 900, 5000, 70][:n_item], [12] * n_ctx
     sd, feats = synth_model(rng, vu, vi, vc, h1, h2)
+    b = synth_batch(rng, B, T, vu, vi, vc)
+    probs, lg = _run(sd, feats, b, table_dtype)
+    po, lo, _ = oracle.din_forward(sd, b["user"], b["item"], b["hist"], b["ctx"], b["mask"], feats,
+                                   round_bf16=table_dtype == "bf16")
+    np.testing.assert_allclose(probs, po, atol=TOL, rtol=0)
+    np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
+
+
+@pytest.mark.parametrize(
+    "dim,n_item,T,B,table_dtype",
+    [
+        (16, 4, 50, 700, "bf16"),   # din_embedding_dim 16: tables zero-padded to 32
+        (16, 3, 30, 300, "fp32"),   # 3 item features -> padded to 4 with the zero row
+        (64, 4, 50, 700, "bf16"),   # 64 = two 32-wide virtual features each -> 8 item features
+        (64, 2, 70, 257, "fp32"),   # T > 64 (general path) at 4 virtual item features
+        (8, 1, 20, 129, "bf16"),    # tiny width, one item feature
+        (48, 3, 50, 200, "bf16"),   # 48 -> 64 padded, 2 x 3 = 6 -> 8 item features
+        (32, 3, 50, 500, "bf16"),   # 3 item features at the native width
+        (32, 6, 40, 300, "fp32"),   # 6 -> 8
+    ],
+)
+def test_din_embedding_dims_vs_oracle(dim, n_item, T, B, table_dtype):
+    """Any din_embedding_dim (config.py:115) and item-feature count: the
+    32-wide virtual-feature layout of ops.DinParams (zero padding, split
+    rows, padding features) against the oracle run at the model's own width."""
+    rng = np.random.default_rng(dim * 1000 + n_item * 10 + T)
+    vu, vi, vc = [50, 300, 7], [60, 900, 5000, 70, 40, 33][:n_item], [12] * 5
+    sd, feats = synth_model(rng, vu, vi, vc, dim=dim)
     b = synth_batch(rng, B, T, vu, vi, vc)
     probs, lg = _run(sd, feats, b, table_dtype)
     po, lo, _ = oracle.din_forward(sd, b["user"], b["item"], b["hist"], b["ctx"], b["mask"], feats,

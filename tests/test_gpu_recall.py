@@ -305,6 +305,35 @@ def test_catalog_shards_merge_equals_single(ops, n_shards):
     assert np.array_equal(r1.cpu().numpy(), ro)
 
 
+@pytest.mark.parametrize("n_shards,k", [(2, 129), (8, 129), (3, 300)])
+def test_catalog_shards_large_k_merge(ops, n_shards, k):
+    """k > IP_KFAST (no MFMA screen): the catalog-sharded merge protocol takes
+    each shard's exact path (no bound exchange) and merges pairwise in a tree
+    when n_shards * k exceeds one nrk_topk_merge call (8 x 129, 3 x 300);
+    the owner protocol refuses such k with an accurate message."""
+    from nrk.dist import HipRangeShard, HipShard, _default_merge, catalog_sharded_topk, shard_range
+
+    rng = np.random.default_rng(k + n_shards)
+    users = _unit(rng.standard_normal((150, 32)))
+    users[3] = 0.0
+    items = _unit(rng.standard_normal((6000, 32)))
+    items[5990] = items[10]
+    so, ro = oracle.ip_topk(users, items, k)
+    u = _dev(users)
+    shards = [HipShard(ops.Catalog(_dev(items[lo:hi])), lo, k, len(users))
+              for lo, hi in (shard_range(len(items), n_shards, r) for r in range(n_shards))]
+    assert not shards[0].bounded
+    lists = [sh.finish(u, None) for sh in shards]
+    s, r, e = _default_merge(torch.stack([x[0] for x in lists]).contiguous(),
+                             torch.stack([x[1] for x in lists]).contiguous(), k)
+    assert np.array_equal(r.cpu().numpy(), ro)
+    assert np.array_equal(s.cpu().numpy(), so)
+    s1, r1, _ = catalog_sharded_topk(u, HipShard(ops.Catalog(_dev(items)), 0, k, len(users)), k)
+    assert np.array_equal(r1.cpu().numpy(), ro)
+    with pytest.raises(NotImplementedError, match="owner protocol"):
+        HipRangeShard(ops.Catalog(_dev(items)), 0, 4, k, len(users))
+
+
 def test_catalog_shards_bound_full_size(ops):
     """8-shard replay of config 4 at the full catalog (364,047 x 32) with the
     bound exchange: merged rows / scores bit-exact vs the oracle on a sample."""
