@@ -593,6 +593,475 @@ __global__ void din_scales_kernel(const float* __restrict__ prep_ap, int ID, con
     }
 }
 
+// ------------------------------------------ 1'. att h, position-major --
+// din_att_tm_kernel (bf16 tables, T <= 64, 1 / 2 / 4 item features): the
+// same h as din_att_h2, computed for the rows that can differ and laid out
+// so the MFMA tiles need no per-sample matrix.
+//
+// * Constant-B formulation: h = (Wk - Wd) k_t + Wp (q .* k_t) + c_b with
+//   c_b = (Wq + Wd) q + b0 (DIN.py:105-114 with the batch-invariant parts
+//   folded): the weights are the MFMA's B operand, the same for every row, so
+//   a 16-row A tile may hold rows of 16 different samples.  Exact-f32-class:
+//   k (bf16) is exact in fp16 at the power-of-two scale s; q .* k at scale
+//   s^2 is an exact fp32 product of two fp16 values, split as
+//   P_hi = fp16(k q) (v_pk_mul_f16) and P_lo = fp16(k q - P_hi)
+//   (v_pk_fma_f16: the residual is exact in fp16); W = W_hi + W_lo.
+//   5 MFMAs per (16 x 16 tile, k-step): k W1_hi, k W1_lo, P_hi Wp_hi,
+//   P_hi Wp_lo, P_lo Wp_hi (the dropped P_lo Wp_lo term is ~2^-22 relative).
+// * Only real rows: a row whose mask is 0 and whose indices are all 0 (the
+//   collate's padding, DIN.py:476-490) has k_t = the item tables' row 0, so
+//   its h is the sample's "pad row" h_pad,b; every row at or past
+//   n_b = 1 + the last other row is such a row.  Rows t < n_b are computed
+//   and stored; for t >= n_b only h_pad,b is computed, once per sample, and
+//   enters the Dice statistics of every column t >= n_b through a
+//   difference array (samples sorted by n_b, D(t) = sum of the pad rows of
+//   the samples with n_b = t, P(t) = sum_{t' <= t} D(t')).  h rows t >= n_b
+//   are left unwritten: their mask is 0, and din_wh2 never reads a masked
+//   row's h.  At config 3 (hist_len ~ U[1, 50], 20% empty) that is ~21 of
+//   50 rows per sample.
+// * Position-major tiles: a workgroup (8 waves, 1 per CU at ~150 KB of LDS)
+//   takes a run of SW = 128 samples of ONE Dice batch, sorts them by n_b
+//   (descending, stable), so the samples with a real row at position t are
+//   the prefix [0, c_t) -- ceil(c_t / 16) tiles whose rows all share t.  A
+//   wave claims positions dynamically (LDS counter, largest first); the
+//   column sums of h and h^2 at t (fp64) are a lane-local sum over the
+//   tile's rows plus a 4-group butterfly, added once into the workgroup's
+//   row R[t] (which starts at P(t)).  Deterministic: every sum's order is
+//   fixed by the data, not by which wave ran it.
+// * Per tile the next tile's k rows and the one after's indices are in
+//   flight; all loads are unconditional (clamped rows), h goes out through
+//   buffer stores whose out-of-range offsets the hardware drops.
+constexpr int TM_SW = 128;  // samples per workgroup
+constexpr int TM_TMAX = 64; // positions (T)
+
+struct DinScalesTM {
+    float s;       // table scale: max |table| s <= 2^7, so |q k| s^2 <= 2^14 fits fp16
+    float s_w;     // W1 = Wk - Wd at s_w, Wp at s_w / s (both <= 2^14)
+    float inv;     // 1 / (s_w s): the accumulator's scale
+    float s_qd;    // Wqd = Wq + Wd at s_qd
+    float inv_qd;  // 1 / (s_qd s)
+    float pad[11];
+};
+
+__host__ __device__ constexpr size_t din_tm_base(int n_item) {
+    return (((size_t)3 * DIN_H * n_item * DIN_E * 4 + 64) + 255) & ~(size_t)255;
+}
+// prep layout past the round-3 part: [DinScalesTM, 256 B][wpack: 3 jt x NI
+// k-steps x 4 parts x 64 lanes x 16 B][qdpack: 3 x NI x 2 x 64 x 16 B]
+__host__ __device__ constexpr size_t din_tm_bytes(int n_item) { return 256 + (size_t)3 * n_item * 6 * 64 * 16; }
+
+__global__ void din_tm_scales_kernel(const float* __restrict__ prep_f, int ID, const unsigned int* __restrict__ tmax,
+                                     DinScalesTM* __restrict__ out) {
+    const int n = DIN_H * ID;
+    float ma = 0.0f, mp = 0.0f, mq = 0.0f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        ma = fmaxf(ma, fabsf(prep_f[i]));
+        mq = fmaxf(mq, fabsf(prep_f[n + i]));
+        mp = fmaxf(mp, fabsf(prep_f[2 * n + i]));
+    }
+    __shared__ float red[3][256];
+    red[0][threadIdx.x] = ma;
+    red[1][threadIdx.x] = mp;
+    red[2][threadIdx.x] = mq;
+    __syncthreads();
+    for (int d = 128; d > 0; d >>= 1) {
+        if ((int)threadIdx.x < d)
+            for (int c = 0; c < 3; ++c) red[c][threadIdx.x] = fmaxf(red[c][threadIdx.x], red[c][threadIdx.x + d]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float tm = __uint_as_float(*tmax);
+        float s = tm > 0.0f ? pow2_scale(tm) * 0.0078125f : 1.0f;  // max |table| s in [2^6, 2^7)
+        s = fminf(s, 1.0995116e12f);                                  // <= 2^40: s_w s stays finite
+        float s_w = pow2_scale(fmaxf(red[0][0], red[1][0] / s));
+        s_w = fminf(s_w, 1.1529215e18f);                              // <= 2^60
+        DinScalesTM o = {};
+        o.s = s;
+        o.s_w = s_w;
+        o.inv = 1.0f / (s_w * s);
+        o.s_qd = fminf(pow2_scale(red[2][0]), 1.1529215e18f);
+        o.inv_qd = 1.0f / (o.s_qd * s);
+        *out = o;
+    }
+}
+
+// fragment (jt, s, lane) of a [36 x ID] matrix as the MFMA B operand: 8
+// consecutive k of output column 16 jt + (lane & 15), zero past 36
+__global__ void din_tm_pack_kernel(const float* __restrict__ prep_f, int NI, const DinScalesTM* __restrict__ sc,
+                                   din_half8* __restrict__ wpack, din_half8* __restrict__ qdpack) {
+    const int ID = NI * DIN_E, n = DIN_H * ID;
+    const int total = 3 * 3 * NI * 64;  // (matrix, jt, s, lane)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int lane = i % 64, s = (i / 64) % NI, jt = (i / (64 * NI)) % 3, m = i / (64 * NI * 3);
+        const int j = 16 * jt + (lane & 15), k = DIN_E * s + 8 * (lane >> 4);
+        const float* src = m == 0 ? prep_f : m == 1 ? prep_f + 2 * n : prep_f + n;  // W1, Wp, Wqd
+        const float scale = m == 0 ? sc->s_w : m == 1 ? sc->s_w / sc->s : sc->s_qd;
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = j < DIN_H ? src[j * ID + k + e] : 0.0f;
+        din_half8 hi, lo;
+        split8(x, scale, hi, lo);
+        if (m < 2) {
+            din_half8* o = wpack + ((size_t)(jt * NI + s) * 4 + 2 * m) * 64 + lane;
+            o[0] = hi;
+            o[64] = lo;
+        } else {
+            din_half8* o = qdpack + ((size_t)(jt * NI + s) * 2) * 64 + lane;
+            o[0] = hi;
+            o[64] = lo;
+        }
+    }
+}
+
+typedef uint32_t tm_u4 __attribute__((ext_vector_type(4)));
+
+// 8 bf16 (one 16-B piece of a row) -> 8 fp16 at scale s (exact for normal results)
+__device__ __forceinline__ din_half8 tm_cvt(const tm_u4& w, float s) {
+    tm_u4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float lo = __uint_as_float(w[i] << 16) * s;
+        const float hi = __uint_as_float(w[i] & 0xFFFF0000u) * s;
+        o[i] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(lo, hi));
+    }
+    return __builtin_bit_cast(din_half8, o);
+}
+
+static inline size_t din_tm_lds(int NI, int T) {
+    const int ID = NI * DIN_E;
+    return (size_t)3 * NI * 4 * 1024                 // W fragments
+           + (size_t)TM_SW * (ID * 2 + 16)             // q rows (fp16, padded stride)
+           + (size_t)DIN_H * (TM_SW + 4) * 4           // c^T (acc init), padded stride
+           + (size_t)TM_SW * DIN_H * 4                 // pad-row h
+           + (size_t)T * DIN_H * 16                    // R: (sum, sumsq) per (t, j)
+           + (size_t)TM_SW * 4 * 2 + (TM_TMAX + 4) * 4;  // perm, n_b, c_t, counter
+}
+
+template <int NI>
+__global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
+    const uint16_t* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
+    const int32_t* __restrict__ item_idx, const int32_t* __restrict__ hist_idx, const float* __restrict__ mask,
+    int64_t N, int64_t S, int G, int T, const uint8_t* __restrict__ tm, const float* __restrict__ att_b0,
+    float* __restrict__ h_out, double* __restrict__ partial) {
+    constexpr int ID = NI * DIN_E;
+    constexpr int QS = ID * 2 + 16;  // q row stride (bytes): 16-B bank shift per row
+    constexpr int CTS = TM_SW + 4;   // c^T row stride (floats)
+    extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
+    din_half8* wl = reinterpret_cast<din_half8*>(tm_lds);
+    uint8_t* ql = tm_lds + 3 * NI * 4 * 1024;
+    float* ct = reinterpret_cast<float*>(ql + TM_SW * QS);
+    float* hp = ct + DIN_H * CTS;
+    double2* R = reinterpret_cast<double2*>(hp + TM_SW * DIN_H);
+    int* perm = reinterpret_cast<int*>(R + T * DIN_H);
+    int* nbs = perm + TM_SW;
+    int* cnt = nbs + TM_SW;        // c_t, t < T
+    int* next_t = cnt + TM_TMAX;   // position claim counter
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lg = lane >> 4;
+    const int64_t seg = blockIdx.x / G, g = blockIdx.x % G;
+    const int64_t b0 = seg * S + g * TM_SW;
+    const int64_t seg_end = (seg + 1) * S < N ? (seg + 1) * S : N;
+    const int nw = (int)(seg_end - b0 < TM_SW ? seg_end - b0 : TM_SW);
+    double2* dst = reinterpret_cast<double2*>(partial) + (size_t)blockIdx.x * T * DIN_H;
+    if (nw <= 0) {  // a short last batch leaves trailing workgroups empty: zero partial rows
+        for (int e = tid; e < T * DIN_H; e += 512) dst[e] = make_double2(0.0, 0.0);
+        return;
+    }
+    const DinScalesTM sc = *reinterpret_cast<const DinScalesTM*>(tm);
+    const din_half8* wpack = reinterpret_cast<const din_half8*>(tm + 256);
+    const din_half8* qdpack = wpack + 3 * NI * 4 * 64;
+
+    // ---- phase 0: W fragments -> LDS; n_b of every sample
+    {
+        const tm_u4* src = reinterpret_cast<const tm_u4*>(wpack);
+        tm_u4* d = reinterpret_cast<tm_u4*>(wl);
+        for (int c = tid; c < 3 * NI * 4 * 64; c += 512) d[c] = src[c];
+    }
+    {
+        bool nz[16];
+        const bool act = lane < T;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = wv * 16 + u;
+            const int64_t b = b0 + (i < nw ? i : nw - 1);
+            const size_t r = (size_t)b * T + (act ? lane : 0);
+            const float m = mask[r];
+            bool any = m != 0.0f;
+            if constexpr (NI == 4) {
+                const int4 x = *reinterpret_cast<const int4*>(hist_idx + r * 4);
+                any |= (x.x | x.y | x.z | x.w) != 0;
+            } else if constexpr (NI == 2) {
+                const int2 x = *reinterpret_cast<const int2*>(hist_idx + r * 2);
+                any |= (x.x | x.y) != 0;
+            } else {
+                any |= hist_idx[r] != 0;
+            }
+            nz[u] = any && act;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(nz[u]);
+            const int i = wv * 16 + u;
+            if (lane == 0) nbs[i] = i < nw ? (bal ? 64 - __builtin_clzll(bal) : 0) : -1;
+        }
+        if (tid == 0) *next_t = 0;
+    }
+    __syncthreads();
+    // ---- phase 1: stable sort by n_b descending -> perm; c_t = #{n_b > t}
+    if (tid < TM_SW) {
+        const int my = nbs[tid];
+        int rank = 0;
+        for (int j = 0; j < TM_SW; j += 4) {
+            const int4 v = *reinterpret_cast<const int4*>(nbs + j);
+            rank += (v.x > my || (v.x == my && j < tid)) + (v.y > my || (v.y == my && j + 1 < tid)) +
+                    (v.z > my || (v.z == my && j + 2 < tid)) + (v.w > my || (v.w == my && j + 3 < tid));
+        }
+        perm[rank] = tid;
+    } else if (tid < TM_SW + T) {
+        const int t = tid - TM_SW;
+        int c = 0;
+        for (int j = 0; j < TM_SW; j += 4) {
+            const int4 v = *reinterpret_cast<const int4*>(nbs + j);
+            c += (v.x > t) + (v.y > t) + (v.z > t) + (v.w > t);
+        }
+        cnt[t] = c;
+    }
+    __syncthreads();
+    // ---- phase 2: q rows of the sorted samples (fp16 at scale s)
+    for (int task = tid; task < TM_SW * NI * 4; task += 512) {
+        const int p = task / (NI * 4), f = (task / 4) % NI, c = task % 4;
+        const int pc = p < nw ? p : 0;
+        const int64_t b = b0 + perm[pc];
+        const int32_t qi = item_idx[b * NI + f];
+        const tm_u4 raw = *reinterpret_cast<const tm_u4*>(table + (row_base[n_user + f] + qi) * DIN_E + 8 * c);
+        din_half8 v = tm_cvt(raw, sc.s);
+        if (p >= nw) v = din_half8{};
+        *reinterpret_cast<din_half8*>(ql + p * QS + (f * DIN_E + 8 * c) * 2) = v;
+    }
+    __syncthreads();
+    // ---- phase 3: c_b = (Wq + Wd) q + b0 for 16 samples per wave (MFMA),
+    // stored pre-scaled (x s_w s) and transposed as the accumulator init
+    {
+        const float b0j[3] = {att_b0[lr], att_b0[16 + lr], 32 + lr < DIN_H ? att_b0[32 + lr] : 0.0f};
+        din_f4 acc[3];
+#pragma unroll
+        for (int jt = 0; jt < 3; ++jt) acc[jt] = din_f4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int p = wv * 16 + lr;
+#pragma unroll
+        for (int s = 0; s < NI; ++s) {
+            const din_half8 a = *reinterpret_cast<const din_half8*>(ql + p * QS + (DIN_E * s + 8 * lg) * 2);
+#pragma unroll
+            for (int jt = 0; jt < 3; ++jt) {
+                const din_half8 bh = qdpack[((jt * NI + s) * 2) * 64 + lane];
+                const din_half8 bl = qdpack[((jt * NI + s) * 2 + 1) * 64 + lane];
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bh, acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bl, acc[jt], 0, 0, 0);
+            }
+        }
+        const float to_acc = sc.s_w * sc.s;
+#pragma unroll
+        for (int jt = 0; jt < 3; ++jt) {
+            const int j = 16 * jt + lr;
+            if (j < DIN_H) {
+                din_f4 c;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) c[r] = (acc[jt][r] * sc.inv_qd + b0j[jt]) * to_acc;
+                *reinterpret_cast<din_f4*>(ct + j * CTS + wv * 16 + 4 * lg) = c;
+            }
+        }
+    }
+    __syncthreads();
+
+    // one 16-row tile: rows = sorted positions 16 i + (lane & 15) for the A
+    // operand; k fragments kf[s]; accumulator starts at c^T
+    auto tile_mfma = [&](int i, const din_half8 (&kf)[NI], int pa, din_f4 (&acc)[3]) {
+#pragma unroll
+        for (int jt = 0; jt < 3; ++jt) {
+            const int j = 16 * jt + lr < DIN_H ? 16 * jt + lr : DIN_H - 1;
+            acc[jt] = *reinterpret_cast<const din_f4*>(ct + j * CTS + 16 * i + 4 * lg);
+        }
+#pragma unroll
+        for (int s = 0; s < NI; ++s) {
+            const din_half8 qf = *reinterpret_cast<const din_half8*>(ql + pa * QS + (DIN_E * s + 8 * lg) * 2);
+            const din_half8 ph = kf[s] * qf;
+            const din_half8 pl = __builtin_elementwise_fma(kf[s], qf, -ph);
+#pragma unroll
+            for (int jt = 0; jt < 3; ++jt) {
+                const din_half8* w = wl + ((jt * NI + s) * 4) * 64 + lane;
+                const din_half8 w1h = w[0], w1l = w[64], wph = w[128], wpl = w[192];
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], w1h, acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], w1l, acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, wph, acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, wpl, acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl, wph, acc[jt], 0, 0, 0);
+            }
+        }
+    };
+
+    // ---- phase 4: pad rows (k = row 0 of every item table) of the samples
+    // with n_b < T: sorted positions [c_{T-1}, nw)
+    {
+        din_half8 k0[NI];
+#pragma unroll
+        for (int s = 0; s < NI; ++s)
+            k0[s] = tm_cvt(*reinterpret_cast<const tm_u4*>(table + row_base[n_user + s] * DIN_E + 8 * lg), sc.s);
+        const int pad_lo = cnt[T - 1];
+        for (int i = pad_lo / 16 + wv; i * 16 < nw; i += 8) {
+            const int pa = 16 * i + lr < nw ? 16 * i + lr : nw - 1;
+            din_f4 acc[3];
+            tile_mfma(i, k0, pa, acc);
+#pragma unroll
+            for (int jt = 0; jt < 3; ++jt) {
+                const int j = 16 * jt + lr;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int p = 16 * i + 4 * lg + r;
+                    if (j < DIN_H && p >= pad_lo && p < nw) hp[p * DIN_H + j] = acc[jt][r] * sc.inv;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // ---- phase 5: D(t) = sum of the pad rows of the samples with n_b = t
+    // (sorted positions [c_t, c_{t-1}), c_{-1} = nw), into R
+    for (int e = tid; e < T * DIN_H; e += 512) {
+        const int t = e / DIN_H, j = e % DIN_H;
+        const int lo = cnt[t], hi = t == 0 ? nw : cnt[t - 1];
+        double s = 0.0, ss = 0.0;
+        for (int p = lo; p < hi; ++p) {
+            const double v = (double)hp[p * DIN_H + j];
+            s += v;
+            ss += v * v;
+        }
+        R[e] = make_double2(s, ss);
+    }
+    __syncthreads();
+    // ---- phase 6: P(t) = prefix over t of D, in place (one lane per column,
+    // eight positions' loads in flight per step)
+    if (tid < DIN_H) {
+        double s = 0.0, ss = 0.0;
+        for (int t0 = 0; t0 < T; t0 += 8) {
+            double2 d[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) d[u] = R[(t0 + u < T ? t0 + u : T - 1) * DIN_H + tid];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s += d[u].x;
+                ss += d[u].y;
+                if (t0 + u < T) R[(t0 + u) * DIN_H + tid] = make_double2(s, ss);
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 7: real rows, positions claimed dynamically (largest first)
+    int t_eff = 0;  // positions with at least one real row (c_t nonincreasing)
+    while (t_eff < T && cnt[t_eff] > 0) ++t_eff;
+    auto claim = [&]() -> int {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(next_t, 1);
+        return __shfl(v, 0, WAVE);
+    };
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(h_out + b0 * T * DIN_H, 0, nw * T * DIN_H * 4, 0x00020000);
+    int64_t rbs[NI];
+#pragma unroll
+    for (int s = 0; s < NI; ++s) rbs[s] = row_base[n_user + s];
+    // job = (t, tile i); t >= t_eff: none
+    auto ntile = [&](int t) { return (cnt[t] + 15) >> 4; };
+    auto succ = [&](int t, int i, int& t2, int& i2) {
+        if (t >= t_eff) { t2 = t; i2 = 0; return; }
+        if (i + 1 < ntile(t)) { t2 = t; i2 = i + 1; return; }
+        t2 = claim();
+        t2 = t2 < t_eff ? t2 : t_eff;
+        i2 = 0;
+    };
+    // A-row position of a job (clamped into [0, c_t)) and its sample's indices
+    auto apos = [&](int t, int i) -> int {
+        if (t >= t_eff) return 0;
+        const int p = 16 * i + lr, c = cnt[t];
+        return p < c ? p : c - 1;
+    };
+    auto idx_load = [&](int t, int pa) -> int4 {
+        const int tc = t < t_eff ? t : 0;
+        const size_t r = ((size_t)(b0 + perm[pa]) * T + tc) * NI;
+        if constexpr (NI == 4) return *reinterpret_cast<const int4*>(hist_idx + r);
+        else if constexpr (NI == 2) { const int2 x = *reinterpret_cast<const int2*>(hist_idx + r); return make_int4(x.x, x.y, 0, 0); }
+        else return make_int4(hist_idx[r], 0, 0, 0);
+    };
+    auto rows_load = [&](const int4& ix, tm_u4 (&raw)[NI]) {
+        const int32_t iv[4] = {ix.x, ix.y, ix.z, ix.w};
+#pragma unroll
+        for (int s = 0; s < NI; ++s)
+            raw[s] = *reinterpret_cast<const tm_u4*>(table + (rbs[s] + iv[s]) * DIN_E + 8 * lg);
+    };
+
+    int t0 = claim();
+    t0 = t0 < t_eff ? t0 : t_eff;
+    int i0 = 0, t1, i1, t2, i2;
+    succ(t0, i0, t1, i1);
+    tm_u4 raw0[NI], raw1[NI];
+    int4 ix1;
+    {
+        const int4 ix0 = idx_load(t0, apos(t0, i0));
+        rows_load(ix0, raw0);
+        ix1 = idx_load(t1, apos(t1, i1));
+    }
+    double ssum[3], ssq[3];
+#pragma unroll
+    for (int jt = 0; jt < 3; ++jt) ssum[jt] = ssq[jt] = 0.0;
+    while (t0 < t_eff) {
+        succ(t1, i1, t2, i2);
+        const int4 ix2 = idx_load(t2, apos(t2, i2));  // indices two jobs ahead
+        rows_load(ix1, raw1);                         // rows one job ahead
+        din_half8 kf[NI];
+#pragma unroll
+        for (int s = 0; s < NI; ++s) kf[s] = tm_cvt(raw0[s], sc.s);
+        din_f4 acc[3];
+        tile_mfma(i0, kf, apos(t0, i0), acc);
+        // epilogue: store h (rows < c_t, j < 36), column sums over valid rows
+        const int c = cnt[t0];
+        const int4 smp = *reinterpret_cast<const int4*>(perm + 16 * i0 + 4 * lg);
+        const int sv[4] = {smp.x, smp.y, smp.z, smp.w};
+#pragma unroll
+        for (int jt = 0; jt < 3; ++jt) {
+            const int j = 16 * jt + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool ok = 16 * i0 + 4 * lg + r < c;
+                const float v = acc[jt][r] * sc.inv;
+                const int off = (ok && j < DIN_H) ? ((sv[r] * T + t0) * DIN_H + j) * 4 : 0x7FFFFFF0;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, off, 0, 0);
+                const double dv = ok ? (double)v : 0.0;
+                ssum[jt] += dv;
+                ssq[jt] += dv * dv;
+            }
+        }
+        if (t1 != t0) {  // last tile of t0: combine the 16 rows' lanes, add to R[t0]
+#pragma unroll
+            for (int jt = 0; jt < 3; ++jt) {
+                ssum[jt] += __shfl_xor(ssum[jt], 16, WAVE);
+                ssq[jt] += __shfl_xor(ssq[jt], 16, WAVE);
+                ssum[jt] += __shfl_xor(ssum[jt], 32, WAVE);
+                ssq[jt] += __shfl_xor(ssq[jt], 32, WAVE);
+                const int j = 16 * jt + lr;
+                if (lane < 16 && j < DIN_H) {
+                    double2* rp = R + t0 * DIN_H + j;
+                    const double2 x = *rp;
+                    *rp = make_double2(x.x + ssum[jt], x.y + ssq[jt]);
+                }
+                ssum[jt] = ssq[jt] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NI; ++s) raw0[s] = raw1[s];
+        ix1 = ix2;
+        t0 = t1; i0 = i1; t1 = t2; i1 = i2;
+    }
+    __syncthreads();
+    // ---- phase 8: the workgroup's partial row
+    for (int e = tid; e < T * DIN_H; e += 512) dst[e] = R[e];
+}
+
 // ---------------------------------------------------------- 2. col stats --
 // mean and unbiased std (torch.std default) of each column over one Dice
 // batch (segment blockIdx.x), from that segment's per-block fp64 (sum, sumsq)
@@ -1488,7 +1957,7 @@ static DinWs din_ws_layout(void* base, int64_t N, int64_t S, int T, int n_user, 
     uint8_t* p = reinterpret_cast<uint8_t*>(base);
     size_t o = 0;
     const int64_t n_seg = (N + S - 1) / S;
-    const int64_t nb_att = n_seg * din_att_groups(N, S);
+    const int64_t nb_att = n_seg * std::max<int64_t>(din_att_groups(N, S), (S + TM_SW - 1) / TM_SW);
     const int64_t nb_m = (N + 63) / 64;
     const int IN = (n_user + n_ctx + 2 * n_item) * DIN_E;
     const bool fast = din_fast(T, h1);
@@ -1537,7 +2006,7 @@ int nrk_din_remap_index(const int32_t* in, int64_t n_rows, int f_in, const int32
 
 size_t nrk_din_prep_bytes(int n_item) {
     if (n_item <= 0) return 0;
-    return (size_t)3 * DIN_H * n_item * DIN_E * sizeof(float) + 64;
+    return din_tm_base(n_item) + din_tm_bytes(n_item);
 }
 
 int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int table_dtype,
@@ -1560,6 +2029,13 @@ int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int tabl
     const int64_t g = (n + 255) / 256;
     din_absmax_kernel<<<(int)(g < 2048 ? g : 2048), 256, 0, s>>>(table, table_dtype, n, mx);
     din_scales_kernel<<<1, 256, 0, s>>>(pf, ID, mx, sc);
+    // the position-major kernel's scales and packed weight fragments
+    uint8_t* tm = reinterpret_cast<uint8_t*>(prep) + din_tm_base(n_item);
+    DinScalesTM* tsc = reinterpret_cast<DinScalesTM*>(tm);
+    din_half8* wpack = reinterpret_cast<din_half8*>(tm + 256);
+    din_tm_scales_kernel<<<1, 256, 0, s>>>(pf, ID, mx, tsc);
+    din_tm_pack_kernel<<<(3 * 3 * n_item * 64 + 255) / 256, 256, 0, s>>>(pf, n_item, tsc, wpack,
+                                                                            wpack + 3 * n_item * 4 * 64);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -1615,6 +2091,18 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     const int64_t nb_att = n_seg * G;
     NRK_REQUIRE(nb_att < (1ll << 31), "too many segments");
     const float* pf = reinterpret_cast<const float*>(prep);
+    const bool tm_path = table_dtype == 1 && T <= TM_TMAX && n_item <= 4;
+    const int G_tm = (int)((S + TM_SW - 1) / TM_SW);
+    const uint8_t* tm = reinterpret_cast<const uint8_t*>(prep) + din_tm_base(n_item);
+#define NRK_ATT_TM(NI)                                                                                 \
+    do {                                                                                               \
+        const size_t lds = din_tm_lds(NI, T);                                                          \
+        (void)hipFuncSetAttribute((const void*)din_att_tm_kernel<NI>,                                  \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
+        din_att_tm_kernel<NI><<<(unsigned)(n_seg * G_tm), 512, lds, s>>>(                              \
+            reinterpret_cast<const uint16_t*>(table), row_base, n_user, item_idx, hist_idx, mask, batch, \
+            S, G_tm, T, tm, att_b0, w.h, w.hpart);                                                     \
+    } while (0)
 #define NRK_ATT_H(TT, NI)                                                                              \
     do {                                                                                               \
         if (T <= 64 && NI <= 4 && (sizeof(TT) == 2 || NI < 4))                                         \
@@ -1630,7 +2118,9 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
                 reinterpret_cast<const TT*>(table), row_base, n_user, item_idx, hist_idx, batch, S, G,    \
                 T, pf, att_b0, w.h, w.hpart);                                                       \
     } while (0)
-    if (table_dtype == 0) {
+    if (tm_path) {
+        if (n_item == 4) NRK_ATT_TM(4); else if (n_item == 2) NRK_ATT_TM(2); else NRK_ATT_TM(1);
+    } else if (table_dtype == 0) {
         if (n_item == 8) NRK_ATT_H(float, 8); else if (n_item == 4) NRK_ATT_H(float, 4);
         else if (n_item == 2) NRK_ATT_H(float, 2); else NRK_ATT_H(float, 1);
     } else {
@@ -1638,10 +2128,12 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         else if (n_item == 2) NRK_ATT_H(uint16_t, 2); else NRK_ATT_H(uint16_t, 1);
     }
 #undef NRK_ATT_H
+#undef NRK_ATT_TM
     const int ncol_att = T * DIN_H;
     const unsigned gs = (unsigned)n_seg;
-    col_stats_kernel<<<dim3(gs, (ncol_att + 3) / 4), 256, 0, s>>>(w.hpart, G, (int)nb_att, ncol_att,
-                                                                   batch, S, w.hstats, w.hinv);
+    const int bps_att = tm_path ? G_tm : G;
+    col_stats_kernel<<<dim3(gs, (ncol_att + 3) / 4), 256, 0, s>>>(w.hpart, bps_att, (int)(n_seg * bps_att),
+                                                                   ncol_att, batch, S, w.hstats, w.hinv);
     const int64_t gb = (batch + 3) / 4;
     const int64_t nb_m = (batch + 63) / 64;
     const int bps = n_seg == 1 ? (int)nb_m : (int)(S / 64);  // 64-row GEMM blocks per segment

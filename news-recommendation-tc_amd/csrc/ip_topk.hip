@@ -47,7 +47,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int IP_KFAST = 128;   // largest k on the screen path
 constexpr int IP_KMAX = 2048;   // largest k at all (exact path above IP_KFAST)
-constexpr int IP_SEL = 256;     // appended maxima >= theta_lb held by the select
+constexpr int IP_SEL = 512;     // appended maxima >= theta_lb held by the select
 constexpr int IP_BQ = 288;      // largest band (k = 128); the refine holds SV + 32 entries
 constexpr int IP_KRING = 256;   // prefilter-kept rows awaiting an exact round (ring, power of two)
 constexpr size_t CATALOG_HDR = 256;
@@ -235,11 +235,17 @@ __device__ __forceinline__ void top_insert(float (&t)[MT], float v) {
 // Scan: NW waves x UG x 32 users per workgroup share one NSL-slot LDS ring of
 // catalog tiles (8 KB, or one 16-KB block at dim 256).  Per tile every wave
 // reads the tile's A fragments once and runs TB x DS x UG MFMAs.
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false>
+// APP = false, tstep > 1: pass 1 of the two-pass screen -- the tiles
+// tile_lo, tile_lo + tstep, ... only, no appends: the record's list bound
+// is then a lower bound of the user's k-th half-block maximum over that
+// sample (its items are real items), which pass 2 (ip_scan_fixed_kernel)
+// uses as a fixed threshold over the whole catalog.
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false,
+          bool APP = true>
 __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
     int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
-    float4* __restrict__ uinfo, int tile_lo, int tile_hi) {
+    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int tstep = 1) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
     constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : 8192 / BLOCK_BYTES;
@@ -334,8 +340,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     // 1-KB piece per wave-instruction, no VGPR staging); tiles past the end
     // re-load the last piece (keeps the per-wave vmcnt accounting uniform,
     // the data is never used).
-    auto issue_tile = [&](int tt) {
-        uint8_t* slot = smem + (tt % NSL) * TILE_BYTES;
+    auto issue_tile = [&](int tt, int sl) {
+        uint8_t* slot = smem + sl * TILE_BYTES;
 #pragma unroll
         for (int p = 0; p < LPT; ++p) {
             const int piece = p * NW + wave;
@@ -351,8 +357,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     // would otherwise drain the in-flight LDS-DMA (the ring prefetch) in
     // front of a compiler-visible LDS access, and a separate wait statement
     // would let the compiler copy an output before the data landed
-    auto read_frags = [&](int tt, u32x4 (&afr)[TB * DS]) {
-        const uint32_t base = lds0 + (uint32_t)((tt % NSL) * TILE_BYTES);
+    auto read_frags = [&](int sl, u32x4 (&afr)[TB * DS]) {
+        const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES);
 #pragma unroll
         for (int g = 0; g < TB * DS; g += 8) {
             u32x4* f = &afr[g];
@@ -370,8 +376,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     };
     // one block's DS fragments (FULLREAD = false: fewer live registers,
     // one LDS round trip per block)
-    auto read_block = [&](int tt, int b, u32x4 (&af)[DS]) {
-        const uint32_t base = lds0 + (uint32_t)((tt % NSL) * TILE_BYTES + b * DS * 1024);
+    auto read_block = [&](int sl, int b, u32x4 (&af)[DS]) {
+        const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
         if constexpr (DS == 1) {
             asm volatile("ds_read_b128 %0, %1 offset:0\n\ts_waitcnt lgkmcnt(0)" : "=&v"(af[0]) : "v"(base) : "memory");
         } else {
@@ -387,7 +393,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     float pend[UG];  // IE = 2: the lane's largest max since its group's last insert
 #pragma unroll
     for (int g = 0; g < UG; ++g) pend[g] = -INFINITY;
-    auto tile = [&](int tt, const u32x4 (&afr)[FULLREAD ? TB * DS : 1], auto mask_c, int) {
+    auto tile = [&](int tt, int sl, const u32x4 (&afr)[FULLREAD ? TB * DS : 1], auto mask_c, int) {
         constexpr bool MASK = decltype(mask_c)::value;
         float mx[UG][TB];
 #pragma unroll
@@ -397,7 +403,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
 #pragma unroll
                 for (int s = 0; s < DS; ++s) afb[s] = afr[b * DS + s];
             } else {
-                read_block(tt, b, afb);
+                read_block(sl, b, afb);
             }
             // the UG independent accumulation chains interleaved, so one
             // group's reduction overlaps the other's MFMAs
@@ -442,7 +448,8 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         // their tile, so the select's thresholds (>= theta_lb, >= cut, both
         // above every tau) never take them.
         bool any_app = false;
-        if constexpr (TAPP) {
+        if constexpr (!APP) {
+        } else if constexpr (TAPP) {
 #pragma unroll
             for (int g = 0; g < UG; ++g) any_app |= vt[g] >= tau[g];
         } else {
@@ -526,21 +533,22 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         }
     };
 
-    auto step = [&](int tt, int ig_c) {
+    auto step = [&](int tt, int it) {
         // own pieces of tile tt landed (the next NSL-2 tiles' stay in
         // flight; appends issued since only make the wait conservative); the
-        // barrier publishes everyone's pieces and retires slot (tt-1) % NSL
+        // barrier publishes everyone's pieces and retires the previous slot
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * (NSL - 2)) : "memory");
         __builtin_amdgcn_s_barrier();
-        issue_tile(tt + NSL - 1);
+        issue_tile(tt + (NSL - 1) * tstep, (it + NSL - 1) % NSL);
+        const int sl = it % NSL;
         u32x4 afr[FULLREAD ? TB * DS : 1];
-        if constexpr (FULLREAD) read_frags(tt, afr);
-        if (tt < full_tiles) tile(tt, afr, std::false_type{}, ig_c);
-        else tile(tt, afr, std::true_type{}, ig_c);
+        if constexpr (FULLREAD) read_frags(sl, afr);
+        if (tt < full_tiles) tile(tt, sl, afr, std::false_type{}, 0);
+        else tile(tt, sl, afr, std::true_type{}, 0);
     };
 #pragma unroll
-    for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p);
-    for (int tt = tile_lo; tt < ntile; ++tt) step(tt, 0);
+    for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p * tstep, p);
+    for (int tt = tile_lo, it = 0; tt < ntile; tt += tstep, ++it) step(tt, it);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
 
 #pragma unroll
@@ -551,6 +559,167 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             acnt[(size_t)user * 2 + h] = cnt[g];
             if (h == 0) uinfo[user] = make_float4(live[g] ? lb : -INFINITY, eps_s[g], scl[g], eps_u[g]);
         }
+    }
+}
+
+// Pass 2 of the two-pass screen: every tile of [tile_lo, tile_hi) against a
+// FIXED per-user threshold from pass 1's record, tau = lb - 2 eps rounded
+// down (ip_scan_kernel's retau) -- no register list, no inserts.  Per
+// (block, user group): 2 MFMAs (D = 32), 8 v_max3 and one compare; the
+// append branch runs only when some lane of the wave passes.  Correctness
+// is the one-pass scan's invariant with lb = pass 1's list bound: lb is a
+// lower bound of the user's k-th half-block maximum (its values are real
+// items' fp16 scores of the sample), and every half-block maximum >= tau is
+// appended, so the select's theta_lb / theta / band reasoning holds as is.
+// The fp16 user fragments are recomputed exactly as pass 1 computed them.
+template <int DP, int NW, int NSL, int UG, int WPE>
+__global__ __launch_bounds__(NW * 64, WPE) void ip_scan_fixed_kernel(
+    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items, int dim,
+    int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt, const float4* __restrict__ uinfo, int tile_lo,
+    int tile_hi) {
+    constexpr int DS = DP / 16;
+    constexpr int BLOCK_BYTES = 64 * DP;
+    constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : 8192 / BLOCK_BYTES;
+    constexpr int TILE_BYTES = TB * BLOCK_BYTES;
+    constexpr int LPT = TILE_BYTES / (NW * 1024);
+    static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
+    static_assert(NSL >= 2, "ring");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NSL * TILE_BYTES];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
+    const int ubase = blockIdx.x * (NW * 32 * UG) + wave * (32 * UG);
+    const int nblk = (n_items + 31) >> 5;
+    const int ntile = tile_hi;
+
+    f16x8 ufrag[UG][DS];
+    float tau[UG];
+    int cnt[UG];
+    uint2* dst[UG];
+#pragma unroll
+    for (int g = 0; g < UG; ++g) {
+        const int user = ubase + g * 32 + q;
+        const bool active = user < n_users;
+        float uval[DS][8];
+        float nrm2 = 0.0f, uabs = 0.0f;
+        const float* urow = users + (size_t)(active ? user : 0) * dim;
+#pragma unroll
+        for (int s = 0; s < DS; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int d = 16 * s + 8 * h + e;
+                const float f = (active && d < dim) ? urow[d] : 0.0f;
+                uval[s][e] = f;
+                nrm2 += f * f;
+                uabs = fmaxf(uabs, fabsf(f));
+            }
+        nrm2 += __shfl_xor(nrm2, 32, WAVE);
+        uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
+        const float su = pow2_scale(uabs);
+#pragma unroll
+        for (int s = 0; s < DS; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ufrag[g][s][e] = (_Float16)(uval[s][e] * su);
+        const float4 inf = uinfo[active ? user : 0];
+        const bool live = active && nrm2 > 0.0f;
+        tau[g] = !live ? INFINITY : inf.x == -INFINITY ? -FLT_MAX : round_down_sub(inf.x, 2.0f * inf.y);
+        cnt[g] = 0;
+        dst[g] = app + ((size_t)(active ? user : 0) * 2 + h) * (size_t)m2;
+    }
+
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
+    const int body_bytes = nblk * BLOCK_BYTES;
+    const int tail_blk = n_items >> 5;
+    auto issue_tile = [&](int tt, int sl) {
+        uint8_t* slot = smem + sl * TILE_BYTES;
+#pragma unroll
+        for (int p = 0; p < LPT; ++p) {
+            const int piece = p * NW + wave;
+            int off = tt * TILE_BYTES + piece * 1024;
+            off = off < body_bytes ? off : body_bytes - 1024;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(catalog + off + lane * 16),
+                (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16, 0, 0);
+        }
+    };
+    const uint32_t lds0 = lds_base + lane * 16;
+    auto read_block = [&](int sl, int b, u32x4 (&af)[DS]) {
+        const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
+        if constexpr (DS == 1) {
+            asm volatile("ds_read_b128 %0, %1 offset:0\n\ts_waitcnt lgkmcnt(0)" : "=&v"(af[0]) : "v"(base) : "memory");
+        } else {
+#pragma unroll
+            for (int s2 = 0; s2 < DS; s2 += 2)
+                asm volatile("ds_read_b128 %0, %2 offset:0\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                             : "=&v"(af[s2]), "=&v"(af[s2 + 1])
+                             : "v"(base + 1024u * s2)
+                             : "memory");
+        }
+    };
+    const int full_tiles = tail_blk / TB;
+    auto tile = [&](int tt, int sl, auto mask_c) {
+        constexpr bool MASK = decltype(mask_c)::value;
+#pragma unroll
+        for (int b = 0; b < TB; ++b) {
+            u32x4 afb[DS];
+            read_block(sl, b, afb);
+            f32x16 acc[UG];
+#pragma unroll
+            for (int g = 0; g < UG; ++g) acc[g] = f32x16{};
+#pragma unroll
+            for (int s = 0; s < DS; ++s)
+#pragma unroll
+                for (int g = 0; g < UG; ++g)
+                    acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[s]), ufrag[g][s],
+                                                                    acc[g], 0, 0, 0);
+            float mx[UG];
+            bool any = false;
+#pragma unroll
+            for (int g = 0; g < UG; ++g) {
+                if constexpr (MASK) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = (tt * TB + b) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (row >= n_items) acc[g][r] = -INFINITY;
+                    }
+                }
+                float v = fmaxf(fmaxf(acc[g][0], acc[g][1]), acc[g][2]);
+#pragma unroll
+                for (int r = 3; r < 15; r += 2) v = fmaxf(fmaxf(v, acc[g][r]), acc[g][r + 1]);
+                mx[g] = fmaxf(v, acc[g][15]);
+                any |= mx[g] >= tau[g];
+            }
+            // appends: the half-block maxima >= tau (the count runs past the
+            // capacity -- the select then sends the user to the exact path --
+            // and extra entries land on the last slot)
+            if (__builtin_amdgcn_ballot_w64(any)) {
+                const uint32_t id = (uint32_t)((tt * TB + b) * 2 + h);
+#pragma unroll
+                for (int g = 0; g < UG; ++g) {
+                    const bool a = mx[g] >= tau[g];
+                    if (a) dst[g][min(cnt[g], m2 - 1)] = make_uint2(__float_as_uint(mx[g]), id);
+                    cnt[g] += a ? 1 : 0;
+                }
+            }
+        }
+    };
+    auto step = [&](int tt, int it) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * (NSL - 2)) : "memory");
+        __builtin_amdgcn_s_barrier();
+        issue_tile(tt + NSL - 1, (it + NSL - 1) % NSL);
+        const int sl = it % NSL;
+        if (tt < full_tiles) tile(tt, sl, std::false_type{});
+        else tile(tt, sl, std::true_type{});
+    };
+#pragma unroll
+    for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p, p);
+    for (int tt = tile_lo, it = 0; tt < ntile; ++tt, ++it) step(tt, it);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+#pragma unroll
+    for (int g = 0; g < UG; ++g) {
+        const int user = ubase + g * 32 + q;
+        if (user < n_users) acnt[(size_t)user * 2 + h] = cnt[g];
     }
 }
 
@@ -1790,6 +1959,21 @@ static inline int next_pow2(int x) {
 
 // scan variants: (DP, waves per workgroup, ring slots, user groups per wave,
 // register list length, waves per SIMD)
+// Two-pass screen (large catalogs, k * SCAN_SAMPLE <= 256): pass 1 runs the
+// list scan over every SCAN_SAMPLE-th tile without appends; its list bound
+// (a valid lower bound of the k-th half-block maximum: the sample's items
+// are real items) becomes pass 2's fixed threshold over the whole range
+// (ip_scan_fixed_kernel: no inserts, the MFMA-paced loop).  Appends ~ the
+// half-blocks above the sample's k-th maximum (~ k * SCAN_SAMPLE / 2 per lane
+// half), the select's theta_lb filter keeps ~ k * SCAN_SAMPLE (<= IP_SEL).
+constexpr int SCAN_SAMPLE = 8;
+constexpr bool SCAN_TWO_PASS = false;  // under evaluation (round 4)
+static inline bool scan_two_pass(int k, int tb, int t_lo, int t_hi) {
+    const int mt = (k + 1) / 2;
+    const int per_lane = tb * ((t_hi - t_lo) / SCAN_SAMPLE);  // pass-1 half-blocks per lane
+    return SCAN_TWO_PASS && k * SCAN_SAMPLE <= 256 && per_lane >= 32 * mt;
+}
+
 template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false>
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
@@ -1797,7 +1981,17 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
     constexpr int TB = 64 * DP >= 8192 ? 1 : 8192 / (64 * DP);
     const int nblk = (n_items + 31) / 32;
     const int t_lo = w.blk_lo / TB, t_hi = (std::min(w.blk_hi, nblk) + TB - 1) / TB;
-    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<(n_users + per_wg - 1) / per_wg, NW * 64, 0, s>>>(
+    const unsigned grid = (unsigned)((n_users + per_wg - 1) / per_wg);
+    if (scan_two_pass(k, TB, t_lo, t_hi)) {
+        ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP, false><<<grid, NW * 64, 0, s>>>(
+            users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, SCAN_SAMPLE);
+        constexpr int NW2 = 8, NSL2 = 3, UG2 = DP <= 64 ? 4 : 2, WPE2 = 2;
+        const int per_wg2 = NW2 * 32 * UG2;
+        ip_scan_fixed_kernel<DP, NW2, NSL2, UG2, WPE2><<<(n_users + per_wg2 - 1) / per_wg2, NW2 * 64, 0, s>>>(
+            users, n_users, cat, n_items, dim, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi);
+        return;
+    }
+    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<grid, NW * 64, 0, s>>>(
         users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi);
 }
 

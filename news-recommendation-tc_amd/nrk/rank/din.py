@@ -173,7 +173,10 @@ class DINRanker(BaseRanker):
         self.item_features = list(item_features)
         self.context_features = list(context_features)
         self.label_encoders = label_encoders
-        self.encoder, self._tables = None, None
+        self.encoder = DinEncoder(user_profile_dict, item_features_dict, user_history_dict,
+                                  self.user_profile_features, self.item_features, self.context_features,
+                                  label_encoders, self.config.din_seq_max_len)
+        self._tables = None
         return self
 
     def _prepare_vocab_dicts(self):

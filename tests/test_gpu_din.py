@@ -162,6 +162,44 @@ def test_din_all_history_masked():
     np.testing.assert_allclose(probs, po, atol=TOL, rtol=0)
 
 
+@pytest.mark.parametrize("case", ["holes", "unit_masks", "full", "mixed_len", "t64", "t1"])
+def test_din_position_major_edges(case):
+    """The position-major attention kernel (bf16 tables, T <= 64) computes
+    only rows before each sample's last non-padding row and enters the
+    padding rows' h through a per-sample pad row: masks that are not
+    prefixes (mask 0 with non-zero indices, mask != 0 with all-zero
+    indices, fractional masks), every row real, ragged lengths around the
+    16-row tiles, T = 64 and T = 1 -- all against the oracle at 1e-5."""
+    rng = np.random.default_rng(["holes", "unit_masks", "full", "mixed_len", "t64", "t1"].index(case) + 71)
+    vu, vi, vc = [50, 300, 7], [60, 900, 5000, 70], [12] * 4
+    sd, feats = synth_model(rng, vu, vi, vc)
+    T = {"t64": 64, "t1": 1}.get(case, 50)
+    B = 700
+    b = synth_batch(rng, B, T, vu, vi, vc)
+    if case == "holes":
+        # interior padding-like rows (mask 0, indices 0), masked rows with real
+        # indices, and unmasked rows whose indices are all 0
+        b["mask"][:, 3:6] = 0.0
+        b["hist"][:, 3:5] = 0
+        b["hist"][:50, 40] = 7
+        b["mask"][60:90, 45] = 1.0
+        b["hist"][60:90, 45] = 0
+    elif case == "unit_masks":
+        b["mask"] = b["mask"] * rng.choice([0.5, 1.0, 2.0], size=b["mask"].shape).astype(np.float32)
+    elif case == "full":
+        b["mask"][:] = 1.0
+        b["hist"] = np.stack([rng.integers(1, v, (B, T)) for v in vi], 2)
+    elif case == "mixed_len":
+        L = rng.choice([0, 1, 15, 16, 17, 31, 32, 33, T], size=B)
+        b["mask"] = (np.arange(T)[None] < L[:, None]).astype(np.float32)
+        b["hist"] = b["hist"] * b["mask"][:, :, None].astype(np.int64)
+    probs, lg = _run(sd, feats, b, "bf16")
+    po, lo, _ = oracle.din_forward(sd, b["user"], b["item"], b["hist"], b["ctx"], b["mask"], feats,
+                                   round_bf16=True)
+    np.testing.assert_allclose(probs, po, atol=TOL, rtol=0)
+    np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
+
+
 def test_din_errors():
     from nrk import ops
 
@@ -192,7 +230,8 @@ def test_din_config3_batch():
     np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
 
 
-@pytest.mark.parametrize("N,S,table_dtype", [(1000, 128, "bf16"), (257, 64, "fp32"), (2 * 4096 + 77, 4096, "bf16")])
+@pytest.mark.parametrize("N,S,table_dtype", [(1000, 128, "bf16"), (257, 64, "fp32"), (2 * 4096 + 77, 4096, "bf16"),
+                                               (1000, 192, "bf16"), (700, 64, "bf16"), (4096 + 2, 4096, "bf16")])
 def test_din_segments_vs_per_batch_oracle(N, S, table_dtype):
     """nrk_din_forward_segments: N samples as consecutive Dice batches of S in
     one call == the oracle run batch by batch (DINRanker.predict's loop);

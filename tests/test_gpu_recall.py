@@ -305,6 +305,28 @@ def test_catalog_shards_merge_equals_single(ops, n_shards):
     assert np.array_equal(r1.cpu().numpy(), ro)
 
 
+@pytest.mark.parametrize("d,k", [(32, 31), (32, 10), (16, 31), (64, 21), (32, 32)])
+def test_two_pass_screen_vs_oracle(ops, d, k):
+    """Catalogs large enough for the two-pass screen (pass 1: list scan of
+    every 8th tile, no appends; pass 2: fixed threshold over every tile,
+    ip_topk.hip scan_two_pass): rows and scores bit-exact vs the oracle for
+    every user, incl. exact duplicate items across the sampled / unsampled
+    tiles, a zero user, a user equal to an item and near-tie scores."""
+    rng = np.random.default_rng(d * 100 + k)
+    n_items = 150_000
+    users = _unit(rng.standard_normal((512, d)))
+    items = _unit(rng.standard_normal((n_items, d)))
+    users[5] = 0.0
+    items[140_001] = items[3]       # duplicate in another tile
+    items[70_000:70_040] = items[9]  # a run of duplicates inside one tile
+    users[6] = items[9]
+    users[7] = np.round(users[7] * 8) / 8  # coarse values: many near-ties
+    so, ro = oracle.ip_topk(users, items, k, nthreads=8)
+    s, r = ops.ip_topk(_dev(users), ops.Catalog(_dev(items)), k)
+    assert np.array_equal(r.cpu().numpy(), ro)
+    assert np.array_equal(s.cpu().numpy(), so)
+
+
 @pytest.mark.parametrize("n_shards,k", [(2, 129), (8, 129), (3, 300)])
 def test_catalog_shards_large_k_merge(ops, n_shards, k):
     """k > IP_KFAST (no MFMA screen): the catalog-sharded merge protocol takes
