@@ -330,10 +330,11 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
  * att_b0 [36], att_w1 [36], att_b1 [1]; mlp_w0 [h1, in], mlp_b0 [h1],
  * mlp_w1 [h2, h1], mlp_b1 [h2], mlp_w2 [h2], mlp_b2 [1]
  * with in = 32 * (n_user + n_ctx + 2 * n_item).
- * nrk_din_prepare derives the batch-invariant attention matrices and the
- * power-of-two scales of the split-fp16 attention product (from max|table|)
- * once per weight load into prep (nrk_din_prep_bytes); call it again if
- * the table changes.  B >= 2 (B = 1 is NaN in the
+ * nrk_din_prepare derives the batch-invariant attention matrices, the
+ * power-of-two scales of the split-fp16 attention products (from max|table|),
+ * the packed weight fragments and (bf16 tables) an fp16 copy of the table at
+ * that scale, once per weight load into prep (nrk_din_prep_bytes(n_item,
+ * n_table_rows)); call it again if the table changes.  B >= 2 (B = 1 is NaN in the
  * reference too). */
 /* Embedding widths other than 32 (din_embedding_dim, src/utils/config.py:115,
  * read back by DINRanker.load_model, DIN.py:1371-1379): the kernels read
@@ -349,7 +350,7 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
  * the item-feature count is 1, 2, 4 or 8 (no call needed). */
 int nrk_din_remap_index(const int32_t* in, int64_t n_rows, int f_in, const int32_t* map, int f_out,
                         int32_t* out, nrk_stream_t stream);
-size_t nrk_din_prep_bytes(int n_item);
+size_t nrk_din_prep_bytes(int n_item, int64_t n_table_rows);
 int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int table_dtype,
                     int64_t n_table_rows, void* prep, nrk_stream_t stream);
 size_t nrk_din_workspace_bytes(int64_t batch, int seq_len, int n_user, int n_item, int n_ctx,

@@ -38,46 +38,95 @@ constexpr int CTX_NMAX = 4;      // last_N
 constexpr int CTX_DC_MAX = 256;  // content dim
 constexpr int CTX_DW_MAX = 128;  // w2v dim
 
-// numpy float64 pairwise sum (loops_utils.h.src) of squares of
-// d_e = f64(f32(r[e])) - h[e]; r from global (f64 table), h from LDS
-struct SqDiff {
-    const double* r;
-    const double* h;
-    __device__ double operator()(int e) const {
-        const double d = __dsub_rn((double)(float)r[e], h[e]);
-        double p = __dmul_rn(d, d);
-        asm volatile("" : "+v"(p));  // keep the rounded square (no contraction)
+// numpy's float64 pairwise sum (loops_utils.h.src) of the squares
+// d_e^2, d_e = f64(f32(r[e])) - h[e] (r: the item's content row, f64 table;
+// h: the history row in LDS) -- restated as pw_sum64<2> below
+// The leaves of that sum, pw_sum64<2>(f, 0, n) (numpy's pairwise blocks of <= 128;
+// a leaf of n >= 8: 8 strided accumulators, a fixed tree, the tail in order)
+// and how they combine: shape 0 = l0; 1 = l0 + l1; 2 = (l0 + l1) + l2;
+// 3 = l0 + (l1 + l2); 4 = (l0 + l1) + (l2 + l3).
+struct PwPlan {
+    int nl, shape;
+    int b[4], n[4];
+};
+__device__ __forceinline__ PwPlan pw_plan(int n) {
+    PwPlan p{};
+    if (n <= 128) {
+        p.nl = 1;
+        p.b[0] = 0;
+        p.n[0] = n;
         return p;
     }
-};
-
-template <typename F>
-__device__ double pw_leaf64(const F& f, int b, int n) {
-    if (n < 8) {
-        double r = 0.0;
-        for (int i = 0; i < n; ++i) r = __dadd_rn(r, f(b + i));
-        return r;
-    }
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = f(b + j);
-    int i = 8;
-    for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = __dadd_rn(r[j], f(b + i + j));
-    }
-    double res = __dadd_rn(__dadd_rn(__dadd_rn(r[0], r[1]), __dadd_rn(r[2], r[3])),
-                           __dadd_rn(__dadd_rn(r[4], r[5]), __dadd_rn(r[6], r[7])));
-    for (; i < n; ++i) res = __dadd_rn(res, f(b + i));
-    return res;
-}
-
-template <int L, typename F>
-__device__ double pw_sum64(const F& f, int b, int n) {
-    if (L == 0 || n <= 128) return pw_leaf64(f, b, n);
     int n2 = n / 2;
     n2 -= n2 % 8;
-    return __dadd_rn(pw_sum64<(L > 0 ? L - 1 : 0)>(f, b, n2), pw_sum64<(L > 0 ? L - 1 : 0)>(f, b + n2, n - n2));
+    int k = 0;
+    const int lb[2] = {0, n2}, ln[2] = {n2, n - n2};
+    bool split[2];
+    for (int h = 0; h < 2; ++h) {
+        split[h] = ln[h] > 128;
+        if (!split[h]) {
+            p.b[k] = lb[h];
+            p.n[k++] = ln[h];
+        } else {
+            int m2 = ln[h] / 2;
+            m2 -= m2 % 8;
+            p.b[k] = lb[h];
+            p.n[k++] = m2;
+            p.b[k] = lb[h] + m2;
+            p.n[k++] = ln[h] - m2;
+        }
+    }
+    p.nl = k;
+    p.shape = (split[0] && split[1]) ? 4 : split[0] ? 2 : split[1] ? 3 : 1;
+    return p;
+}
+
+// word_diff of one (recalled row, history item) task on a half-wave (32
+// lanes): lane (leaf l, j) keeps numpy's j-th leaf accumulator (elements
+// b + j, b + j + 8, ...: 8 lanes read 64 consecutive bytes of the item row),
+// a xor-1/2/4 butterfly is the leaf's ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)),
+// lane j = 0 adds the leaf's tail in order, and the leaves combine by the
+// plan's shape -- the same operations in the same order as pw_sum64<2>, so
+// the result is bit-identical to the per-lane loop (and to numpy).
+__device__ __forceinline__ double coop_word_diff(const PwPlan& pl, const double* __restrict__ r,
+                                                 const double* __restrict__ h, int s) {
+    const int l = s >> 3, j = s & 7;
+    const bool act = l < pl.nl;
+    const int lb = act ? pl.b[l] : 0, ln = act ? pl.n[l] : 0;
+    auto f = [&](int e) {
+        const double d = __dsub_rn((double)(float)r[e], h[e]);
+        double p = __dmul_rn(d, d);
+        asm volatile("" : "+v"(p));
+        return p;
+    };
+    double acc = 0.0;
+    const int full = ln - ln % 8;
+    if (ln >= 8) {
+        acc = f(lb + j);
+        for (int i = 8; i < full; i += 8) acc = __dadd_rn(acc, f(lb + i + j));
+    }
+    // butterfly over j (the 8 lanes of the leaf)
+    acc = __dadd_rn(acc, __shfl_xor(acc, 1, WAVE));
+    acc = __dadd_rn(acc, __shfl_xor(acc, 2, WAVE));
+    acc = __dadd_rn(acc, __shfl_xor(acc, 4, WAVE));
+    if (j == 0 && act) {
+        if (ln < 8) {
+            acc = 0.0;
+            for (int i = 0; i < ln; ++i) acc = __dadd_rn(acc, f(lb + i));
+        } else {
+            for (int i = full; i < ln; ++i) acc = __dadd_rn(acc, f(lb + i));
+        }
+    }
+    const int base = threadIdx.x & 32;  // this half-wave's lane 0
+    const double v0 = __shfl(acc, base, WAVE), v1 = __shfl(acc, base + 8, WAVE);
+    const double v2 = __shfl(acc, base + 16, WAVE), v3 = __shfl(acc, base + 24, WAVE);
+    switch (pl.shape) {
+        case 0: return v0;
+        case 1: return __dadd_rn(v0, v1);
+        case 2: return __dadd_rn(__dadd_rn(v0, v1), v2);
+        case 3: return __dadd_rn(v0, __dadd_rn(v1, v2));
+        default: return __dadd_rn(__dadd_rn(v0, v1), __dadd_rn(v2, v3));
+    }
 }
 
 __device__ __forceinline__ float dot_f32(const float* a, const float* b, int n) {
@@ -103,6 +152,7 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
                                                            int32_t* __restrict__ out_codes) {
     __shared__ double s_cont[4][CTX_NMAX][CTX_DC_MAX];
     __shared__ float s_w2v[4][CTX_NMAX][CTX_DW_MAX];
+    __shared__ double s_wd[4][64][CTX_NMAX];  // word_diff of this chunk's rows
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t g = (int64_t)blockIdx.x * 4 + wv;
     if (g >= tb.n_groups) return;
@@ -126,7 +176,32 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const bool uyt = tb.user_yt != nullptr && u >= 0 && tb.user_yt_ok[u];
     const int64_t p0 = tb.group_off[g], p1 = tb.group_off[g + 1];
-    for (int64_t q = p0 + lane; q < p1; q += 64) {
+    const PwPlan plan = pw_plan(tb.dc);
+    for (int64_t c0 = p0; c0 < p1; c0 += 64) {
+        // word_diff of the chunk's rows first, two (row, history item)
+        // tasks per wave instruction (coalesced item-row reads), into LDS
+        const int nr = (int)(p1 - c0 < 64 ? p1 - c0 : 64);
+        if (hn > 0) {
+            const int ntask = nr * N;
+            for (int t0 = 0; t0 < ntask; t0 += 2) {
+                const int task = t0 + (lane >> 5);
+                const int tc = task < ntask ? task : ntask - 1;
+                const int qr = tc / N, i = tc % N;
+                const int64_t pos = tb.pair_pos ? tb.pair_pos[c0 + qr] : c0 + qr;
+                const int32_t it = tb.pair_item[pos];
+                const bool on = i < hn && hcont[i] && it >= 0 && (tb.content_flags[it] & 2);
+                const double* rrow = tb.content + (int64_t)(on ? it : 0) * tb.dc;
+                // every lane runs the (shuffling) sum; rows that do not count take 0
+                const double ss = coop_word_diff(plan, rrow, s_cont[wv][i], lane & 31);
+                const double wd = on ? sqrt(ss) : 0.0;
+                if ((lane & 31) == 0 && task < ntask) s_wd[wv][qr][i] = wd;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        const int64_t q = c0 + lane;
+        if (q >= p1) continue;
         const int64_t pos = tb.pair_pos ? tb.pair_pos[q] : q;
         const int32_t it = tb.pair_item[pos];
         double f[1 + 3 * CTX_NMAX + 6];
@@ -141,7 +216,6 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
         f[1 + 3 * N + 5] = 0.0;
         if (hn >= 0) {
             const bool iw2v = it >= 0 && tb.w2v_ok[it];
-            const uint8_t icf = it >= 0 ? tb.content_flags[it] : 0;
             const double icre = it >= 0 ? (double)(float)tb.created[it] : (double)NAN;  // f32 array (:588-594)
             float sims[CTX_NMAX];
             for (int i = 0; i < N; ++i) {
@@ -159,13 +233,8 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
                     td = d == d ? d : 0.0;
                 }
                 f[2 + 3 * i] = (double)(float)td;
-                // word_diff_i (:633-648)
-                double wd = 0.0;
-                if (hcont[i] && (icf & 2)) {
-                    SqDiff sq{tb.content + (int64_t)it * tb.dc, s_cont[wv][i]};
-                    wd = sqrt(pw_sum64<2>(sq, 0, tb.dc));
-                }
-                f[3 + 3 * i] = (double)(float)wd;
+                // word_diff_i (:633-648), computed cooperatively above
+                f[3 + 3 * i] = (double)(float)s_wd[wv][lane][i];
             }
             // nan-statistics of the sims (:660-664), float32
             float mx = -INFINITY, mn = INFINITY, tot = 0.0f;

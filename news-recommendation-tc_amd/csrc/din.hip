@@ -648,7 +648,24 @@ __host__ __device__ constexpr size_t din_tm_base(int n_item) {
 }
 // prep layout past the round-3 part: [DinScalesTM, 256 B][wpack: 3 jt x NI
 // k-steps x 4 parts x 64 lanes x 16 B][qdpack: 3 x NI x 2 x 64 x 16 B]
+// [tab16: the table at scale s as fp16, n_rows x 32, 256-B aligned]
 __host__ __device__ constexpr size_t din_tm_bytes(int n_item) { return 256 + (size_t)3 * n_item * 6 * 64 * 16; }
+__host__ __device__ constexpr size_t din_tm_tab16_off(int n_item) {
+    return (din_tm_base(n_item) + din_tm_bytes(n_item) + 255) & ~(size_t)255;
+}
+
+// tab16 = fp16(table * s): bf16 values are exact in fp16 at the power-of-two
+// scale s unless they fall below fp16's normal range (|x| < max |table| 2^-21)
+__global__ void din_tm_tab16_kernel(const uint16_t* __restrict__ table, int64_t n, const DinScalesTM* __restrict__ sc,
+                                    uint32_t* __restrict__ out) {
+    const float s = sc->s;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 2; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(table)[i];
+        const _Float16 lo = (_Float16)(__uint_as_float(w << 16) * s);
+        const _Float16 hi = (_Float16)(__uint_as_float(w & 0xFFFF0000u) * s);
+        out[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    }
+}
 
 __global__ void din_tm_scales_kernel(const float* __restrict__ prep_f, int ID, const unsigned int* __restrict__ tmax,
                                      DinScalesTM* __restrict__ out) {
@@ -715,18 +732,6 @@ __global__ void din_tm_pack_kernel(const float* __restrict__ prep_f, int NI, con
 
 typedef uint32_t tm_u4 __attribute__((ext_vector_type(4)));
 
-// 8 bf16 (one 16-B piece of a row) -> 8 fp16 at scale s (exact for normal results)
-__device__ __forceinline__ din_half8 tm_cvt(const tm_u4& w, float s) {
-    tm_u4 o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float lo = __uint_as_float(w[i] << 16) * s;
-        const float hi = __uint_as_float(w[i] & 0xFFFF0000u) * s;
-        o[i] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(lo, hi));
-    }
-    return __builtin_bit_cast(din_half8, o);
-}
-
 static inline size_t din_tm_lds(int NI, int T) {
     const int ID = NI * DIN_E;
     return (size_t)3 * NI * 4 * 1024                 // W fragments
@@ -739,7 +744,7 @@ static inline size_t din_tm_lds(int NI, int T) {
 
 template <int NI>
 __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
-    const uint16_t* __restrict__ table, const int64_t* __restrict__ row_base, int n_user,
+    const din_half8* __restrict__ tab16, const int64_t* __restrict__ row_base, int n_user,
     const int32_t* __restrict__ item_idx, const int32_t* __restrict__ hist_idx, const float* __restrict__ mask,
     int64_t N, int64_t S, int G, int T, const uint8_t* __restrict__ tm, const float* __restrict__ att_b0,
     float* __restrict__ h_out, double* __restrict__ partial) {
@@ -833,8 +838,7 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
         const int pc = p < nw ? p : 0;
         const int64_t b = b0 + perm[pc];
         const int32_t qi = item_idx[b * NI + f];
-        const tm_u4 raw = *reinterpret_cast<const tm_u4*>(table + (row_base[n_user + f] + qi) * DIN_E + 8 * c);
-        din_half8 v = tm_cvt(raw, sc.s);
+        din_half8 v = tab16[(row_base[n_user + f] + qi) * 4 + c];
         if (p >= nw) v = din_half8{};
         *reinterpret_cast<din_half8*>(ql + p * QS + (f * DIN_E + 8 * c) * 2) = v;
     }
@@ -903,8 +907,7 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
     {
         din_half8 k0[NI];
 #pragma unroll
-        for (int s = 0; s < NI; ++s)
-            k0[s] = tm_cvt(*reinterpret_cast<const tm_u4*>(table + row_base[n_user + s] * DIN_E + 8 * lg), sc.s);
+        for (int s = 0; s < NI; ++s) k0[s] = tab16[row_base[n_user + s] * 4 + lg];
         const int pad_lo = cnt[T - 1];
         for (int i = pad_lo / 16 + wv; i * 16 < nw; i += 8) {
             const int pa = 16 * i + lr < nw ? 16 * i + lr : nw - 1;
@@ -957,86 +960,87 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
     // ---- phase 7: real rows, positions claimed dynamically (largest first)
     int t_eff = 0;  // positions with at least one real row (c_t nonincreasing)
     while (t_eff < T && cnt[t_eff] > 0) ++t_eff;
-    auto claim = [&]() -> int {
-        int v = 0;
-        if (lane == 0) v = atomicAdd(next_t, 1);
-        return __shfl(v, 0, WAVE);
-    };
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(h_out + b0 * T * DIN_H, 0, nw * T * DIN_H * 4, 0x00020000);
     int64_t rbs[NI];
 #pragma unroll
-    for (int s = 0; s < NI; ++s) rbs[s] = row_base[n_user + s];
-    // job = (t, tile i); t >= t_eff: none
-    auto ntile = [&](int t) { return (cnt[t] + 15) >> 4; };
-    auto succ = [&](int t, int i, int& t2, int& i2) {
-        if (t >= t_eff) { t2 = t; i2 = 0; return; }
-        if (i + 1 < ntile(t)) { t2 = t; i2 = i + 1; return; }
-        t2 = claim();
-        t2 = t2 < t_eff ? t2 : t_eff;
-        i2 = 0;
+    for (int s = 0; s < NI; ++s) rbs[s] = row_base[n_user + s] * 4 + lg;  // in 16-B pieces
+    // job = (position t, tile i, c = c_t); t >= t_eff: none
+    struct Job {
+        int t, i, c;
+    };
+    auto claim_job = [&]() -> Job {
+        int t = 0;
+        if (lane == 0) t = atomicAdd(next_t, 1);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t >= t_eff) return Job{t_eff, 0, 0};
+        return Job{t, 0, cnt[t]};
+    };
+    auto succ = [&](const Job& j) -> Job {
+        if (j.t >= t_eff) return j;
+        if (16 * (j.i + 1) < j.c) return Job{j.t, j.i + 1, j.c};
+        return claim_job();
     };
     // A-row position of a job (clamped into [0, c_t)) and its sample's indices
-    auto apos = [&](int t, int i) -> int {
-        if (t >= t_eff) return 0;
-        const int p = 16 * i + lr, c = cnt[t];
-        return p < c ? p : c - 1;
+    auto apos = [&](const Job& j) -> int {
+        const int p = 16 * j.i + lr;
+        return j.t >= t_eff ? 0 : (p < j.c ? p : j.c - 1);
     };
-    auto idx_load = [&](int t, int pa) -> int4 {
-        const int tc = t < t_eff ? t : 0;
-        const size_t r = ((size_t)(b0 + perm[pa]) * T + tc) * NI;
+    auto idx_load = [&](const Job& j) -> int4 {
+        const int tc = j.t < t_eff ? j.t : 0;
+        const size_t r = ((size_t)(b0 + perm[apos(j)]) * T + tc) * NI;
         if constexpr (NI == 4) return *reinterpret_cast<const int4*>(hist_idx + r);
         else if constexpr (NI == 2) { const int2 x = *reinterpret_cast<const int2*>(hist_idx + r); return make_int4(x.x, x.y, 0, 0); }
         else return make_int4(hist_idx[r], 0, 0, 0);
     };
-    auto rows_load = [&](const int4& ix, tm_u4 (&raw)[NI]) {
+    auto rows_load = [&](const int4& ix, din_half8 (&kf)[NI]) {
         const int32_t iv[4] = {ix.x, ix.y, ix.z, ix.w};
 #pragma unroll
-        for (int s = 0; s < NI; ++s)
-            raw[s] = *reinterpret_cast<const tm_u4*>(table + (rbs[s] + iv[s]) * DIN_E + 8 * lg);
+        for (int s = 0; s < NI; ++s) kf[s] = tab16[rbs[s] + (int64_t)iv[s] * 4];
     };
 
-    int t0 = claim();
-    t0 = t0 < t_eff ? t0 : t_eff;
-    int i0 = 0, t1, i1, t2, i2;
-    succ(t0, i0, t1, i1);
-    tm_u4 raw0[NI], raw1[NI];
+    Job j0 = claim_job();
+    Job j1 = succ(j0);
+    din_half8 k_0[NI], k_1[NI];
     int4 ix1;
     {
-        const int4 ix0 = idx_load(t0, apos(t0, i0));
-        rows_load(ix0, raw0);
-        ix1 = idx_load(t1, apos(t1, i1));
+        const int4 ix0 = idx_load(j0);
+        rows_load(ix0, k_0);
+        ix1 = idx_load(j1);
     }
     double ssum[3], ssq[3];
 #pragma unroll
     for (int jt = 0; jt < 3; ++jt) ssum[jt] = ssq[jt] = 0.0;
-    while (t0 < t_eff) {
-        succ(t1, i1, t2, i2);
-        const int4 ix2 = idx_load(t2, apos(t2, i2));  // indices two jobs ahead
-        rows_load(ix1, raw1);                         // rows one job ahead
-        din_half8 kf[NI];
-#pragma unroll
-        for (int s = 0; s < NI; ++s) kf[s] = tm_cvt(raw0[s], sc.s);
+    while (j0.t < t_eff) {
+        const Job j2 = succ(j1);
+        const int4 ix2 = idx_load(j2);  // indices two jobs ahead
+        rows_load(ix1, k_1);            // rows one job ahead
         din_f4 acc[3];
-        tile_mfma(i0, kf, apos(t0, i0), acc);
+        tile_mfma(j0.i, k_0, apos(j0), acc);
         // epilogue: store h (rows < c_t, j < 36), column sums over valid rows
-        const int c = cnt[t0];
-        const int4 smp = *reinterpret_cast<const int4*>(perm + 16 * i0 + 4 * lg);
+        const int4 smp = *reinterpret_cast<const int4*>(perm + 16 * j0.i + 4 * lg);
         const int sv[4] = {smp.x, smp.y, smp.z, smp.w};
+        int roff[4];
+        bool rok[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            rok[r] = 16 * j0.i + 4 * lg + r < j0.c;
+            roff[r] = rok[r] ? (sv[r] * T + j0.t) * (DIN_H * 4) : 0x7FFFF000;  // past num_records: dropped
+        }
 #pragma unroll
         for (int jt = 0; jt < 3; ++jt) {
             const int j = 16 * jt + lr;
+            const bool jok = jt < 2 || lr < DIN_H - 32;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const bool ok = 16 * i0 + 4 * lg + r < c;
                 const float v = acc[jt][r] * sc.inv;
-                const int off = (ok && j < DIN_H) ? ((sv[r] * T + t0) * DIN_H + j) * 4 : 0x7FFFFFF0;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, off, 0, 0);
-                const double dv = ok ? (double)v : 0.0;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, jok ? roff[r] + 4 * j : 0x7FFFF000,
+                                                      0, 0);
+                const double dv = (double)(rok[r] ? v : 0.0f);
                 ssum[jt] += dv;
-                ssq[jt] += dv * dv;
+                ssq[jt] = fma(dv, dv, ssq[jt]);
             }
         }
-        if (t1 != t0) {  // last tile of t0: combine the 16 rows' lanes, add to R[t0]
+        if (j1.t != j0.t) {  // last tile of j0.t: combine the 16 rows' lanes, add to R[t]
 #pragma unroll
             for (int jt = 0; jt < 3; ++jt) {
                 ssum[jt] += __shfl_xor(ssum[jt], 16, WAVE);
@@ -1045,7 +1049,7 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
                 ssq[jt] += __shfl_xor(ssq[jt], 32, WAVE);
                 const int j = 16 * jt + lr;
                 if (lane < 16 && j < DIN_H) {
-                    double2* rp = R + t0 * DIN_H + j;
+                    double2* rp = R + j0.t * DIN_H + j;
                     const double2 x = *rp;
                     *rp = make_double2(x.x + ssum[jt], x.y + ssq[jt]);
                 }
@@ -1053,9 +1057,10 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
             }
         }
 #pragma unroll
-        for (int s = 0; s < NI; ++s) raw0[s] = raw1[s];
+        for (int s = 0; s < NI; ++s) k_0[s] = k_1[s];
         ix1 = ix2;
-        t0 = t1; i0 = i1; t1 = t2; i1 = i2;
+        j0 = j1;
+        j1 = j2;
     }
     __syncthreads();
     // ---- phase 8: the workgroup's partial row
@@ -2004,9 +2009,9 @@ int nrk_din_remap_index(const int32_t* in, int64_t n_rows, int f_in, const int32
     return NRK_OK;
 }
 
-size_t nrk_din_prep_bytes(int n_item) {
-    if (n_item <= 0) return 0;
-    return din_tm_base(n_item) + din_tm_bytes(n_item);
+size_t nrk_din_prep_bytes(int n_item, int64_t n_table_rows) {
+    if (n_item <= 0 || n_table_rows < 0) return 0;
+    return din_tm_tab16_off(n_item) + (size_t)n_table_rows * DIN_E * 2;
 }
 
 int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int table_dtype,
@@ -2036,6 +2041,12 @@ int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int tabl
     din_tm_scales_kernel<<<1, 256, 0, s>>>(pf, ID, mx, tsc);
     din_tm_pack_kernel<<<(3 * 3 * n_item * 64 + 255) / 256, 256, 0, s>>>(pf, n_item, tsc, wpack,
                                                                             wpack + 3 * n_item * 4 * 64);
+    if (table_dtype == 1) {  // the position-major kernel reads the item rows as fp16 (bf16 tables)
+        const int64_t nw = n_table_rows * DIN_E / 2;
+        din_tm_tab16_kernel<<<(unsigned)std::min<int64_t>((nw + 255) / 256, 4096), 256, 0, s>>>(
+            reinterpret_cast<const uint16_t*>(table), n_table_rows * DIN_E, tsc,
+            reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(prep) + din_tm_tab16_off(n_item)));
+    }
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -2100,8 +2111,9 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         (void)hipFuncSetAttribute((const void*)din_att_tm_kernel<NI>,                                  \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
         din_att_tm_kernel<NI><<<(unsigned)(n_seg * G_tm), 512, lds, s>>>(                              \
-            reinterpret_cast<const uint16_t*>(table), row_base, n_user, item_idx, hist_idx, mask, batch, \
-            S, G_tm, T, tm, att_b0, w.h, w.hpart);                                                     \
+            reinterpret_cast<const din_half8*>(reinterpret_cast<const uint8_t*>(prep) +                \
+                                               din_tm_tab16_off(n_item)),                               \
+            row_base, n_user, item_idx, hist_idx, mask, batch, S, G_tm, T, tm, att_b0, w.h, w.hpart);   \
     } while (0)
 #define NRK_ATT_H(TT, NI)                                                                              \
     do {                                                                                               \

@@ -47,6 +47,11 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int IP_KFAST = 128;   // largest k on the screen path
 constexpr int IP_KMAX = 2048;   // largest k at all (exact path above IP_KFAST)
+// screen tile: one LDS ring slot, one barrier (dev builds may try NRK_SCAN_TILE = 16384)
+#ifndef NRK_SCAN_TILE
+#define NRK_SCAN_TILE 8192
+#endif
+constexpr int SCAN_TILE = NRK_SCAN_TILE;
 constexpr int IP_SEL = 512;     // appended maxima >= theta_lb held by the select
 constexpr int IP_BQ = 288;      // largest band (k = 128); the refine holds SV + 32 entries
 constexpr int IP_KRING = 256;   // prefilter-kept rows awaiting an exact round (ring, power of two)
@@ -248,7 +253,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     float4* __restrict__ uinfo, int tile_lo, int tile_hi, int tstep = 1) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
-    constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : 8192 / BLOCK_BYTES;
+    constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
     constexpr int TILE_BYTES = TB * BLOCK_BYTES;
     constexpr int LPT = TILE_BYTES / (NW * 1024);  // 1-KB LDS-DMA pieces per wave per tile
     static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
@@ -389,6 +394,28 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                              : "memory");
         }
     };
+    // DS = 2: block b + 1's fragments are read while block b's MFMAs run --
+    // the wait for block b's data and the issue of block b + 1's reads are one
+    // asm statement whose operands tie both register sets, so nothing reads
+    // (or copies) a fragment before its wait
+    constexpr bool PF = !FULLREAD && DS == 2;
+    auto pf_issue = [&](int sl, int b, u32x4 (&af)[DS]) {
+        const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
+        asm volatile("ds_read_b128 %0, %2 offset:0\n\tds_read_b128 %1, %2 offset:1024"
+                     : "=&v"(af[0]), "=&v"(af[1])
+                     : "v"(base)
+                     : "memory");
+    };
+    auto pf_wait_issue = [&](u32x4 (&cur)[DS], int sl, int b, u32x4 (&nxt)[DS]) {
+        const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b128 %0, %4 offset:0\n\tds_read_b128 %1, %4 offset:1024"
+                     : "=&v"(nxt[0]), "=&v"(nxt[1]), "+v"(cur[0]), "+v"(cur[1])
+                     : "v"(base)
+                     : "memory");
+    };
+    auto pf_wait = [&](u32x4 (&cur)[DS]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1])::"memory");
+    };
     const int full_tiles = tail_blk / TB;  // tiles whose blocks are all full
     float pend[UG];  // IE = 2: the lane's largest max since its group's last insert
 #pragma unroll
@@ -396,10 +423,22 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     auto tile = [&](int tt, int sl, const u32x4 (&afr)[FULLREAD ? TB * DS : 1], auto mask_c, int) {
         constexpr bool MASK = decltype(mask_c)::value;
         float mx[UG][TB];
+        u32x4 afp[DS];
+        if constexpr (PF) pf_issue(sl, 0, afp);
 #pragma unroll
         for (int b = 0; b < TB; ++b) {
             u32x4 afb[DS];
-            if constexpr (FULLREAD) {
+            if constexpr (PF) {
+                u32x4 afn[DS];
+                if (b + 1 < TB) pf_wait_issue(afp, sl, b + 1, afn);
+                else pf_wait(afp);
+#pragma unroll
+                for (int s = 0; s < DS; ++s) afb[s] = afp[s];
+                if (b + 1 < TB) {
+#pragma unroll
+                    for (int s = 0; s < DS; ++s) afp[s] = afn[s];
+                }
+            } else if constexpr (FULLREAD) {
 #pragma unroll
                 for (int s = 0; s < DS; ++s) afb[s] = afr[b * DS + s];
             } else {
@@ -579,7 +618,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_fixed_kernel(
     int tile_hi) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
-    constexpr int TB = BLOCK_BYTES >= 8192 ? 1 : 8192 / BLOCK_BYTES;
+    constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
     constexpr int TILE_BYTES = TB * BLOCK_BYTES;
     constexpr int LPT = TILE_BYTES / (NW * 1024);
     static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
@@ -1907,7 +1946,7 @@ static inline int ip_m2(int64_t n_items, int k, int dim) {
     m2 = std::min<int64_t>(m2, ((nblk + 63) / 64) * 64);
     if (mt <= 16) {
         const int dp = pad_dim(dim);
-        const int64_t tb = 64 * dp >= 8192 ? 1 : 8192 / (64 * dp);
+        const int64_t tb = 64 * dp >= SCAN_TILE ? 1 : SCAN_TILE / (64 * dp);
         const int64_t ntile = (nblk + tb - 1) / tb;
         const double et = mt * (1.0 + log(std::max(1.0, (double)ntile / mt)));
         int64_t mt2 = ((tb * ((int64_t)(2.0 * et) + 16) + 63) / 64) * 64;
@@ -1966,8 +2005,15 @@ static inline int next_pow2(int x) {
 // (ip_scan_fixed_kernel: no inserts, the MFMA-paced loop).  Appends ~ the
 // half-blocks above the sample's k-th maximum (~ k * SCAN_SAMPLE / 2 per lane
 // half), the select's theta_lb filter keeps ~ k * SCAN_SAMPLE (<= IP_SEL).
-constexpr int SCAN_SAMPLE = 8;
-constexpr bool SCAN_TWO_PASS = false;  // under evaluation (round 4)
+#ifndef NRK_SCAN_SAMPLE
+#define NRK_SCAN_SAMPLE 8
+#endif
+constexpr int SCAN_SAMPLE = NRK_SCAN_SAMPLE;
+// dev builds only (`make dev`): the default library is built without it
+#ifndef NRK_SCAN_TWO_PASS
+#define NRK_SCAN_TWO_PASS 0
+#endif
+constexpr bool SCAN_TWO_PASS = NRK_SCAN_TWO_PASS;  // under evaluation (round 4)
 static inline bool scan_two_pass(int k, int tb, int t_lo, int t_hi) {
     const int mt = (k + 1) / 2;
     const int per_lane = tb * ((t_hi - t_lo) / SCAN_SAMPLE);  // pass-1 half-blocks per lane
@@ -1978,7 +2024,7 @@ template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1,
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
     const int per_wg = NW * 32 * UG;
-    constexpr int TB = 64 * DP >= 8192 ? 1 : 8192 / (64 * DP);
+    constexpr int TB = 64 * DP >= SCAN_TILE ? 1 : SCAN_TILE / (64 * DP);
     const int nblk = (n_items + 31) / 32;
     const int t_lo = w.blk_lo / TB, t_hi = (std::min(w.blk_hi, nblk) + TB - 1) / TB;
     const unsigned grid = (unsigned)((n_users + per_wg - 1) / per_wg);
@@ -2042,7 +2088,7 @@ static void scan_dispatch(const float* users, int nu, const uint8_t* cat, int ni
 
 // a tile-aligned block range of a shard (config 4), checked
 static int ip_range(IpWs& w, int64_t n_items, int dim, int64_t blk_lo, int64_t blk_hi) {
-    const int tb = 64 * pad_dim(dim) >= 8192 ? 1 : 8192 / (64 * pad_dim(dim));
+    const int tb = 64 * pad_dim(dim) >= SCAN_TILE ? 1 : SCAN_TILE / (64 * pad_dim(dim));
     NRK_REQUIRE(blk_lo >= 0 && blk_lo <= blk_hi && blk_hi <= n_blocks_of(n_items), "block range out of bounds");
     NRK_REQUIRE(blk_lo == blk_hi || (blk_lo % tb == 0 && (blk_hi % tb == 0 || blk_hi == n_blocks_of(n_items))),
                 "block range must start (and end, unless at the catalog end) on a 8-KB tile");

@@ -77,7 +77,7 @@ SIGNATURES = {
     "nrk_fuse_wide": (INT, [P, I64, P, P, P, P, INT, P, INT, INT, F64, F64, P, P, P, P, INT, INT, P, P, P, P]),
     "nrk_ctx_features": (INT, [P, P, P, P, P]),
     "nrk_din_remap_index": (INT, [P, I64, INT, P, INT, P, P]),
-    "nrk_din_prep_bytes": (SZ, [INT]),
+    "nrk_din_prep_bytes": (SZ, [INT, I64]),
     "nrk_din_prepare": (INT, [P, INT, P, INT, I64, P, P]),
     "nrk_din_workspace_bytes": (SZ, [I64, INT, INT, INT, INT, INT, INT]),
     "nrk_din_forward": (INT, [P, INT, P, INT, INT, INT, P, P, P, P, P, I64, INT, P, P, P, P,

@@ -510,7 +510,7 @@ class DinParams:
         self.h1, self.h2 = self.mlp_w0.shape[0], self.mlp_w1.shape[0]
         if self.mlp_w1.shape[1] != self.h1 or self.mlp_w2.numel() != self.h2 or self.att_w1.numel() != 36:
             raise ValueError("state_dict shapes do not match the feature lists")
-        nb = _lib.lib().nrk_din_prep_bytes(self.kn_item)
+        nb = _lib.lib().nrk_din_prep_bytes(self.kn_item, self.table.shape[0])
         self.prep = torch.empty(nb, dtype=torch.uint8, device=device)
         _lib.call("nrk_din_prepare", _ptr(self.att_w0), self.kn_item, _ptr(self.table), self.table_code,
                   self.table.shape[0], _ptr(self.prep), _stream())
