@@ -619,7 +619,8 @@ __global__ void din_scales_kernel(const float* __restrict__ prep_ap, int ID, con
 //   are left unwritten: their mask is 0, and din_wh2 never reads a masked
 //   row's h.  At config 3 (hist_len ~ U[1, 50], 20% empty) that is ~21 of
 //   50 rows per sample.
-// * Position-major tiles: a workgroup (8 waves, 1 per CU at ~150 KB of LDS)
+// * Position-major tiles: a workgroup (4 waves, one per SIMD, each holding
+//   all weight fragments in registers; ~100 KB of LDS)
 //   takes a run of SW = 128 samples of ONE Dice batch, sorts them by n_b
 //   (descending, stable), so the samples with a real row at position t are
 //   the prefix [0, c_t) -- ceil(c_t / 16) tiles whose rows all share t.  A
@@ -628,10 +629,24 @@ __global__ void din_scales_kernel(const float* __restrict__ prep_ap, int ID, con
 //   tile's rows plus a 4-group butterfly, added once into the workgroup's
 //   row R[t] (which starts at P(t)).  Deterministic: every sum's order is
 //   fixed by the data, not by which wave ran it.
-// * Per tile the next tile's k rows and the one after's indices are in
-//   flight; all loads are unconditional (clamped rows), h goes out through
+// * Per tile the k rows of the next two tiles and the indices of the third
+//   are in flight (issued before the tile's MFMAs); all loads are unconditional (clamped rows), h goes out through
 //   buffer stores whose out-of-range offsets the hardware drops.
+// dev-only A/B switch (make devdin DEVFLAGS=-DNRK_TM_DEV=n; the product
+// build leaves it 0): 1 skips phase 7, 2 its stores, 3 its MFMAs, 4 phases 4-6
+#ifndef NRK_TM_DEV
+#define NRK_TM_DEV 0
+#endif
 constexpr int TM_SW = 128;  // samples per workgroup
+// waves per workgroup: 8 (two per SIMD, the weight fragments in LDS, read
+// one k-step ahead) or, dev builds only, 4 (one per SIMD, the fragments in
+// registers -- issue-bound: ~2.5k cycles per tile against ~1.5k)
+#ifndef NRK_TM_NW
+#define NRK_TM_NW 8
+#endif
+constexpr int TM_NW = NRK_TM_NW;
+constexpr bool TM_WLDS = TM_NW == 8;
+constexpr int TM_NT = TM_NW * 64;
 constexpr int TM_TMAX = 64; // positions (T)
 
 struct DinScalesTM {
@@ -734,60 +749,64 @@ typedef uint32_t tm_u4 __attribute__((ext_vector_type(4)));
 
 static inline size_t din_tm_lds(int NI, int T) {
     const int ID = NI * DIN_E;
-    return (size_t)3 * NI * 4 * 1024                 // W fragments
+    return (TM_WLDS ? (size_t)3 * NI * 4 * 1024 : 0)   // W fragments
            + (size_t)TM_SW * (ID * 2 + 16)             // q rows (fp16, padded stride)
            + (size_t)DIN_H * (TM_SW + 4) * 4           // c^T (acc init), padded stride
            + (size_t)TM_SW * DIN_H * 4                 // pad-row h
            + (size_t)T * DIN_H * 16                    // R: (sum, sumsq) per (t, j)
-           + (size_t)TM_SW * 4 * 2 + (TM_TMAX + 4) * 4;  // perm, n_b, c_t, counter
+           + (size_t)TM_SW * 12 + (TM_TMAX + 4) * 4;  // perm, perm * T, perm * T * 144, c_t, counter
 }
 
-template <int NI>
-__global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
-    const din_half8* __restrict__ tab16, const int64_t* __restrict__ row_base, int n_user,
-    const int32_t* __restrict__ item_idx, const int32_t* __restrict__ hist_idx, const float* __restrict__ mask,
-    int64_t N, int64_t S, int G, int T, const uint8_t* __restrict__ tm, const float* __restrict__ att_b0,
-    float* __restrict__ h_out, double* __restrict__ partial) {
-    constexpr int ID = NI * DIN_E;
-    constexpr int QS = ID * 2 + 16;  // q row stride (bytes): 16-B bank shift per row
-    constexpr int CTS = TM_SW + 4;   // c^T row stride (floats)
-    extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
-    din_half8* wl = reinterpret_cast<din_half8*>(tm_lds);
-    uint8_t* ql = tm_lds + 3 * NI * 4 * 1024;
-    float* ct = reinterpret_cast<float*>(ql + TM_SW * QS);
-    float* hp = ct + DIN_H * CTS;
-    double2* R = reinterpret_cast<double2*>(hp + TM_SW * DIN_H);
-    int* perm = reinterpret_cast<int*>(R + T * DIN_H);
-    int* nbs = perm + TM_SW;
-    int* cnt = nbs + TM_SW;        // c_t, t < T
-    int* next_t = cnt + TM_TMAX;   // position claim counter
+// Dice(x) with the batch (mean, 1 / (std + 1e-8)) of x's column (DIN.py:39-44)
+__device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
+    const float p = __builtin_amdgcn_rcpf(1.0f + __expf((mean - x) * inv));
+    return p * x + ((1.0f - p) * 0.01f) * x;
+}
 
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lg = lane >> 4;
+// Plan of a run of TM_SW samples (one Dice batch):
+// n_b of every sample (1 + its last row that is not the collate's padding),
+// a stable sort by n_b descending (perm: sorted position -> sample) and c_t
+// = #{n_b > t}.  plan[blk] = [perm (TM_SW) | c_t (TM_TMAX)]; one 256-thread
+// workgroup per run, every (mask, index) row read once, coalesced.
+constexpr int TM_PLAN = TM_SW + TM_TMAX;
+
+// dev-only phase stamps (make devdin DEVFLAGS=-DNRK_TM_STAMP=1, read by
+// nrk_dev_tm_stamps): per workgroup, shader cycles spent in each phase
+#ifndef NRK_TM_STAMP
+#define NRK_TM_STAMP 0
+#endif
+#if NRK_TM_STAMP
+__device__ unsigned long long tm_stamps[1024 * 12];
+#define TM_STAMP(k)                                           \
+    do {                                                      \
+        const uint64_t t_now_ = __builtin_readcyclecounter(); \
+        stp[k] += t_now_ - t_prev;                            \
+        t_prev = t_now_;                                      \
+    } while (0)
+#else
+#define TM_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
+template <int NI>
+__global__ __launch_bounds__(256) void din_tm_plan_kernel(const int32_t* __restrict__ hist_idx,
+                                                          const float* __restrict__ mask, int64_t N, int64_t S,
+                                                          int G, int T, int32_t* __restrict__ plan) {
+    __shared__ int nbs[TM_SW];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t seg = blockIdx.x / G, g = blockIdx.x % G;
     const int64_t b0 = seg * S + g * TM_SW;
     const int64_t seg_end = (seg + 1) * S < N ? (seg + 1) * S : N;
     const int nw = (int)(seg_end - b0 < TM_SW ? seg_end - b0 : TM_SW);
-    double2* dst = reinterpret_cast<double2*>(partial) + (size_t)blockIdx.x * T * DIN_H;
-    if (nw <= 0) {  // a short last batch leaves trailing workgroups empty: zero partial rows
-        for (int e = tid; e < T * DIN_H; e += 512) dst[e] = make_double2(0.0, 0.0);
-        return;
-    }
-    const DinScalesTM sc = *reinterpret_cast<const DinScalesTM*>(tm);
-    const din_half8* wpack = reinterpret_cast<const din_half8*>(tm + 256);
-    const din_half8* qdpack = wpack + 3 * NI * 4 * 64;
-
-    // ---- phase 0: W fragments -> LDS; n_b of every sample
-    {
-        const tm_u4* src = reinterpret_cast<const tm_u4*>(wpack);
-        tm_u4* d = reinterpret_cast<tm_u4*>(wl);
-        for (int c = tid; c < 3 * NI * 4 * 64; c += 512) d[c] = src[c];
-    }
-    {
+    int32_t* out = plan + (size_t)blockIdx.x * TM_PLAN;
+    if (nw <= 0) return;
+    const bool act = lane < T;
+    for (int u0 = 0; u0 < TM_SW / 4; u0 += 16) {
         bool nz[16];
-        const bool act = lane < T;
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            const int i = wv * 16 + u;
+            const int i = wv * (TM_SW / 4) + u0 + u;
             const int64_t b = b0 + (i < nw ? i : nw - 1);
             const size_t r = (size_t)b * T + (act ? lane : 0);
             const float m = mask[r];
@@ -806,13 +825,11 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             const uint64_t bal = __builtin_amdgcn_ballot_w64(nz[u]);
-            const int i = wv * 16 + u;
+            const int i = wv * (TM_SW / 4) + u0 + u;
             if (lane == 0) nbs[i] = i < nw ? (bal ? 64 - __builtin_clzll(bal) : 0) : -1;
         }
-        if (tid == 0) *next_t = 0;
     }
     __syncthreads();
-    // ---- phase 1: stable sort by n_b descending -> perm; c_t = #{n_b > t}
     if (tid < TM_SW) {
         const int my = nbs[tid];
         int rank = 0;
@@ -821,7 +838,7 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
             rank += (v.x > my || (v.x == my && j < tid)) + (v.y > my || (v.y == my && j + 1 < tid)) +
                     (v.z > my || (v.z == my && j + 2 < tid)) + (v.w > my || (v.w == my && j + 3 < tid));
         }
-        perm[rank] = tid;
+        out[rank] = tid;
     } else if (tid < TM_SW + T) {
         const int t = tid - TM_SW;
         int c = 0;
@@ -829,28 +846,118 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
             const int4 v = *reinterpret_cast<const int4*>(nbs + j);
             c += (v.x > t) + (v.y > t) + (v.z > t) + (v.w > t);
         }
-        cnt[t] = c;
+        out[TM_SW + t] = c;
     }
+}
+
+// Persistent: one workgroup per CU walks the runs blk = blockIdx.x,
+// blockIdx.x + gridDim.x, ...; the weight fragments are loaded once.
+template <int NI>
+__global__ __launch_bounds__(TM_NT, 1) __attribute__((amdgpu_waves_per_eu(TM_NW / 4, TM_NW / 4))) void din_att_tm_kernel(
+    const din_half8* __restrict__ tab16, const int64_t* __restrict__ row_base, int n_user,
+    const int32_t* __restrict__ item_idx, const int32_t* __restrict__ hist_idx, const int32_t* __restrict__ plan,
+    int64_t N, int64_t S, int G, int T, const uint8_t* __restrict__ tm, const float* __restrict__ att_b0,
+    float* __restrict__ h_out, double* __restrict__ partial) {
+    constexpr int ID = NI * DIN_E;
+    constexpr int QS = ID * 2 + 16;  // q row stride (bytes): 16-B bank shift per row
+    constexpr int CTS = TM_SW + 4;   // c^T row stride (floats)
+    extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
+    din_half8* wl = reinterpret_cast<din_half8*>(tm_lds);
+    uint8_t* ql = tm_lds + (TM_WLDS ? 3 * NI * 4 * 1024 : 0);
+    float* ct = reinterpret_cast<float*>(ql + TM_SW * QS);
+    float* hp = ct + DIN_H * CTS;
+    double2* R = reinterpret_cast<double2*>(hp + TM_SW * DIN_H);
+    int* perm = reinterpret_cast<int*>(R + T * DIN_H);
+    int* pT = perm + TM_SW;         // perm * T (row of position 0)
+    int* pH = pT + TM_SW;           // perm * T * 144 (byte offset of its h row 0)
+    int* cnt = pH + TM_SW;          // c_t, t < T
+    int* next_t = cnt + TM_TMAX;    // position claim counter
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, lr = lane & 15, lg = lane >> 4;
+    const DinScalesTM sc = *reinterpret_cast<const DinScalesTM*>(tm);
+    const din_half8* wpack = reinterpret_cast<const din_half8*>(tm + 256);
+    const din_half8* qdpack = wpack + 3 * NI * 4 * 64;
+    // W fragments (12 NI per lane: the B operand of every tile), once per
+    // workgroup: to LDS (TM_WLDS; published by the first run's barrier) or
+    // to registers
+    din_half8 wr[TM_WLDS ? 1 : 3][TM_WLDS ? 1 : NI][4];
+    if constexpr (TM_WLDS) {
+        const tm_u4* src = reinterpret_cast<const tm_u4*>(wpack);
+        tm_u4* d = reinterpret_cast<tm_u4*>(wl);
+        for (int c = tid; c < 3 * NI * 4 * 64; c += TM_NT) d[c] = src[c];
+    } else {
+#pragma unroll
+        for (int jt = 0; jt < 3; ++jt)
+#pragma unroll
+            for (int s = 0; s < NI; ++s)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) wr[jt][s][c] = wpack[((jt * NI + s) * 4 + c) * 64 + lane];
+    }
+    const int64_t n_blk = (N + S - 1) / S * G;
+#if NRK_TM_STAMP
+    uint64_t stp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t_prev = __builtin_readcyclecounter();
+#endif
+    for (int64_t blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+    const int64_t seg = blk / G, g = blk % G;
+    const int64_t b0 = seg * S + g * TM_SW;
+    const int64_t seg_end = (seg + 1) * S < N ? (seg + 1) * S : N;
+    const int nw = (int)(seg_end - b0 < TM_SW ? seg_end - b0 : TM_SW);
+    double2* dst = reinterpret_cast<double2*>(partial) + (size_t)blk * T * DIN_H;
+    if (nw <= 0) {  // a short last batch leaves trailing runs empty: zero partial rows
+        for (int e = tid; e < T * DIN_H; e += TM_NT) dst[e] = make_double2(0.0, 0.0);
+        continue;
+    }
+    // ---- phase 1 (din_tm_plan_kernel): perm and c_t -> LDS
+    for (int e = tid; e < TM_SW + T; e += TM_NT) {
+        const int v = plan[(size_t)blk * TM_PLAN + e];
+        if (e < TM_SW) {
+            perm[e] = v;
+            pT[e] = v * T;
+            pH[e] = v * T * (DIN_H * 4);
+        } else {
+            cnt[e - TM_SW] = v;
+        }
+    }
+    if (tid == 0) *next_t = 0;
     __syncthreads();
+    TM_STAMP(0);
     // ---- phase 2: q rows of the sorted samples (fp16 at scale s)
-    for (int task = tid; task < TM_SW * NI * 4; task += 512) {
-        const int p = task / (NI * 4), f = (task / 4) % NI, c = task % 4;
-        const int pc = p < nw ? p : 0;
-        const int64_t b = b0 + perm[pc];
-        const int32_t qi = item_idx[b * NI + f];
-        din_half8 v = tab16[(row_base[n_user + f] + qi) * 4 + c];
-        if (p >= nw) v = din_half8{};
-        *reinterpret_cast<din_half8*>(ql + p * QS + (f * DIN_E + 8 * c) * 2) = v;
+    // (each thread's QT tasks: all index loads in flight, then all row loads)
+    {
+        constexpr int QT = TM_SW * NI * 4 / TM_NT;
+        static_assert(QT * TM_NT == TM_SW * NI * 4, "q tasks");
+        int64_t rbq[NI];
+#pragma unroll
+        for (int f = 0; f < NI; ++f) rbq[f] = row_base[n_user + f];
+        int32_t qi[QT];
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+            const int task = tid + u * TM_NT, p = task / (NI * 4), f = (task / 4) % NI;
+            qi[u] = item_idx[(b0 + perm[p < nw ? p : 0]) * NI + f];
+        }
+        din_half8 v[QT];
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+            const int task = tid + u * TM_NT, f = (task / 4) % NI, c = task % 4;
+            v[u] = tab16[(rbq[f] + qi[u]) * 4 + c];
+        }
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+            const int task = tid + u * TM_NT, p = task / (NI * 4), f = (task / 4) % NI, c = task % 4;
+            *reinterpret_cast<din_half8*>(ql + p * QS + (f * DIN_E + 8 * c) * 2) = p < nw ? v[u] : din_half8{};
+        }
     }
     __syncthreads();
+    TM_STAMP(1);
     // ---- phase 3: c_b = (Wq + Wd) q + b0 for 16 samples per wave (MFMA),
     // stored pre-scaled (x s_w s) and transposed as the accumulator init
-    {
+    for (int pb = wv; pb < TM_SW / 16; pb += TM_NW) {
         const float b0j[3] = {att_b0[lr], att_b0[16 + lr], 32 + lr < DIN_H ? att_b0[32 + lr] : 0.0f};
         din_f4 acc[3];
 #pragma unroll
         for (int jt = 0; jt < 3; ++jt) acc[jt] = din_f4{0.0f, 0.0f, 0.0f, 0.0f};
-        const int p = wv * 16 + lr;
+        const int p = pb * 16 + lr;
 #pragma unroll
         for (int s = 0; s < NI; ++s) {
             const din_half8 a = *reinterpret_cast<const din_half8*>(ql + p * QS + (DIN_E * s + 8 * lg) * 2);
@@ -870,7 +977,7 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
                 din_f4 c;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) c[r] = (acc[jt][r] * sc.inv_qd + b0j[jt]) * to_acc;
-                *reinterpret_cast<din_f4*>(ct + j * CTS + wv * 16 + 4 * lg) = c;
+                *reinterpret_cast<din_f4*>(ct + j * CTS + pb * 16 + 4 * lg) = c;
             }
         }
     }
@@ -884,24 +991,53 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
             const int j = 16 * jt + lr < DIN_H ? 16 * jt + lr : DIN_H - 1;
             acc[jt] = *reinterpret_cast<const din_f4*>(ct + j * CTS + 16 * i + 4 * lg);
         }
+        if constexpr (TM_WLDS) {
+            // k-step s + 1's 12 fragments are read while k-step s's 15 MFMAs
+            // run (two register sets; the barrier keeps the reads ahead)
+            din_half8 wb[2][3][4];
+            auto wread = [&](int s, din_half8 (&w)[3][4]) {
 #pragma unroll
-        for (int s = 0; s < NI; ++s) {
-            const din_half8 qf = *reinterpret_cast<const din_half8*>(ql + pa * QS + (DIN_E * s + 8 * lg) * 2);
-            const din_half8 ph = kf[s] * qf;
-            const din_half8 pl = __builtin_elementwise_fma(kf[s], qf, -ph);
+                for (int jt = 0; jt < 3; ++jt)
 #pragma unroll
-            for (int jt = 0; jt < 3; ++jt) {
-                const din_half8* w = wl + ((jt * NI + s) * 4) * 64 + lane;
-                const din_half8 w1h = w[0], w1l = w[64], wph = w[128], wpl = w[192];
-                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], w1h, acc[jt], 0, 0, 0);
-                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], w1l, acc[jt], 0, 0, 0);
-                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, wph, acc[jt], 0, 0, 0);
-                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, wpl, acc[jt], 0, 0, 0);
-                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl, wph, acc[jt], 0, 0, 0);
+                    for (int c = 0; c < 4; ++c) w[jt][c] = wl[((jt * NI + s) * 4 + c) * 64 + lane];
+            };
+            wread(0, wb[0]);
+#pragma unroll
+            for (int s = 0; s < NI; ++s) {
+                if (s + 1 < NI) wread(s + 1, wb[(s + 1) & 1]);
+                const din_half8 qf = *reinterpret_cast<const din_half8*>(ql + pa * QS + (DIN_E * s + 8 * lg) * 2);
+                __builtin_amdgcn_sched_barrier(0);
+                const din_half8 ph = kf[s] * qf;
+                const din_half8 pl = __builtin_elementwise_fma(kf[s], qf, -ph);
+                const din_half8(&w)[3][4] = wb[s & 1];
+#pragma unroll
+                for (int jt = 0; jt < 3; ++jt) {
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], w[jt][0], acc[jt], 0, 0, 0);
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], w[jt][1], acc[jt], 0, 0, 0);
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, w[jt][2], acc[jt], 0, 0, 0);
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, w[jt][3], acc[jt], 0, 0, 0);
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl, w[jt][2], acc[jt], 0, 0, 0);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < NI; ++s) {
+                const din_half8 qf = *reinterpret_cast<const din_half8*>(ql + pa * QS + (DIN_E * s + 8 * lg) * 2);
+                const din_half8 ph = kf[s] * qf;
+                const din_half8 pl = __builtin_elementwise_fma(kf[s], qf, -ph);
+#pragma unroll
+                for (int jt = 0; jt < 3; ++jt) {
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], wr[jt][s][0], acc[jt], 0, 0, 0);
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], wr[jt][s][1], acc[jt], 0, 0, 0);
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, wr[jt][s][2], acc[jt], 0, 0, 0);
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, wr[jt][s][3], acc[jt], 0, 0, 0);
+                    acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl, wr[jt][s][2], acc[jt], 0, 0, 0);
+                }
             }
         }
     };
 
+    TM_STAMP(2);
     // ---- phase 4: pad rows (k = row 0 of every item table) of the samples
     // with n_b < T: sorted positions [c_{T-1}, nw)
     {
@@ -909,7 +1045,7 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
 #pragma unroll
         for (int s = 0; s < NI; ++s) k0[s] = tab16[row_base[n_user + s] * 4 + lg];
         const int pad_lo = cnt[T - 1];
-        for (int i = pad_lo / 16 + wv; i * 16 < nw; i += 8) {
+        for (int i = pad_lo / 16 + wv; NRK_TM_DEV != 4 && i * 16 < nw; i += TM_NW) {
             const int pa = 16 * i + lr < nw ? 16 * i + lr : nw - 1;
             din_f4 acc[3];
             tile_mfma(i, k0, pa, acc);
@@ -925,11 +1061,12 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
         }
     }
     __syncthreads();
+    TM_STAMP(3);
     // ---- phase 5: D(t) = sum of the pad rows of the samples with n_b = t
     // (sorted positions [c_t, c_{t-1}), c_{-1} = nw), into R
-    for (int e = tid; e < T * DIN_H; e += 512) {
+    for (int e = tid; e < T * DIN_H; e += TM_NT) {
         const int t = e / DIN_H, j = e % DIN_H;
-        const int lo = cnt[t], hi = t == 0 ? nw : cnt[t - 1];
+        const int lo = cnt[t], hi = NRK_TM_DEV == 4 ? lo : t == 0 ? nw : cnt[t - 1];
         double s = 0.0, ss = 0.0;
         for (int p = lo; p < hi; ++p) {
             const double v = (double)hp[p * DIN_H + j];
@@ -939,6 +1076,7 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
         R[e] = make_double2(s, ss);
     }
     __syncthreads();
+    TM_STAMP(4);
     // ---- phase 6: P(t) = prefix over t of D, in place (one lane per column,
     // eight positions' loads in flight per step)
     if (tid < DIN_H) {
@@ -957,10 +1095,10 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
     }
     __syncthreads();
 
+    TM_STAMP(5);
     // ---- phase 7: real rows, positions claimed dynamically (largest first)
     int t_eff = 0;  // positions with at least one real row (c_t nonincreasing)
     while (t_eff < T && cnt[t_eff] > 0) ++t_eff;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(h_out + b0 * T * DIN_H, 0, nw * T * DIN_H * 4, 0x00020000);
     int64_t rbs[NI];
 #pragma unroll
     for (int s = 0; s < NI; ++s) rbs[s] = row_base[n_user + s] * 4 + lg;  // in 16-B pieces
@@ -985,12 +1123,15 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
         const int p = 16 * j.i + lr;
         return j.t >= t_eff ? 0 : (p < j.c ? p : j.c - 1);
     };
+    // 32-bit offsets from the run's first row (u24 products: sample * T + t
+    // < TM_SW * TM_TMAX), so no 64-bit multiply per tile
+    const int32_t* hrun = hist_idx + (size_t)b0 * T * NI;
     auto idx_load = [&](const Job& j) -> int4 {
         const int tc = j.t < t_eff ? j.t : 0;
-        const size_t r = ((size_t)(b0 + perm[apos(j)]) * T + tc) * NI;
-        if constexpr (NI == 4) return *reinterpret_cast<const int4*>(hist_idx + r);
-        else if constexpr (NI == 2) { const int2 x = *reinterpret_cast<const int2*>(hist_idx + r); return make_int4(x.x, x.y, 0, 0); }
-        else return make_int4(hist_idx[r], 0, 0, 0);
+        const int r = (pT[apos(j)] + tc) * NI;
+        if constexpr (NI == 4) return *reinterpret_cast<const int4*>(hrun + r);
+        else if constexpr (NI == 2) { const int2 x = *reinterpret_cast<const int2*>(hrun + r); return make_int4(x.x, x.y, 0, 0); }
+        else return make_int4(hrun[r], 0, 0, 0);
     };
     auto rows_load = [&](const int4& ix, din_half8 (&kf)[NI]) {
         const int32_t iv[4] = {ix.x, ix.y, ix.z, ix.w};
@@ -998,48 +1139,97 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
         for (int s = 0; s < NI; ++s) kf[s] = tab16[rbs[s] + (int64_t)iv[s] * 4];
     };
 
+    // three slots (k rows + indices) rotate so no register copy waits on a
+    // load: in the step of job m, slot m % 3 holds job m's rows and receives
+    // job m+3's indices, slot (m+2) % 3 receives job m+2's rows (from the
+    // indices it got one step earlier)
     Job j0 = claim_job();
     Job j1 = succ(j0);
-    din_half8 k_0[NI], k_1[NI];
-    int4 ix1;
-    {
-        const int4 ix0 = idx_load(j0);
-        rows_load(ix0, k_0);
-        ix1 = idx_load(j1);
-    }
+    Job j2 = succ(j1);
+    din_half8 k_a[NI], k_b[NI], k_c[NI];
+    int4 ix_a, ix_b, ix_c;
+    ix_a = idx_load(j0);
+    ix_b = idx_load(j1);
+    rows_load(ix_a, k_a);
+    ix_c = idx_load(j2);
+    rows_load(ix_b, k_b);
+    // h goes out through buffer stores whose out-of-range offsets the
+    // hardware drops (unconditional: 12 per step); a step is entered with its
+    // far indices followed by 4 row loads and 12 stores, and 12 dropped stores
+    // give the loop entry the same shape, so the wait counts merged at the
+    // loop head stay those of a steady-state step
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(h_out + b0 * T * DIN_H, 0, nw * T * DIN_H * 4, 0x00020000);
+#pragma unroll
+    for (int e = 0; e < 12; ++e) __builtin_amdgcn_raw_buffer_store_b32(0u, rsrc, 0x7FFFF000, 0, 0);
     double ssum[3], ssq[3];
 #pragma unroll
     for (int jt = 0; jt < 3; ++jt) ssum[jt] = ssq[jt] = 0.0;
-    while (j0.t < t_eff) {
-        const Job j2 = succ(j1);
-        const int4 ix2 = idx_load(j2);  // indices two jobs ahead
-        rows_load(ix1, k_1);            // rows one job ahead
+    auto step = [&](din_half8 (&kcur)[NI], int4& ixcur, din_half8 (&kfar)[NI], const int4& ixfar) {
+#if NRK_TM_STAMP
+        uint64_t t_s = __builtin_readcyclecounter();
+#define TM_SSTAMP(k)                                          \
+    do {                                                      \
+        const uint64_t t_now_ = __builtin_readcyclecounter(); \
+        stp[k] += t_now_ - t_s;                               \
+        t_s = t_now_;                                         \
+    } while (0)
+#else
+#define TM_SSTAMP(k) \
+    do {             \
+    } while (0)
+#endif
+        const Job j3 = succ(j2);
+        TM_SSTAMP(8);
+        ixcur = idx_load(j3);   // indices three jobs ahead
+        rows_load(ixfar, kfar); // rows two jobs ahead
+        TM_SSTAMP(9);
+        // keep the loads ahead of this tile's MFMAs (the scheduler would sink
+        // them past the chain, leaving a load latency exposed per tile)
+        __builtin_amdgcn_sched_barrier(0);
         din_f4 acc[3];
-        tile_mfma(j0.i, k_0, apos(j0), acc);
-        // epilogue: store h (rows < c_t, j < 36), column sums over valid rows
-        const int4 smp = *reinterpret_cast<const int4*>(perm + 16 * j0.i + 4 * lg);
-        const int sv[4] = {smp.x, smp.y, smp.z, smp.w};
-        int roff[4];
-        bool rok[4];
+        if constexpr (NRK_TM_DEV == 3) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            rok[r] = 16 * j0.i + 4 * lg + r < j0.c;
-            roff[r] = rok[r] ? (sv[r] * T + j0.t) * (DIN_H * 4) : 0x7FFFF000;  // past num_records: dropped
+            for (int jt = 0; jt < 3; ++jt)
+                acc[jt] = din_f4{kcur[0][0] + kcur[NI - 1][1], 0.0f, 0.0f, 0.0f} * (float)ixfar.x;
+        } else {
+            tile_mfma(j0.i, kcur, apos(j0), acc);
         }
-#pragma unroll
-        for (int jt = 0; jt < 3; ++jt) {
-            const int j = 16 * jt + lr;
-            const bool jok = jt < 2 || lr < DIN_H - 32;
+#if NRK_TM_STAMP
+        asm volatile("s_nop 0" ::"v"(acc[0][0]), "v"(acc[1][0]), "v"(acc[2][0]));
+#endif
+        TM_SSTAMP(10);
+        // epilogue: h of rows < c_t (j < 36) to HBM; column sums of h and
+        // h^2 over those rows -- the lane's 4 rows in fp32 (relative error
+        // ~2^-22, below the reference's own fp32 statistics), then fp64
+        const int4 smp = *reinterpret_cast<const int4*>(pH + 16 * j0.i + 4 * lg);
+        const int toff = j0.t * (DIN_H * 4) + 4 * lr;
+        const int sv[4] = {smp.x, smp.y, smp.z, smp.w};
+        auto epi = [&](auto full_c) {
+            constexpr bool FULL = decltype(full_c)::value;
+            int roff[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float v = acc[jt][r] * sc.inv;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, jok ? roff[r] + 4 * j : 0x7FFFF000,
-                                                      0, 0);
-                const double dv = (double)(rok[r] ? v : 0.0f);
-                ssum[jt] += dv;
-                ssq[jt] = fma(dv, dv, ssq[jt]);
+                const bool ok = FULL || 16 * j0.i + 4 * lg + r < j0.c;
+                roff[r] = ok ? sv[r] + toff : 0x7FFFF000;  // past num_records: dropped
             }
-        }
+#pragma unroll
+            for (int jt = 0; jt < 3; ++jt) {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[jt][r] * sc.inv;
+                    const int off = jt < 2 || lr < DIN_H - 32 ? roff[r] + 64 * jt : 0x7FFFF000;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rsrc, off, 0, 0);
+                    if constexpr (!FULL) v[r] = 16 * j0.i + 4 * lg + r < j0.c ? v[r] : 0.0f;
+                }
+                const float s4 = (v[0] + v[1]) + (v[2] + v[3]);
+                const float q4 = fmaf(v[3], v[3], fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0])));
+                ssum[jt] += (double)s4;
+                ssq[jt] += (double)q4;
+            }
+        };
+        if (16 * (j0.i + 1) <= j0.c) epi(std::true_type{});  // uniform: a full tile
+        else epi(std::false_type{});
         if (j1.t != j0.t) {  // last tile of j0.t: combine the 16 rows' lanes, add to R[t]
 #pragma unroll
             for (int jt = 0; jt < 3; ++jt) {
@@ -1056,15 +1246,29 @@ __global__ __launch_bounds__(512, 1) void din_att_tm_kernel(
                 ssum[jt] = ssq[jt] = 0.0;
             }
         }
-#pragma unroll
-        for (int s = 0; s < NI; ++s) k_0[s] = k_1[s];
-        ix1 = ix2;
+        TM_SSTAMP(11);
         j0 = j1;
         j1 = j2;
+        j2 = j3;
+    };
+    while (NRK_TM_DEV != 1 && j0.t < t_eff) {
+        step(k_a, ix_a, k_c, ix_c);
+        if (j0.t >= t_eff) break;
+        step(k_b, ix_b, k_a, ix_a);
+        if (j0.t >= t_eff) break;
+        step(k_c, ix_c, k_b, ix_b);
     }
+    TM_STAMP(6);
     __syncthreads();
-    // ---- phase 8: the workgroup's partial row
-    for (int e = tid; e < T * DIN_H; e += 512) dst[e] = R[e];
+    // ---- phase 8: the run's partial row
+    for (int e = tid; e < T * DIN_H; e += TM_NT) dst[e] = R[e];
+    __syncthreads();  // R, perm and c_t are rewritten by the next run
+    TM_STAMP(7);
+    }
+#if NRK_TM_STAMP
+    if (tid == 0 && blockIdx.x < 1024)
+        for (int k = 0; k < 12; ++k) tm_stamps[blockIdx.x * 12 + k] = stp[k];
+#endif
 }
 
 // ---------------------------------------------------------- 2. col stats --
@@ -1181,10 +1385,6 @@ __global__ __launch_bounds__(256) void din_att_out_kernel(
 // during the gathers.  Each wave owns a contiguous run of samples and
 // publishes max |wh| per Dice batch (atomicMax on the float bits) for
 // GEMM1's fp16 scale.
-__device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
-    const float p = __builtin_amdgcn_rcpf(1.0f + __expf((mean - x) * inv));
-    return p * x + ((1.0f - p) * 0.01f) * x;
-}
 
 // din_wh2: the Dice statistics live in LDS, not registers.  Workgroup
 // (seg, g) takes a contiguous run of ONE Dice batch (segment), so its four
@@ -1925,6 +2125,7 @@ static inline int din_att_groups(int64_t N, int64_t S) {
 struct DinWs {
     float* h;
     double* hpart;
+    int32_t* plan;   // position-major path: per run of TM_SW samples, din_tm_plan_kernel
     float2* hstats;
     float* mlp_in;   // general path only
     float* wh;       // fast path only: [N, ID]
@@ -1969,6 +2170,7 @@ static DinWs din_ws_layout(void* base, int64_t N, int64_t S, int T, int n_user, 
     auto take = [&](size_t bytes) { uint8_t* r = p + o; o += al(bytes); return r; };
     w.h = (float*)take((size_t)N * T * DIN_H * 4);
     w.hpart = (double*)take((size_t)nb_att * T * DIN_H * 16);
+    w.plan = (int32_t*)take((size_t)n_seg * ((S + TM_SW - 1) / TM_SW) * TM_PLAN * 4);
     w.hstats = (float2*)take((size_t)n_seg * T * DIN_H * 8);
     w.mlp_in = fast ? nullptr : (float*)take((size_t)N * IN * 4);
     w.wh = fast ? (float*)take((size_t)N * n_item * DIN_E * 4) : nullptr;
@@ -1994,6 +2196,13 @@ static DinWs din_ws_layout(void* base, int64_t N, int64_t S, int T, int n_user, 
 using namespace nrk;
 
 extern "C" {
+
+#if NRK_TM_STAMP
+// dev-only: the phase stamps of the last din_att_tm launch (1024 x 8 u64)
+int nrk_dev_tm_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tm_stamps), sizeof(tm_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int nrk_din_remap_index(const int32_t* in, int64_t n_rows, int f_in, const int32_t* map, int f_out,
                         int32_t* out, nrk_stream_t stream) {
@@ -2102,18 +2311,27 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     const int64_t nb_att = n_seg * G;
     NRK_REQUIRE(nb_att < (1ll << 31), "too many segments");
     const float* pf = reinterpret_cast<const float*>(prep);
-    const bool tm_path = table_dtype == 1 && T <= TM_TMAX && n_item <= 4;
+    // position-major attention (bf16 tables, T <= 64, <= 4 item features,
+    // the fast MLP path): plan, then h + its statistics
+    const bool tm_path = table_dtype == 1 && T <= TM_TMAX && n_item <= 4 && din_fast(T, h1);
     const int G_tm = (int)((S + TM_SW - 1) / TM_SW);
+    // persistent: one workgroup per CU (register- and LDS-bound)
+    static const int n_cu = [] {
+        int dev = 0, cu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+        return cu > 0 ? cu : 256;
+    }();
+    const unsigned tm_grid = (unsigned)std::min<int64_t>(n_seg * G_tm, n_cu);
     const uint8_t* tm = reinterpret_cast<const uint8_t*>(prep) + din_tm_base(n_item);
 #define NRK_ATT_TM(NI)                                                                                 \
     do {                                                                                               \
         const size_t lds = din_tm_lds(NI, T);                                                          \
         (void)hipFuncSetAttribute((const void*)din_att_tm_kernel<NI>,                                  \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
-        din_att_tm_kernel<NI><<<(unsigned)(n_seg * G_tm), 512, lds, s>>>(                              \
+        din_att_tm_kernel<NI><<<tm_grid, TM_NT, lds, s>>>(                                             \
             reinterpret_cast<const din_half8*>(reinterpret_cast<const uint8_t*>(prep) +                \
                                                din_tm_tab16_off(n_item)),                               \
-            row_base, n_user, item_idx, hist_idx, mask, batch, S, G_tm, T, tm, att_b0, w.h, w.hpart);   \
+            row_base, n_user, item_idx, hist_idx, w.plan, batch, S, G_tm, T, tm, att_b0, w.h, w.hpart); \
     } while (0)
 #define NRK_ATT_H(TT, NI)                                                                              \
     do {                                                                                               \
@@ -2131,6 +2349,9 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
                 T, pf, att_b0, w.h, w.hpart);                                                       \
     } while (0)
     if (tm_path) {
+#define NRK_TM_PLAN(NI) din_tm_plan_kernel<NI><<<(unsigned)(n_seg * G_tm), 256, 0, s>>>(hist_idx, mask, batch, S, G_tm, T, w.plan)
+        if (n_item == 4) NRK_TM_PLAN(4); else if (n_item == 2) NRK_TM_PLAN(2); else NRK_TM_PLAN(1);
+#undef NRK_TM_PLAN
         if (n_item == 4) NRK_ATT_TM(4); else if (n_item == 2) NRK_ATT_TM(2); else NRK_ATT_TM(1);
     } else if (table_dtype == 0) {
         if (n_item == 8) NRK_ATT_H(float, 8); else if (n_item == 4) NRK_ATT_H(float, 4);
@@ -2140,12 +2361,12 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         else if (n_item == 2) NRK_ATT_H(uint16_t, 2); else NRK_ATT_H(uint16_t, 1);
     }
 #undef NRK_ATT_H
-#undef NRK_ATT_TM
     const int ncol_att = T * DIN_H;
     const unsigned gs = (unsigned)n_seg;
     const int bps_att = tm_path ? G_tm : G;
     col_stats_kernel<<<dim3(gs, (ncol_att + 3) / 4), 256, 0, s>>>(w.hpart, bps_att, (int)(n_seg * bps_att),
                                                                    ncol_att, batch, S, w.hstats, w.hinv);
+#undef NRK_ATT_TM
     const int64_t gb = (batch + 3) / 4;
     const int64_t nb_m = (batch + 63) / 64;
     const int bps = n_seg == 1 ? (int)nb_m : (int)(S / 64);  // 64-row GEMM blocks per segment

@@ -1,13 +1,9 @@
 #!/bin/bash
-# A/B the scan variants (NRK_SCAN_VARIANT) on config 2 (dev tool, GPU box)
-set -o pipefail
-cd "$GRAFT_REPO_ROOT" || exit 1
-export TMPDIR=/tmp
-O=gpurun_out/${1:-ab}; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_recall.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -1 $O/pytest.log
-for v in ${VARIANTS:-0 1 2 3}; do
-  NRK_SCAN_VARIANT=$v timeout -k 10 120 python3 tools/screen_time.py 2>&1 | tail -1 || exit 1
+# dev: config-2 screen (tools/scan_diag.py) under each build: prod or build_<name>
+cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
+o=gpurun_out/$1; shift; mkdir -p $o
+for v in "$@"; do
+  lib=news-recommendation-tc_amd/nrk/libnrk.so; [ "$v" != prod ] && lib=news-recommendation-tc_amd/build_$v/libnrk.so
+  NRK_LIB_PATH=$lib timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $o/s_$v -o run -- python3 tools/scan_diag.py > $o/scan_$v.txt 2>&1 || exit 1
+  echo "== screen $v"; tail -3 $o/scan_$v.txt; python3 tools/kstats.py $o/s_$v/run_kernel_stats.csv 5
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/screen_time.py > $O/tool.log 2>&1 || { tail -30 $O/tool.log; exit 1; }
-python3 tools/kstats.py $O/prof/run_kernel_stats.csv 6
