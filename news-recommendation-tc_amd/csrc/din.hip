@@ -757,6 +757,28 @@ static inline size_t din_tm_lds(int NI, int T) {
            + (size_t)TM_SW * 12 + (TM_TMAX + 4) * 4;  // perm, perm * T, perm * T * 144, c_t, counter
 }
 
+// the value of lane l ^ 16 / l ^ 32 (v_permlane16_swap / v_permlane32_swap
+// with vdst = src = v: r[0] holds the lower row's value in the upper row,
+// r[1] the upper row's in the lower one) -- VALU, no LDS round trip
+__device__ __forceinline__ uint32_t xor16u(uint32_t v, int lane) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return ((lane >> 4) & 1) ? (uint32_t)r[0] : (uint32_t)r[1];
+}
+__device__ __forceinline__ uint32_t xor32u(uint32_t v, int lane) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane >> 5) ? (uint32_t)r[0] : (uint32_t)r[1];
+}
+__device__ __forceinline__ double xor16d(double v, int lane) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double((long long)((uint64_t)xor16u((uint32_t)b, lane) |
+                                            ((uint64_t)xor16u((uint32_t)(b >> 32), lane) << 32)));
+}
+__device__ __forceinline__ double xor32d(double v, int lane) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double((long long)((uint64_t)xor32u((uint32_t)b, lane) |
+                                            ((uint64_t)xor32u((uint32_t)(b >> 32), lane) << 32)));
+}
+
 // Dice(x) with the batch (mean, 1 / (std + 1e-8)) of x's column (DIN.py:39-44)
 __device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
     const float p = __builtin_amdgcn_rcpf(1.0f + __expf((mean - x) * inv));
@@ -767,7 +789,9 @@ __device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
 // n_b of every sample (1 + its last row that is not the collate's padding),
 // a stable sort by n_b descending (perm: sorted position -> sample) and c_t
 // = #{n_b > t}.  plan[blk] = [perm (TM_SW) | c_t (TM_TMAX)]; one 256-thread
-// workgroup per run, every (mask, index) row read once, coalesced.
+// workgroup per run, every (mask, index) row read once, coalesced.  (A
+// static longest-first schedule of positions to waves was tried: the waves
+// then wait ~10% of the kernel at the end of each run.)
 constexpr int TM_PLAN = TM_SW + TM_TMAX;
 
 // dev-only phase stamps (make devdin DEVFLAGS=-DNRK_TM_STAMP=1, read by
@@ -1096,7 +1120,9 @@ __global__ __launch_bounds__(TM_NT, 1) __attribute__((amdgpu_waves_per_eu(TM_NW 
     __syncthreads();
 
     TM_STAMP(5);
-    // ---- phase 7: real rows, positions claimed dynamically (largest first)
+    // ---- phase 7: real rows, positions claimed dynamically (largest first:
+    // c_t is nonincreasing in t); a wave's next claim is issued one claim
+    // ahead, so its LDS atomic never sits on the path to the next tile
     int t_eff = 0;  // positions with at least one real row (c_t nonincreasing)
     while (t_eff < T && cnt[t_eff] > 0) ++t_eff;
     int64_t rbs[NI];
@@ -1106,11 +1132,11 @@ __global__ __launch_bounds__(TM_NT, 1) __attribute__((amdgpu_waves_per_eu(TM_NW 
     struct Job {
         int t, i, c;
     };
+    int pend = lane == 0 ? atomicAdd(next_t, 1) : 0;  // lane 0: the claimed position
     auto claim_job = [&]() -> Job {
-        int t = 0;
-        if (lane == 0) t = atomicAdd(next_t, 1);
-        t = __builtin_amdgcn_readfirstlane(t);
+        const int t = __builtin_amdgcn_readfirstlane(pend);
         if (t >= t_eff) return Job{t_eff, 0, 0};
+        pend = lane == 0 ? atomicAdd(next_t, 1) : 0;
         return Job{t, 0, cnt[t]};
     };
     auto succ = [&](const Job& j) -> Job {
@@ -1154,13 +1180,13 @@ __global__ __launch_bounds__(TM_NT, 1) __attribute__((amdgpu_waves_per_eu(TM_NW 
     ix_c = idx_load(j2);
     rows_load(ix_b, k_b);
     // h goes out through buffer stores whose out-of-range offsets the
-    // hardware drops (unconditional: 12 per step); a step is entered with its
-    // far indices followed by 4 row loads and 12 stores, and 12 dropped stores
+    // hardware drops (unconditional: 3 per step); a step is entered with its
+    // far indices followed by 4 row loads and 3 stores, and 3 dropped stores
     // give the loop entry the same shape, so the wait counts merged at the
     // loop head stay those of a steady-state step
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(h_out + b0 * T * DIN_H, 0, nw * T * DIN_H * 4, 0x00020000);
 #pragma unroll
-    for (int e = 0; e < 12; ++e) __builtin_amdgcn_raw_buffer_store_b32(0u, rsrc, 0x7FFFF000, 0, 0);
+    for (int e = 0; e < 3; ++e) __builtin_amdgcn_raw_buffer_store_b128(tm_u4{0u, 0u, 0u, 0u}, rsrc, 0x7FFFF000, 0, 0);
     double ssum[3], ssq[3];
 #pragma unroll
     for (int jt = 0; jt < 3; ++jt) ssum[jt] = ssq[jt] = 0.0;
@@ -1198,28 +1224,21 @@ __global__ __launch_bounds__(TM_NT, 1) __attribute__((amdgpu_waves_per_eu(TM_NW 
         asm volatile("s_nop 0" ::"v"(acc[0][0]), "v"(acc[1][0]), "v"(acc[2][0]));
 #endif
         TM_SSTAMP(10);
-        // epilogue: h of rows < c_t (j < 36) to HBM; column sums of h and
-        // h^2 over those rows -- the lane's 4 rows in fp32 (relative error
-        // ~2^-22, below the reference's own fp32 statistics), then fp64
-        const int4 smp = *reinterpret_cast<const int4*>(pH + 16 * j0.i + 4 * lg);
-        const int toff = j0.t * (DIN_H * 4) + 4 * lr;
-        const int sv[4] = {smp.x, smp.y, smp.z, smp.w};
+        // epilogue: column sums of h and h^2 over the rows < c_t -- the
+        // lane's 4 rows in fp32 (relative error ~2^-22, below the reference's
+        // own fp32 statistics), then fp64; h of those rows to HBM, transposed
+        // through the wave's LDS stage so each lane stores 16 contiguous bytes
+        // of a row (3 wide stores per tile instead of 12 scattered ones)
+        float* stg = hp + wv * (16 * DIN_H);
         auto epi = [&](auto full_c) {
             constexpr bool FULL = decltype(full_c)::value;
-            int roff[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const bool ok = FULL || 16 * j0.i + 4 * lg + r < j0.c;
-                roff[r] = ok ? sv[r] + toff : 0x7FFFF000;  // past num_records: dropped
-            }
 #pragma unroll
             for (int jt = 0; jt < 3; ++jt) {
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     v[r] = acc[jt][r] * sc.inv;
-                    const int off = jt < 2 || lr < DIN_H - 32 ? roff[r] + 64 * jt : 0x7FFFF000;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rsrc, off, 0, 0);
+                    if (jt < 2 || lr < DIN_H - 32) stg[(4 * lg + r) * DIN_H + 16 * jt + lr] = v[r];
                     if constexpr (!FULL) v[r] = 16 * j0.i + 4 * lg + r < j0.c ? v[r] : 0.0f;
                 }
                 const float s4 = (v[0] + v[1]) + (v[2] + v[3]);
@@ -1230,13 +1249,40 @@ __global__ __launch_bounds__(TM_NT, 1) __attribute__((amdgpu_waves_per_eu(TM_NW 
         };
         if (16 * (j0.i + 1) <= j0.c) epi(std::true_type{});  // uniform: a full tile
         else epi(std::false_type{});
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        {
+            // all six LDS reads in flight before the stores (unconditional,
+            // clamped rows)
+            const int toff = j0.t * (DIN_H * 4);
+            tm_u4 x[3];
+            int ph[3], c4[3];
+            bool ok[3];
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                const int e = lane + 64 * m;  // 16-B piece e = 9 row + c4 of the 16 x 36 tile
+                const int row = e / 9;
+                c4[m] = e - 9 * row;
+                ok[m] = e < 16 * 9 && 16 * j0.i + row < j0.c;
+                const int rc = ok[m] ? row : 0;
+                x[m] = *reinterpret_cast<const tm_u4*>(stg + rc * DIN_H + 4 * (ok[m] ? c4[m] : 0));
+                ph[m] = pH[16 * j0.i + rc];
+            }
+#pragma unroll
+            for (int m = 0; m < 3; ++m)  // past num_records: dropped
+                __builtin_amdgcn_raw_buffer_store_b128(x[m], rsrc, ok[m] ? ph[m] + toff + 16 * c4[m] : 0x7FFFF000, 0, 0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (j1.t != j0.t) {  // last tile of j0.t: combine the 16 rows' lanes, add to R[t]
 #pragma unroll
             for (int jt = 0; jt < 3; ++jt) {
-                ssum[jt] += __shfl_xor(ssum[jt], 16, WAVE);
-                ssq[jt] += __shfl_xor(ssq[jt], 16, WAVE);
-                ssum[jt] += __shfl_xor(ssum[jt], 32, WAVE);
-                ssq[jt] += __shfl_xor(ssq[jt], 32, WAVE);
+                ssum[jt] += xor16d(ssum[jt], lane);
+                ssq[jt] += xor16d(ssq[jt], lane);
+                ssum[jt] += xor32d(ssum[jt], lane);
+                ssq[jt] += xor32d(ssq[jt], lane);
                 const int j = 16 * jt + lr;
                 if (lane < 16 && j < DIN_H) {
                     double2* rp = R + j0.t * DIN_H + j;
@@ -1482,10 +1528,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         }
     };
     for (int64_t b = b0; b < b1e; ++b) {
+        // Dice only up to the last live row (rows past it are padding: their
+        // weight is 0 whatever Dice gives; ~60% of the rows at config 3)
+        const uint64_t lv = __builtin_amdgcn_ballot_w64(act && mk != 0.0f);
+        const int tl = lv ? 64 - __builtin_clzll(lv) : 0;
+        const int nql = tl * HQ;
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
             const int q = 64 * i + lane;
-            if (q < nq) {
+            if (64 * i >= nql) break;  // uniform
+            if (q < nql) {
                 const f4n m4 = smean[q], i4 = sinv[q];
                 f4n d;
 #pragma unroll
@@ -1497,7 +1549,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         float w = 0.0f;
-        if (act) {
+        if (lane < tl && mk != 0.0f) {
             const f4n* dr = reinterpret_cast<const f4n*>(&dsc[lane * DIN_H]);
             float sacc = 0.0f;
 #pragma unroll
