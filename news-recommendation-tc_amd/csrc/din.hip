@@ -22,12 +22,10 @@
 //   8. din_head       Dice -> Linear(h2->1) -> sigmoid (:282-284).
 // The general path (T > 64 or h1 > 256) assembles the MLP input with
 // din_att_out and runs the f32 MFMA din_gemm instead of 3, 4 and 6.
-#include "nrk_common.h"
+#include "din_common.h"
 
 namespace nrk {
 
-constexpr int DIN_E = 32;   // embedding dim (din_embedding_dim, config.py:115)
-constexpr int DIN_H = 36;   // ActivationUnit hidden (default [36], DIN.py:188)
 
 template <typename TT>
 __device__ __forceinline__ float tload(const TT* p);
@@ -65,14 +63,9 @@ __device__ __forceinline__ float dice(float x, float mean, float std) {
 // straight from the table into A fragments.  Column statistics of h
 // (fp64 sum / sumsq per (t, j)) stay in registers across the workgroup's
 // samples (grid-strided), one partial row per workgroup.
-typedef _Float16 din_half8 __attribute__((ext_vector_type(8)));
-typedef float din_f4 __attribute__((ext_vector_type(4)));
 
 constexpr int DIN_JT = 3;  // 36 columns -> 3 tiles of 16
 
-struct DinScales {
-    float s_k, s_m, inv, pad;
-};
 
 template <typename TT>
 __device__ __forceinline__ void load8(const TT* p, float (&v)[8]);
@@ -94,25 +87,6 @@ __device__ __forceinline__ void load8<uint16_t>(const uint16_t* p, float (&v)[8]
     }
 }
 
-__device__ __forceinline__ void split8(const float (&x)[8], float s, din_half8& hi, din_half8& lo) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const float v = x[e] * s;
-        const _Float16 h = (_Float16)v;
-        hi[e] = h;
-        lo[e] = (_Float16)(v - (float)h);
-    }
-}
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic
-// (lgkmcnt) but not for its outstanding global loads, which __syncthreads()
-// (a workgroup release fence: vmcnt(0) on gfx9) would drain -- prefetched
-// gathers stay in flight across it.
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
 
 // Segments: the N samples are scored as consecutive Dice batches of S
 // (DINRanker.predict's DataLoader batches, DIN.py:1245-1283); workgroup
@@ -562,12 +536,6 @@ __global__ void din_absmax_kernel(const void* __restrict__ table, int dtype, int
     if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // m >= 0: bit order == value order
 }
 
-__device__ __forceinline__ float pow2_scale(float mx) {
-    if (!(mx > 0.0f)) return 1.0f;
-    int e;
-    frexpf(mx, &e);  // mx in [2^(e-1), 2^e)
-    return ldexpf(1.0f, 14 - e);
-}
 
 __global__ void din_scales_kernel(const float* __restrict__ prep_ap, int ID, const unsigned int* __restrict__ mx,
                                   DinScales* __restrict__ out) {
@@ -757,27 +725,6 @@ static inline size_t din_tm_lds(int NI, int T) {
            + (size_t)TM_SW * 12 + (TM_TMAX + 4) * 4;  // perm, perm * T, perm * T * 144, c_t, counter
 }
 
-// the value of lane l ^ 16 / l ^ 32 (v_permlane16_swap / v_permlane32_swap
-// with vdst = src = v: r[0] holds the lower row's value in the upper row,
-// r[1] the upper row's in the lower one) -- VALU, no LDS round trip
-__device__ __forceinline__ uint32_t xor16u(uint32_t v, int lane) {
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return ((lane >> 4) & 1) ? (uint32_t)r[0] : (uint32_t)r[1];
-}
-__device__ __forceinline__ uint32_t xor32u(uint32_t v, int lane) {
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return (lane >> 5) ? (uint32_t)r[0] : (uint32_t)r[1];
-}
-__device__ __forceinline__ double xor16d(double v, int lane) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    return __longlong_as_double((long long)((uint64_t)xor16u((uint32_t)b, lane) |
-                                            ((uint64_t)xor16u((uint32_t)(b >> 32), lane) << 32)));
-}
-__device__ __forceinline__ double xor32d(double v, int lane) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    return __longlong_as_double((long long)((uint64_t)xor32u((uint32_t)b, lane) |
-                                            ((uint64_t)xor32u((uint32_t)(b >> 32), lane) << 32)));
-}
 
 // Dice(x) with the batch (mean, 1 / (std + 1e-8)) of x's column (DIN.py:39-44)
 __device__ __forceinline__ float dice_fast(float x, float mean, float inv) {
@@ -1724,22 +1671,6 @@ __device__ __forceinline__ void mlp_epilogue(const din_f4 (&acc)[2][NT], float i
     __syncthreads();
 }
 
-// W0 slice staging: every thread moves CPT 16-B chunks (clamped, so the
-// loads are unconditional; the stores past the slice are skipped)
-typedef uint32_t din_u4 __attribute__((ext_vector_type(4)));  // native vector: promotable to VGPRs
-
-template <int CPT, int CH>
-__device__ __forceinline__ void stage_load(din_u4 (&stg)[CPT], const din_u4* __restrict__ src, int tid) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) stg[i] = src[min(tid + 256 * i, CH - 1)];
-}
-template <int CPT, int CH>
-__device__ __forceinline__ void stage_store(const din_u4 (&stg)[CPT], din_u4* dst, int tid) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i)
-        if (tid + 256 * i < CH) dst[tid + 256 * i] = stg[i];
-}
-
 template <typename TT, int NT>
 __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
     const TT* __restrict__ table, const int64_t* __restrict__ row_base, int n_user, int n_item,
@@ -1819,7 +1750,12 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
     stage_load<CPT, CH>(stg, w1pack, tid);
     stage_store<CPT, CH>(stg, wr[0], tid);
     lds_barrier();
-    for (int s = 0; s < KS; ++s) {
+    // one k-step: prefetch the next slice / A rows / indices, the MFMAs
+    // (A fragments: hi, and lo when split; per column tile its two W
+    // fragments), then the slice hand-off.  The split (fp32 tables, the wh
+    // steps) is a compile-time parameter: two loops, no branch per MFMA.
+    auto kstep = [&](int s, auto split_c) {
+        constexpr bool SPLIT = decltype(split_c)::value;
         if (s + 1 < KS) stage_load<CPT, CH>(stg, w1pack + (size_t)(s + 1) * CH, tid);
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
@@ -1827,20 +1763,12 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
             idx1[a] = idx2[a];
             idx2[a] = idx_load(s + 3 < KS ? s + 3 : KS - 1, a);
         }
-        if (s == KE) {
-            const float r = s_h / s_k;  // exact: both are powers of two
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int j = 0; j < NT; ++j) acc[a][j] *= r;
-        }
-        const bool split = F32 || s >= KE;
         const float sc = s >= KE ? s_h : s_k;
         din_half8 ahi[2], alo[2];
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
             float v[8];
-            if (F32 || s >= KE) {
+            if (SPLIT) {
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(raw[a][e >> 2][e & 3]);
             } else {
@@ -1863,7 +1791,8 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
             for (int a = 0; a < 2; ++a) {
                 acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[a], bh, acc[a][j], 0, 0, 0);
                 acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[a], bl, acc[a][j], 0, 0, 0);
-                if (split) acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[a], bh, acc[a][j], 0, 0, 0);
+                if constexpr (SPLIT)
+                    acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[a], bh, acc[a][j], 0, 0, 0);
             }
         }
         if (s + 1 < KS) stage_store<CPT, CH>(stg, wr[(s + 1) & 1], tid);
@@ -1873,7 +1802,19 @@ __global__ __launch_bounds__(256, 2) void din_mlp1_kernel(
             raw[a][0] = nraw[a][0];
             raw[a][1] = nraw[a][1];
         }
+    };
+    for (int s = 0; s < KE; ++s) {
+        if constexpr (F32) kstep(s, std::true_type{});
+        else kstep(s, std::false_type{});
     }
+    {
+        const float r = s_h / s_k;  // exact: both are powers of two
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[a][j] *= r;
+    }
+    for (int s = KE; s < KS; ++s) kstep(s, std::true_type{});
     // epilogue: scale, bias, store, per-64-row-half fp64 column sums, max |z1|
     lds_barrier();  // (every wave is past its last read of wr)
     double2* cs = reinterpret_cast<double2*>(&wr[0][0]);  // [4 waves][NT * 16]
