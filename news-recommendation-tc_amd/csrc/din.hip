@@ -2049,24 +2049,38 @@ __global__ __launch_bounds__(512) void din_gemm_kernel(
 }
 
 // ------------------------------------------------------------ 8. head --
-__global__ void din_head_kernel(const float* __restrict__ Z, const float2* __restrict__ zstats_all,
-                                int64_t B, int64_t S, int H, const float* __restrict__ w,
-                                const float* __restrict__ bias, float* __restrict__ probs,
-                                float* __restrict__ logits) {
-    const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= B) return;
-    const float2* zstats = zstats_all + (b / S) * H;
-    float s = 0.0f;
-    for (int j = lane; j < H; j += 64) {
-        const float2 st = zstats[j];
-        s += w[j] * dice_fast(Z[b * H + j], st.x, st.y);  // st = (mean, 1 / (std + 1e-8))
-    }
-    s = wave_sum_f32(s);
-    if (lane == 0) {
-        const float lg = s + bias[0];
-        if (logits) logits[b] = lg;
-        probs[b] = 1.0f / (1.0f + expf(-lg));
+// logit = sum_j w_j Dice(z2_j) + b (DIN.py:283-284), prob = sigmoid.  16
+// lanes per sample (4 samples per wave, lane l16 takes j = l16, l16 + 16, ...
+// in order), the 16 partial sums combined by a fixed DPP tree within the
+// row; grid-strided over the samples.
+__device__ __forceinline__ float row16_sum(float x) {
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false));  // row_half_mirror
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, false));  // row_mirror
+    return x;
+}
+
+__global__ __launch_bounds__(256) void din_head_kernel(const float* __restrict__ Z, const float2* __restrict__ zstats_all,
+                                                       int64_t B, int64_t S, int H, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, float* __restrict__ probs,
+                                                       float* __restrict__ logits) {
+    const int l16 = threadIdx.x & 15;
+    const float b0 = bias[0];
+    for (int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; b < B; b += (int64_t)gridDim.x * 16) {
+        const float2* zstats = zstats_all + (b / S) * H;
+        const float* zr = Z + b * H;
+        float s = 0.0f;
+        for (int j = l16; j < H; j += 16) {
+            const float2 st = zstats[j];
+            s += w[j] * dice_fast(zr[j], st.x, st.y);  // st = (mean, 1 / (std + 1e-8))
+        }
+        s = row16_sum(s);
+        if (l16 == 0) {
+            const float lg = s + b0;
+            if (logits) logits[b] = lg;
+            probs[b] = 1.0f / (1.0f + expf(-lg));
+        }
     }
 }
 
@@ -2360,7 +2374,6 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     col_stats_kernel<<<dim3(gs, (ncol_att + 3) / 4), 256, 0, s>>>(w.hpart, bps_att, (int)(n_seg * bps_att),
                                                                    ncol_att, batch, S, w.hstats, w.hinv);
 #undef NRK_ATT_TM
-    const int64_t gb = (batch + 3) / 4;
     const int64_t nb_m = (batch + 63) / 64;
     const int bps = n_seg == 1 ? (int)nb_m : (int)(S / 64);  // 64-row GEMM blocks per segment
     if (din_fast(T, h1)) {
@@ -2456,8 +2469,8 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
     }
     col_stats_kernel<<<dim3(gs, (h2 + 3) / 4), 256, 0, s>>>(w.z2part, bps, (int)nb_m, h2, batch, S,
                                                             nullptr, w.z2stats);
-    din_head_kernel<<<(unsigned)gb, 256, 0, s>>>(w.z2, w.z2stats, batch, S, h2, mlp_w2, mlp_b2,
-                                                 out_probs, out_logits);
+    din_head_kernel<<<(unsigned)std::min<int64_t>((batch + 15) / 16, 8192), 256, 0, s>>>(
+        w.z2, w.z2stats, batch, S, h2, mlp_w2, mlp_b2, out_probs, out_logits);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
