@@ -234,6 +234,25 @@ __device__ __forceinline__ void top_insert(float (&t)[MT], float v) {
     t[0] = fmaxf(t[0], v);
 }
 
+// dev-only phase stamps of ip_scan_kernel (make dev DEVFLAGS=-DNRK_SCAN_STAMP=1,
+// read by nrk_dev_scan_stamps): wave 0 of each workgroup, shader cycles per phase
+#ifndef NRK_SCAN_STAMP
+#define NRK_SCAN_STAMP 0
+#endif
+#if NRK_SCAN_STAMP
+__device__ unsigned long long scan_stamps[1024 * 8];
+#define SC_STAMP(k)                                           \
+    do {                                                      \
+        const uint64_t t_now_ = __builtin_readcyclecounter(); \
+        sstp[k] += t_now_ - t_prev;                           \
+        t_prev = t_now_;                                      \
+    } while (0)
+#else
+#define SC_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
 // Per-user screen record (uinfo): theta_lb (scaled), eps (scaled), the
 // exact power-of-two scale scl = su * catalog scale, eps (unscaled).
 //
@@ -264,6 +283,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
     const int ubase = blockIdx.x * (NW * 32 * UG) + wave * (32 * UG);
+#if NRK_SCAN_STAMP
+    uint64_t sstp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t_prev = 0;
+#endif
 
     const int nblk = (n_items + 31) >> 5;
     // tiles [tile_lo, tile_hi) of the catalog (a catalog shard of config 4
@@ -497,6 +520,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
 #pragma unroll
                 for (int b = 0; b < TB; ++b) any_app |= mx[g][b] >= tau[g];
         }
+        SC_STAMP(2);
         if (__builtin_amdgcn_ballot_w64(any_app)) {
 #pragma unroll
             for (int g = 0; g < UG; ++g) {
@@ -546,6 +570,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             const float tv = lb == -INFINITY ? -FLT_MAX : __uint_as_float(rb);
             tau[g] = live[g] ? tv : INFINITY;
         };
+        SC_STAMP(3);
         if constexpr (IE == 1) {
 #pragma unroll
             for (int g = 0; g < UG; ++g) {
@@ -576,8 +601,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         // own pieces of tile tt landed (the next NSL-2 tiles' stay in
         // flight; appends issued since only make the wait conservative); the
         // barrier publishes everyone's pieces and retires the previous slot
+        SC_STAMP(4);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * (NSL - 2)) : "memory");
+        SC_STAMP(0);
         __builtin_amdgcn_s_barrier();
+        SC_STAMP(1);
         issue_tile(tt + (NSL - 1) * tstep, (it + NSL - 1) % NSL);
         const int sl = it % NSL;
         u32x4 afr[FULLREAD ? TB * DS : 1];
@@ -585,9 +613,17 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         if (tt < full_tiles) tile(tt, sl, afr, std::false_type{}, 0);
         else tile(tt, sl, afr, std::true_type{}, 0);
     };
+#if NRK_SCAN_STAMP
+    t_prev = __builtin_readcyclecounter();
+#endif
 #pragma unroll
     for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p * tstep, p);
     for (int tt = tile_lo, it = 0; tt < ntile; tt += tstep, ++it) step(tt, it);
+#if NRK_SCAN_STAMP
+    SC_STAMP(4);
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && APP)
+        for (int k = 0; k < 8; ++k) scan_stamps[blockIdx.x * 8 + k] = sstp[k];
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
 
 #pragma unroll
@@ -2137,6 +2173,13 @@ static void launch_exact(const float* users, int64_t n_users, const float* items
 using namespace nrk;
 
 extern "C" {
+
+#if NRK_SCAN_STAMP
+// dev-only: the phase stamps of the last ip_scan_kernel launch (1024 x 8 u64)
+int nrk_dev_scan_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(scan_stamps), sizeof(scan_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t nrk_ip_catalog_bytes(int64_t n_items, int dim) {
     if (n_items < 0 || dim <= 0 || dim > 256) return 0;
