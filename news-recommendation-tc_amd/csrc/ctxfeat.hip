@@ -129,6 +129,84 @@ __device__ __forceinline__ double coop_word_diff(const PwPlan& pl, const double*
     }
 }
 
+// xor-1 / xor-2 / xor-4 partner of a double within 8 lanes (DPP quad swaps
+// and the half-row mirror: lane j gets 7 - j, whose pair sums equal the
+// xor-4 partner's after the first two steps)
+__device__ __forceinline__ double dpp_f64(double v, int ctrl) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    int lo = (int)(uint32_t)b, hi = (int)(uint32_t)(b >> 32);
+    switch (ctrl) {
+        case 0xB1: lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false); break;
+        case 0x4E: lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false); break;
+        default: lo = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, false); break;
+    }
+    return __longlong_as_double((long long)((uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32)));
+}
+
+// coop_word_diff for all N history items of one recalled row at once: the
+// item row's elements are read once and feed the N accumulators (the same
+// operations, per item, as coop_word_diff: bit-identical results)
+__device__ __forceinline__ void coop_word_diff_n(const PwPlan& pl, const double* __restrict__ r,
+                                                 const double (*__restrict__ h)[CTX_DC_MAX], int N, int s,
+                                                 double (&out)[CTX_NMAX]) {
+    const int l = s >> 3, j = s & 7;
+    const bool act = l < pl.nl;
+    const int lb = act ? pl.b[l] : 0, ln = act ? pl.n[l] : 0;
+    double acc[CTX_NMAX] = {0.0, 0.0, 0.0, 0.0};
+    auto fa = [&](int e, bool first) {
+        const double re = (double)(float)r[e];
+#pragma unroll
+        for (int i = 0; i < CTX_NMAX; ++i) {
+            if (i >= N) break;
+            const double d = __dsub_rn(re, h[i][e]);
+            double p = __dmul_rn(d, d);
+            asm volatile("" : "+v"(p));
+            acc[i] = first ? p : __dadd_rn(acc[i], p);
+        }
+    };
+    const int full = ln - ln % 8;
+    if (ln >= 8) {
+        fa(lb + j, true);
+        for (int i = 8; i < full; i += 8) fa(lb + i + j, false);
+    }
+    const int base = threadIdx.x & 32;  // this half-wave's lane 0
+#pragma unroll
+    for (int i = 0; i < CTX_NMAX; ++i) {
+        if (i >= N) break;
+        double a = acc[i];
+        a = __dadd_rn(a, dpp_f64(a, 0xB1));
+        a = __dadd_rn(a, dpp_f64(a, 0x4E));
+        a = __dadd_rn(a, dpp_f64(a, 0x141));
+        acc[i] = a;
+    }
+    if (j == 0 && act) {
+        for (int e = ln < 8 ? 0 : full; e < ln; ++e) {
+            const double re = (double)(float)r[lb + e];
+#pragma unroll
+            for (int i = 0; i < CTX_NMAX; ++i) {
+                if (i >= N) break;
+                const double d = __dsub_rn(re, h[i][lb + e]);
+                double p = __dmul_rn(d, d);
+                asm volatile("" : "+v"(p));
+                acc[i] = (ln < 8 && e == 0) ? p : __dadd_rn(acc[i], p);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < CTX_NMAX; ++i) {
+        if (i >= N) break;
+        const double v0 = __shfl(acc[i], base, WAVE), v1 = __shfl(acc[i], base + 8, WAVE);
+        const double v2 = __shfl(acc[i], base + 16, WAVE), v3 = __shfl(acc[i], base + 24, WAVE);
+        switch (pl.shape) {
+            case 0: out[i] = v0; break;
+            case 1: out[i] = __dadd_rn(v0, v1); break;
+            case 2: out[i] = __dadd_rn(__dadd_rn(v0, v1), v2); break;
+            case 3: out[i] = __dadd_rn(v0, __dadd_rn(v1, v2)); break;
+            default: out[i] = __dadd_rn(__dadd_rn(v0, v1), __dadd_rn(v2, v3)); break;
+        }
+    }
+}
+
 __device__ __forceinline__ float dot_f32(const float* a, const float* b, int n) {
     float s = 0.0f;
     for (int i = 0; i < n; ++i) s = fmaf(a[i], b[i], s);
@@ -151,7 +229,7 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
                                                            double* __restrict__ out_raw,
                                                            int32_t* __restrict__ out_codes) {
     __shared__ double s_cont[4][CTX_NMAX][CTX_DC_MAX];
-    __shared__ float s_w2v[4][CTX_NMAX][CTX_DW_MAX];
+    __shared__ __attribute__((aligned(16))) float s_w2v[4][CTX_NMAX][CTX_DW_MAX];
     __shared__ double s_wd[4][64][CTX_NMAX];  // word_diff of this chunk's rows
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t g = (int64_t)blockIdx.x * 4 + wv;
@@ -182,19 +260,19 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
         // tasks per wave instruction (coalesced item-row reads), into LDS
         const int nr = (int)(p1 - c0 < 64 ? p1 - c0 : 64);
         if (hn > 0) {
-            const int ntask = nr * N;
-            for (int t0 = 0; t0 < ntask; t0 += 2) {
-                const int task = t0 + (lane >> 5);
-                const int tc = task < ntask ? task : ntask - 1;
-                const int qr = tc / N, i = tc % N;
+            // one row per half-wave, all N history items per pass over the row
+            for (int r0 = 0; r0 < nr; r0 += 2) {
+                const int qr0 = r0 + (lane >> 5);
+                const int qr = qr0 < nr ? qr0 : nr - 1;
                 const int64_t pos = tb.pair_pos ? tb.pair_pos[c0 + qr] : c0 + qr;
                 const int32_t it = tb.pair_item[pos];
-                const bool on = i < hn && hcont[i] && it >= 0 && (tb.content_flags[it] & 2);
-                const double* rrow = tb.content + (int64_t)(on ? it : 0) * tb.dc;
-                // every lane runs the (shuffling) sum; rows that do not count take 0
-                const double ss = coop_word_diff(plan, rrow, s_cont[wv][i], lane & 31);
-                const double wd = on ? sqrt(ss) : 0.0;
-                if ((lane & 31) == 0 && task < ntask) s_wd[wv][qr][i] = wd;
+                const bool ion = it >= 0 && (tb.content_flags[it] & 2);
+                const double* rrow = tb.content + (int64_t)(ion ? it : 0) * tb.dc;
+                // every lane runs the (shuffling) sums; rows that do not count take 0
+                double ss[CTX_NMAX];
+                coop_word_diff_n(plan, rrow, s_cont[wv], N, lane & 31, ss);
+                if ((lane & 31) == 0 && qr0 < nr)
+                    for (int i = 0; i < N; ++i) s_wd[wv][qr][i] = (ion && i < hn && hcont[i]) ? sqrt(ss[i]) : 0.0;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
@@ -218,12 +296,30 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
             const bool iw2v = it >= 0 && tb.w2v_ok[it];
             const double icre = it >= 0 ? (double)(float)tb.created[it] : (double)NAN;  // f32 array (:588-594)
             float sims[CTX_NMAX];
+            // sim_i (:612-615): 0 when h_i has no vector, zero vector for a
+            // missing item.  The N dots run interleaved over one pass of the
+            // item's row (16-B loads; each dot still sums e = 0, 1, ... in order)
+            float dots[CTX_NMAX] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (iw2v && hn > 0) {
+                const float* ir = tb.w2v + (int64_t)it * tb.dw;
+                if ((tb.dw & 3) == 0) {
+                    for (int e = 0; e < tb.dw; e += 4) {
+                        const float4 x = *reinterpret_cast<const float4*>(ir + e);
+#pragma unroll
+                        for (int i = 0; i < CTX_NMAX; ++i) {
+                            if (i >= N) break;
+                            const float4 y = *reinterpret_cast<const float4*>(&s_w2v[wv][i][e]);
+                            dots[i] = fmaf(x.w, y.w, fmaf(x.z, y.z, fmaf(x.y, y.y, fmaf(x.x, y.x, dots[i]))));
+                        }
+                    }
+                } else {
+                    for (int i = 0; i < N; ++i) dots[i] = dot_f32(ir, s_w2v[wv][i], tb.dw);
+                }
+            }
             for (int i = 0; i < N; ++i) {
                 sims[i] = NAN;
                 if (i >= hn) continue;
-                // sim_i (:612-615): 0 when h_i has no vector, zero vector for a missing item
-                float sv = 0.0f;
-                if (hw2v[i] && iw2v) sv = dot_f32(tb.w2v + (int64_t)it * tb.dw, s_w2v[wv][i], tb.dw);
+                const float sv = hw2v[i] && iw2v ? dots[i] : 0.0f;
                 sims[i] = sv;
                 f[1 + 3 * i] = (double)sv;
                 // time_diff_i (:617-631)
@@ -263,8 +359,21 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
                 f[1 + 3 * N + 3] = (double)(float)sqrt((double)var);  // correctly rounded f32 sqrt
             }
             // item_user_sim (:538-558), zero vector for a missing item
-            if (uyt && it >= 0 && tb.item_yt_ok[it])
-                f[1 + 3 * N + 4] = (double)dot_f32(tb.item_yt + (int64_t)it * tb.dy, tb.user_yt + (int64_t)u * tb.dy, tb.dy);
+            if (uyt && it >= 0 && tb.item_yt_ok[it]) {
+                const float* a = tb.item_yt + (int64_t)it * tb.dy;
+                const float* b = tb.user_yt + (int64_t)u * tb.dy;
+                float d = 0.0f;
+                if ((tb.dy & 3) == 0) {
+                    for (int e = 0; e < tb.dy; e += 4) {
+                        const float4 x = *reinterpret_cast<const float4*>(a + e);
+                        const float4 y = *reinterpret_cast<const float4*>(b + e);
+                        d = fmaf(x.w, y.w, fmaf(x.z, y.z, fmaf(x.y, y.y, fmaf(x.x, y.x, d))));
+                    }
+                } else {
+                    d = dot_f32(a, b, tb.dy);
+                }
+                f[1 + 3 * N + 4] = (double)d;
+            }
             // recall_in_user_cat (:677-690)
             const int32_t c = it >= 0 ? tb.category[it] : -1;
             int inc = 0;
