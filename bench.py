@@ -53,8 +53,8 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
-BUSY_FILE = os.path.join(REPO, "profiles", "r03_busy.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04_traffic.json")
+BUSY_FILE = os.path.join(REPO, "profiles", "r04_busy.json")
 CSRC = os.path.join(REPO, "news-recommendation-tc_amd", "csrc")
 
 
@@ -92,7 +92,9 @@ def pmc_busy(kernels, default_config):
         return None
     out = {}
     for k in kernels:
-        m = [v for name, v in b["kernels"].items() if name.startswith(k)]
+        # demangled names start with k; a kernel whose name stays mangled
+        # (template + lambda) contains it without the namespace
+        m = [v for name, v in b["kernels"].items() if name.startswith(k) or k.replace("nrk::", "") in name]
         if m:
             out[k.replace("nrk::", "")] = {x: m[0].get(x) for x in ("mfma_busy", "valu_busy", "wait_any", "wait_inst",
                                                                      "active")}
@@ -663,12 +665,12 @@ def run_din(args, device, rank, world):
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": din_traffic,
                         "traffic_unit": "bytes per pass, every launch of one nrk_din_forward_segments call "
-                                        "(profiles/r03_traffic.json din_pass)",
+                                        "(profiles/r04_traffic.json din_pass)",
                         "kernel": f"nrk_din_forward_segments ({n_loc} samples in Dice batches of {B}, one call)",
                         "kernel_ms": round(pass_ms, 4),
                         "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * n_loc,
-                        "busy": pmc_busy(["nrk::din_att", "nrk::din_wh", "nrk::din_mlp1", "nrk::din_mlp2",
-                                          "nrk::din_head"], default_cfg)}}
+                        "busy": pmc_busy(["nrk::din_tm_plan", "nrk::din_att", "nrk::din_wh", "nrk::din_mlp1",
+                                          "nrk::din_mlp2", "nrk::din_head"], default_cfg)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle
 
@@ -1005,7 +1007,7 @@ def main(argv=None):
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                 "traffic": round(traffic) if traffic else None,
-                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r03_traffic.json; "
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r04_traffic.json; "
                                 "null when absent or measured on other kernel sources)",
                 "kernel": ("ip_scan_kernel (fp16 MFMA 32x32x16 screen) + ip_shard_bound_kernel + bound all_gather, "
                            "this rank's item blocks" if catalog_mode else
@@ -1014,7 +1016,7 @@ def main(argv=None):
                 "algorithmic_flop_per_launch": flops,
                 "busy": pmc_busy(["nrk::ip_scan_kernel", "nrk::ip_select_kernel", "nrk::ip_refine_kernel",
                                   "nrk::tt_user_kernel"], default_cfg),
-                "busy_source": "profiles/r03_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
+                "busy_source": "profiles/r04_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
                                "SQ_WAIT_ANY, GRBM_GUI_ACTIVE passes; tools/pmc_busy.py, calibrated by "
                                "tools/calib)"}
 

@@ -28,7 +28,7 @@ from collections import defaultdict
 
 SIMDS = 256 * 4
 KEEP = ("ip_screen", "ip_scan", "ip_select", "ip_refine", "din_att_h", "din_wh", "din_mlp1", "din_mlp2", "din_head", "tt_user",
-        "din_att_stats", "din_att_wh")
+        "din_att_stats", "din_att_wh", "din_att_tm", "din_tm_plan")
 
 
 def load(path):
