@@ -28,14 +28,15 @@ def main():
     for _ in range(2):
         ops.ip_topk_scan(u, cat, K, ws)
     torch.cuda.synchronize()
-    buf = np.zeros(1024 * 8, np.uint64)
+    buf = np.zeros(1024 * 16, np.uint64)
     assert _lib.lib().nrk_dev_scan_stamps(buf.ctypes.data_as(ctypes.c_void_p)) == 0
-    st = buf.reshape(1024, 8)[:, :5]
-    st = st[st.sum(1) > 0].astype(np.float64)
-    tot = st.sum(1)
-    print(f"workgroups {len(st)}; cycles: mean {tot.mean():.0f} min {tot.min():.0f} max {tot.max():.0f}")
-    for k, nm in enumerate(NAMES):
-        print(f"  {nm:14s} {st[:, k].mean():12.0f}  {100 * st[:, k].mean() / tot.mean():5.1f}%")
+    for half, name in ((0, "wave 0 (books after its tile)"), (1, "wave NW/2 (books one tile late)")):
+        st = buf.reshape(1024, 2, 8)[:, half, :5]
+        st = st[st.sum(1) > 0].astype(np.float64)
+        tot = st.sum(1)
+        print(f"{name}: workgroups {len(st)}; cycles: mean {tot.mean():.0f} min {tot.min():.0f} max {tot.max():.0f}")
+        for k, nm in enumerate(NAMES):
+            print(f"  {nm:14s} {st[:, k].mean():12.0f}  {100 * st[:, k].mean() / tot.mean():5.1f}%")
 
 
 if __name__ == "__main__":
