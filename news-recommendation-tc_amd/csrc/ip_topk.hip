@@ -263,6 +263,9 @@ __device__ __forceinline__ void top_insert(float (&t)[MT], float v) {
 #ifndef NRK_SCAN_STAGGER
 #define NRK_SCAN_STAGGER 1
 #endif
+#ifndef NRK_SCAN_FLOOR
+#define NRK_SCAN_FLOOR 0
+#endif
 #ifndef NRK_SCAN_PRIO
 #define NRK_SCAN_PRIO 0
 #endif
@@ -278,7 +281,10 @@ constexpr bool STAG = NRK_SCAN_STAGGER;
 #ifndef NRK_SCAN_INS_BR
 #define NRK_SCAN_INS_BR 1
 #endif
-constexpr bool SCAN_APP_ASM = NRK_SCAN_APP_ASM, SCAN_INS_BR = NRK_SCAN_INS_BR;
+#ifndef NRK_SCAN_APP_GRP
+#define NRK_SCAN_APP_GRP 1
+#endif
+constexpr bool SCAN_APP_ASM = NRK_SCAN_APP_ASM, SCAN_INS_BR = NRK_SCAN_INS_BR, SCAN_APP_GRP = NRK_SCAN_APP_GRP;
 #if NRK_SCAN_STAMP
 __device__ unsigned long long scan_stamps[1024 * 16];
 #define SC_STAMP(k)                                           \
@@ -423,7 +429,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             "s_mov_b64 exec, %0"
             : "=&s"(sv)
             : "s"(m), "v"(off), "v"(d), "s"(wapp)
-            : "memory");
+            : "memory", "scc");  // s_and_saveexec writes SCC
     };
 
     const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
@@ -572,6 +578,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         tau[g] = live[g] ? tv : INFINITY;
     };
     auto book = [&](int tt, const float (&mx)[UG][TB], bool ins_ok) __attribute__((always_inline)) {
+#if NRK_SCAN_FLOOR  // dev floor builds (tools/scan_only.py): 1 = no bookkeeping, 2 = no appends, 3 = no inserts
+        if constexpr (NRK_SCAN_FLOOR == 1) return;
+        if constexpr (NRK_SCAN_FLOOR == 3) ins_ok = false;
+#endif
         // the lane's largest max of the tile, per user group
         float vt[UG];
 #pragma unroll
@@ -605,6 +615,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                 }
         }
         SC_STAMP(2);
+#if NRK_SCAN_FLOOR == 2
+        any_app = 0;
+#endif
         if (any_app) {
 #pragma unroll
             for (int g = 0; g < UG; ++g) {
@@ -622,6 +635,38 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                                                id0 + 2u * (b + 1));
                         }
                         pos[g] += TB;
+                    }
+                } else if constexpr (SCAN_APP_GRP && TB > 1) {
+                    // one store per group: a lane appends 0 or 1 of its TB
+                    // half-blocks per tile nearly always, and when it appends
+                    // any, its largest (the tile max vt) is among them -- so a
+                    // single append IS the tile max's half-block; lanes with
+                    // two or more redo theirs in block order from the same slot
+                    // behind a rare scalar branch
+                    uint64_t gm = 0, multi = 0;
+#pragma unroll
+                    for (int b = 0; b < TB; ++b) {
+                        multi |= gm & am[g][b];
+                        gm |= am[g][b];
+                    }
+                    if (gm) {
+                        uint32_t fid = (uint32_t)((tt * TB + TB - 1) * 2 + h);
+#pragma unroll
+                        for (int b = TB - 2; b >= 0; --b)
+                            fid = mx[g][b] >= tau[g] ? (uint32_t)((tt * TB + b) * 2 + h) : fid;
+                        const uint32_t p0 = pos[g];
+                        app_store_if(gm, min(p0, lim[g]), make_uint2(__float_as_uint(vt[g]), fid));
+#pragma unroll
+                        for (int b = 0; b < TB; ++b) pos[g] = add_if(pos[g], am[g][b]);
+                        if (multi) {
+                            uint32_t p = p0;
+#pragma unroll
+                            for (int b = 0; b < TB; ++b) {
+                                app_store_if(am[g][b] & multi, min(p, lim[g]),
+                                             make_uint2(__float_as_uint(mx[g][b]), (uint32_t)((tt * TB + b) * 2 + h)));
+                                p = add_if(p, am[g][b]);
+                            }
+                        }
                     }
                 } else {
 #pragma unroll
