@@ -2246,6 +2246,13 @@ static inline int next_pow2(int x) {
 #define NRK_SCAN_SAMPLE 8
 #endif
 constexpr int SCAN_SAMPLE = NRK_SCAN_SAMPLE;
+// ring slots of the UG = 4 scan (config 2): 4 (one more tile in flight
+// than round 3's 3) since the bookkeeping got cheaper -- bench context, one
+// box, three pairs: scan 5.77 vs 5.80-5.86 ms
+#ifndef NRK_SCAN_NSL4
+#define NRK_SCAN_NSL4 4
+#endif
+constexpr int SCAN_NSL4 = NRK_SCAN_NSL4;
 // list pre-pass of the one-pass scan: n_pre = min(SCAN_PRE_MAX, n / 6) tiles
 // of an n-tile range, none below SCAN_PRE_MIN tiles (dev: -DNRK_SCAN_PRE_MAX=0
 // turns it off)
@@ -2303,7 +2310,7 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
         // (UG = 4) per workgroup at 2 waves / SIMD -- every LDS fragment read
         // and tile barrier serves twice the MFMAs of the 64-user waves
         // (round 3): config-2 screen 6.8-7.0 vs 7.0-7.2 ms
-        launch_scan_v<DP, 8, 3, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s);
+        launch_scan_v<DP, 8, SCAN_NSL4, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s);
         return;
     }
     // 8 waves share a 3-slot ring, 2 workgroups (4 waves / SIMD) per CU; every
