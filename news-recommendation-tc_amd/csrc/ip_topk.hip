@@ -656,9 +656,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                             fid = mx[g][b] >= tau[g] ? (uint32_t)((tt * TB + b) * 2 + h) : fid;
                         const uint32_t p0 = pos[g];
                         app_store_if(gm, min(p0, lim[g]), make_uint2(__float_as_uint(vt[g]), fid));
-#pragma unroll
-                        for (int b = 0; b < TB; ++b) pos[g] = add_if(pos[g], am[g][b]);
+                        pos[g] = add_if(p0, gm);  // one append per lane, unless multi
                         if (multi) {
+                            // p ends at p0 + the lane's append count: the same
+                            // as pos for the lanes with one or none
                             uint32_t p = p0;
 #pragma unroll
                             for (int b = 0; b < TB; ++b) {
@@ -666,6 +667,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                                              make_uint2(__float_as_uint(mx[g][b]), (uint32_t)((tt * TB + b) * 2 + h)));
                                 p = add_if(p, am[g][b]);
                             }
+                            pos[g] = p;
                         }
                     }
                 } else {
