@@ -2461,6 +2461,9 @@ static int ip_check(const float* users, int64_t n_users, const float* items, con
     NRK_REQUIRE(dim > 0 && dim <= 256, "dim must be in [1, 256]");
     NRK_REQUIRE(k >= 1, "k must be >= 1");
     if (k > IP_KMAX) NRK_UNSUPPORTED("k > 2048 is not compiled");
+    // the MFMA scan addresses the packed catalog body with 32-bit offsets
+    NRK_REQUIRE(k > IP_KFAST || catalog_body_bytes(n_items, pad_dim(dim)) <= (size_t)INT32_MAX,
+                "packed catalog body must be < 2 GiB (n_items * pad_dim(dim) * 2 bytes): split the items");
     if (n_users == 0) return NRK_OK;
     NRK_REQUIRE(users && workspace, "null pointer");
     NRK_REQUIRE(n_items == 0 || (items && catalog), "items/catalog null");

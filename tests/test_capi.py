@@ -52,6 +52,12 @@ def test_argument_errors_raise_valueerror():
     for k in (61, 129):
         rc = L.nrk_ip_topk(None, 10, None, None, 100, 32, k, 0, None, None, None, None, 0, None)
         assert rc == _lib.NRK_EINVAL and b"null pointer" in L.nrk_last_error()
+    # the scan's 32-bit catalog offsets: a packed body of 2 GiB or more is refused up front
+    # (20M items x 256 dims = 10 GB), the exact path (k > 128) takes it
+    rc = L.nrk_ip_topk(None, 10, None, None, 20_000_000, 256, 31, 0, None, None, None, None, 0, None)
+    assert rc == _lib.NRK_EINVAL and b"2 GiB" in L.nrk_last_error()
+    rc = L.nrk_ip_topk(None, 10, None, None, 20_000_000, 256, 129, 0, None, None, None, None, 0, None)
+    assert rc == _lib.NRK_EINVAL and b"null pointer" in L.nrk_last_error()
     # the append lists live in the workspace: bounded at config 2 (250k users), none on the exact path
     ws31 = L.nrk_ip_topk_workspace_bytes(250000, 364047, 32, 31)
     assert 0 < ws31 < 4 << 30
