@@ -84,6 +84,31 @@ def test_ip_topk_vs_oracle(ops, n_users, n_items, d, k):
     assert np.array_equal(e[ro >= 0], eo[ro >= 0])
 
 
+@pytest.mark.parametrize(
+    "n_users,n_items,d,k",
+    [
+        (130, 40000, 32, 10),  # UG = 4 scan, 4-slot ring: 312 tiles, list pre-pass of 52
+        (300, 12000, 64, 61),  # MT = 32, two waves / SIMD (staggered): 187 tiles
+        (257, 20000, 128, 31),  # one block per tile: 625 tiles, pre-pass of 64
+        (100, 9000, 250, 21),  # 16-KB tiles: 281 tiles
+        (64, 32700, 16, 31),  # 8 blocks per tile: 128 tiles, the smallest range with a pre-pass (21)
+    ],
+)
+def test_ip_topk_list_prepass_vs_oracle(ops, n_users, n_items, d, k):
+    """Ranges of >= 128 tiles run the scan's sampled list pre-pass (tile
+    maxima of up to 64 tiles spread over the range seed tau, the main pass
+    does not insert them again): bit-exact rows and scores against the
+    oracle on every scan instantiation it applies to."""
+    rng = np.random.default_rng(n_users * 11 + n_items + d)
+    users = _unit(rng.standard_normal((n_users, d)))
+    items = _unit(rng.standard_normal((n_items, d)))
+    s, r, e = _run_topk(ops, users, items, k)
+    so, ro, eo = oracle.ip_topk(users, items, k, exact=True)
+    assert np.array_equal(r, ro)
+    assert np.array_equal(s, so)
+    assert np.array_equal(e[ro >= 0], eo[ro >= 0])
+
+
 def test_ip_topk_unnormalised_and_offset(ops):
     rng = np.random.default_rng(3)
     users = (rng.standard_normal((150, 32)) * 5).astype(np.float32)
