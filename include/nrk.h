@@ -34,12 +34,15 @@ typedef void* nrk_stream_t; /* hipStream_t */
 #define NRK_EUNSUPPORTED 3 /* configuration outside the compiled variants   */
 
 const char* nrk_last_error(void);
-/* ABI version 2 (round 4): nrk_ip_topk_bound takes k before m (the screen's
- * k, so the bound pass knows the list length); the packed catalog carries a
+/* ABI version 3 (round 5): the round-3 CSR owner protocol
+ * (nrk_ip_topk_screen_range, nrk_ip_topk_band_pack, nrk_ip_topk_refine_csr)
+ * is gone; config 4 runs shard_screen -> shard_band -> refine_x.
+ * Version 2 (round 4): nrk_ip_topk_bound takes k before m (the screen's k, so
+ * the bound pass knows the list length); the packed catalog carries a
  * half-block-major fp16 copy after its header (nrk_ip_catalog_bytes grew);
  * nrk_din_remap_index added; DIN item features 1, 2, 4 or 8.  A caller built
- * against version 1 must be rebuilt. */
-#define NRK_ABI_VERSION 2
+ * against an older version must be rebuilt. */
+#define NRK_ABI_VERSION 3
 int nrk_abi_version(void);
 
 /* ---------------------------------------------------------------------- */
@@ -149,55 +152,37 @@ int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, i
  * holds the SAME packed catalog and fp32 rows (nrk_ip_catalog_build over all
  * items) and screens only its block range [blk_lo, blk_hi) (32-item blocks;
  * blk_lo a multiple of 8192 / (64 * pad_dim(dim)), blk_hi too unless it is
- * the catalog end) for every user; half-block ids stay global.  After the
- * bound exchange (nrk_ip_topk_bound / _apply_bound), nrk_ip_topk_band_pack
- * writes each user's band entries at or above its cut, compacted to
- * out_ent[u * band_cap + j] (8-B entries: scaled fp16 max, global half-block
- * id), out_cnt[u] (-1: the user overflowed -> exact path on the owner);
- * band_cap = nrk_ip_topk_band_cap(k).  The entries of each user block go to
- * its owner (all_to_all), which runs nrk_ip_topk_refine_csr over its users:
- * band_off [n_users + 1] CSR offsets into band (all shards' entries), ucut
- * [n_users, 2] (cut, eps: the owner's own workspace values after
- * apply_bound), ovf_in [n_users] (1 = exact fallback over the full catalog).
- * Output = the final top-k (no merge).  New: no reference counterpart. */
-int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
-                             int dim, int k, int64_t blk_lo, int64_t blk_hi, void* workspace,
-                             size_t workspace_bytes, nrk_stream_t stream);
-int nrk_ip_topk_band_cap(int k);
-int nrk_ip_topk_band_pack(int64_t n_users, int64_t n_items, int dim, int k, const void* workspace,
-                          size_t workspace_bytes, void* out_ent, int32_t* out_cnt, nrk_stream_t stream);
-/* The same shard protocol without the per-shard select (what nrk.dist uses):
- * nrk_ip_topk_shard_screen = the scan of [blk_lo, blk_hi) + per user the m
- * (1..256) largest appended half-block maxima as exact lower bounds
- * (out_bound [n_users, m] f32, descending, -inf padded; k <= 128);
- * nrk_ip_topk_shard_band, after the all_gather of every shard's bounds
- * (bounds [n_lists][n_users][m], n_lists * m <= 512, or NULL): cut =
- * max(the scan's own list bound - 2 eps, k-th largest bound - eps), the
- * appended half-blocks >= cut packed as uint32 global half-block ids to
- * out_ent[u * x_cap + j] (x_cap in [1, 288]; out_cnt -1 when more), and
- * ucut written for the refine. */
+ * the catalog end) for every user; half-block ids stay global.  No per-shard
+ * select:
+ *   nrk_ip_topk_shard_screen = the scan of [blk_lo, blk_hi) + per user the m
+ *   (1..256) largest appended half-block maxima as exact lower bounds
+ *   (out_bound [n_users, m] f32, descending, -inf padded; k <= 128);
+ *   nrk_ip_topk_shard_band, after the all_gather of every shard's bounds
+ *   (bounds [n_lists][n_users][m], n_lists * m <= 512, or NULL): cut =
+ *   max(the scan's own list bound - 2 eps, k-th largest bound - eps), the
+ *   appended half-blocks >= cut packed as uint32 global half-block ids to
+ *   out_ent[u * x_cap + j] (x_cap in [1, 288]; out_cnt -1 when more: the
+ *   user then takes the owner's exact path), and ucut written for the refine.
+ * The ids and counts of each user block go to its owner in one fixed-size
+ * all_to_all (nrk.dist.catalog_sharded_owner, or nrk_rccl_band_alltoall),
+ * and the owner runs nrk_ip_topk_refine_x over its users: source s's ids for
+ * user u at band[(s * src_users + u) * x_cap + j], j < src_cnt[s * src_users
+ * + u]; ucut [n_users, 2] (cut, eps) = the owner's own shard_band values
+ * for its user block (every shard's cut bounds the user's k-th exact score
+ * over the whole catalog); ovf_in [n_users] (1 = exact path over the full
+ * catalog).  Output = the final top-k (no merge).  New: no reference
+ * counterpart. */
 int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
                              int k, int64_t blk_lo, int64_t blk_hi, int m, float* out_bound, void* workspace,
                              size_t workspace_bytes, nrk_stream_t stream);
 int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, const float* bounds, int n_lists,
                            int m, int x_cap, void* workspace, size_t workspace_bytes, void* out_ent,
                            int32_t* out_cnt, nrk_stream_t stream);
-/* The owner's refine over the fixed-slot exchange (what nrk.dist sends: one
- * all_to_all of [n_src][src_users][x_cap] uint32 half-block ids + one of
- * [n_src][src_users] counts, no host-side sizes): source s's ids for user u at
- * band[(s * src_users + u) * x_cap + j], j < src_cnt[s * src_users + u]
- * (shard_band wrote at most x_cap per user, -1 when it had more: the user is
- * then in ovf_in).  Otherwise as nrk_ip_topk_refine_csr. */
 int nrk_ip_topk_refine_x(const float* users, int64_t n_users, const float* items, const void* catalog,
                          int64_t n_items, int dim, int k, int64_t row_offset, const void* band, int n_src,
                          int64_t src_users, int x_cap, const int32_t* src_cnt, const float* ucut,
                          const int32_t* ovf_in, float* out_scores, int32_t* out_rows, double* out_exact,
                          void* workspace, size_t workspace_bytes, nrk_stream_t stream);
-int nrk_ip_topk_refine_csr(const float* users, int64_t n_users, const float* items, const void* catalog,
-                           int64_t n_items, int dim, int k, int64_t row_offset, const int64_t* band_off,
-                           const void* band, const float* ucut, const int32_t* ovf_in, float* out_scores,
-                           int32_t* out_rows, double* out_exact, void* workspace, size_t workspace_bytes,
-                           nrk_stream_t stream);
 
 /* Merge n_lists per-shard top-k_in lists (fp64 exact scores + global rows,
  * list l of user u at [l * list_stride + u * k_in]) into the top-k_out by

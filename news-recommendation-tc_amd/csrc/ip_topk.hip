@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 namespace nrk {
 
@@ -285,6 +286,72 @@ constexpr bool STAG = NRK_SCAN_STAGGER;
 #define NRK_SCAN_APP_GRP 1
 #endif
 constexpr bool SCAN_APP_ASM = NRK_SCAN_APP_ASM, SCAN_INS_BR = NRK_SCAN_INS_BR, SCAN_APP_GRP = NRK_SCAN_APP_GRP;
+// round 5 A/B switches (make dev DEVFLAGS=...):
+//   LAZY   -- round-robin list inserts: every tile folds the lane's tile max
+//             into a pending max per user group, and only group (tt mod UG)
+//             inserts its pending max (one insert check per tile instead of UG)
+//   BSEL   -- the appended half-block picked by v_cndmask on the compare's
+//             lane masks with inline-constant block numbers (no re-compare)
+//   LDSAPP -- appends staged per lane in LDS and flushed to the HBM lists in
+//             runs when some lane's stage fills (one store per flushed entry
+//             slot instead of one per (tile, group); the DMA ring's vmcnt gate
+//             then waits on ring pieces only)
+#ifndef NRK_SCAN_LAZY
+#define NRK_SCAN_LAZY 0
+#endif
+#ifndef NRK_SCAN_BSEL
+#define NRK_SCAN_BSEL 0
+#endif
+#ifndef NRK_SCAN_LDSAPP
+#define NRK_SCAN_LDSAPP 0
+#endif
+// SWP -- the tile's MFMAs software-pipelined against the half-block max
+// reductions (see tile())
+#ifndef NRK_SCAN_SWP
+#define NRK_SCAN_SWP 0
+#endif
+constexpr bool SCAN_LAZY = NRK_SCAN_LAZY, SCAN_BSEL = NRK_SCAN_BSEL, SCAN_LDSAPP = NRK_SCAN_LDSAPP,
+               SCAN_SWP = NRK_SCAN_SWP;
+
+// (lane bit of m) ? T : F, one v_cndmask_b32 on the compare's SGPR lane mask
+// with inline constants (0..64); sel_mask_v: (lane bit of m) ? T : f
+template <int F, int T>
+__device__ __forceinline__ uint32_t sel_mask_c(uint64_t m) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "n"(F), "n"(T), "s"(m));
+    return r;
+}
+template <int T>
+__device__ __forceinline__ uint32_t sel_mask_v(uint64_t m, uint32_t f) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "n"(T), "s"(m));
+    return r;
+}
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): unrolled
+// with the index usable as a constant expression (asm "n" operands)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+// the first b < TB whose lane bit is set in am[b] (TB - 1 if none):
+// TB - 1 v_cndmask_b32 on the compare masks
+template <int TB>
+__device__ __forceinline__ uint32_t first_set_block(const uint64_t (&am)[TB]) {
+    if constexpr (TB == 1) {
+        return 0u;
+    } else {
+        uint32_t bs = sel_mask_c<TB - 1, TB - 2>(am[TB - 2]);
+        static_for<TB - 2>([&](auto bc) {
+            constexpr int b = TB - 3 - decltype(bc)::value;
+            bs = sel_mask_v<b>(am[b], bs);
+        });
+        return bs;
+    }
+}
 #if NRK_SCAN_STAMP
 __device__ unsigned long long scan_stamps[1024 * 16];
 #define SC_STAMP(k)                                           \
@@ -305,17 +372,12 @@ __device__ unsigned long long scan_stamps[1024 * 16];
 // Scan: NW waves x UG x 32 users per workgroup share one NSL-slot LDS ring of
 // catalog tiles (8 KB, or one 16-KB block at dim 256).  Per tile every wave
 // reads the tile's A fragments once and runs TB x DS x UG MFMAs.
-// APP = false, tstep > 1: pass 1 of the two-pass screen -- the tiles
-// tile_lo, tile_lo + tstep, ... only, no appends: the record's list bound
-// is then a lower bound of the user's k-th half-block maximum over that
-// sample (its items are real items), which pass 2 (ip_scan_fixed_kernel)
-// uses as a fixed threshold over the whole catalog.
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false,
-          bool APP = true>
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false>
 __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
     int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
-    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int tstep = 1, int n_pre = 0, int pstride = 1) {
+    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int n_pre = 0, int pstride = 1) {
+    constexpr bool APP = true;  // (the two-pass screen's append-free pass 1 is gone)
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
     constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
@@ -325,6 +387,15 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     static_assert(!FULLREAD || (TB * DS) % 8 == 0, "fragment groups of 8");
     static_assert(NSL >= 2, "ring");
     __shared__ __attribute__((aligned(16))) uint8_t smem[NSL * TILE_BYTES];
+    // LDS append stage (LDSAPP): per (wave, group) STG_C entry slots x 64
+    // lanes x 8 B, entry-major (slot e of lane l at e * 512 + l * 8: any mix
+    // of per-lane slots is bank-conflict free), sized to what the ring leaves
+    // of the CU's LDS share
+    constexpr int WG_PER_CU = (WPE * 4) / NW > 0 ? (WPE * 4) / NW : 1;
+    constexpr int STG_RAW = (163840 / WG_PER_CU - NSL * TILE_BYTES) / (NW * UG * 512);
+    constexpr bool LDSAPP = SCAN_LDSAPP && APP && !TAPP && SCAN_APP_GRP && TB > 1 && STG_RAW >= TB + 1;
+    constexpr int STG_C = LDSAPP ? (STG_RAW < 8 ? STG_RAW : 8) : 1;
+    __shared__ __attribute__((aligned(16))) uint8_t stg[LDSAPP ? NW * UG * STG_C * 512 : 16];
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
@@ -431,6 +502,46 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             : "s"(m), "v"(off), "v"(d), "s"(wapp)
             : "memory", "scc");  // s_and_saveexec writes SCC
     };
+    // LDS stage (LDSAPP): nb = the lane's staged entries per group, pos = the
+    // list position of its first staged entry.  Slot e of group g of this
+    // lane at stg_lane + (g * STG_C + e) * 512.
+    uint32_t nb[UG];
+#pragma unroll
+    for (int g = 0; g < UG; ++g) nb[g] = 0u;
+    const uint32_t stg_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(stg) +
+                              (uint32_t)__builtin_amdgcn_readfirstlane(wave) * (UG * STG_C * 512) + lane * 8;
+    // (score, id) into slot n of group G, from the lanes of m only
+    auto stg_store_if = [&](auto gc, uint64_t m, uint32_t n, uint32_t score, uint32_t id) {
+        constexpr int G = decltype(gc)::value;
+        const uint32_t a = (n << 9) + stg_lane;
+        const uint64_t d = ((uint64_t)id << 32) | score;
+        uint64_t sv;
+        asm volatile(
+            "s_and_saveexec_b64 %0, %1\n\t"
+            "ds_write_b64 %2, %3 offset:%4\n\t"
+            "s_mov_b64 exec, %0"
+            : "=&s"(sv)
+            : "s"(m), "v"(a), "v"(d), "n"(G * STG_C * 512)
+            : "memory", "scc");
+    };
+    // group G's staged entries -> its HBM list (slot e of every lane with
+    // more than e entries -> list position pos + e, clamped like the direct
+    // appends); rare (a lane's stage nearly full), so a run-time loop
+    auto stg_flush = [&](auto gc) {
+        constexpr int G = decltype(gc)::value;
+        for (uint32_t e = 0; e < (uint32_t)STG_C; ++e) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(nb[G] > e);
+            if (!m) break;
+            uint64_t d;
+            asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                         : "=v"(d)
+                         : "v"(stg_lane + e * 512u), "n"(G * STG_C * 512)
+                         : "memory");
+            app_store_if(m, min(pos[G] + e, lim[G]), make_uint2((uint32_t)d, (uint32_t)(d >> 32)));
+        }
+        pos[G] += nb[G];
+        nb[G] = 0u;
+    };
 
     const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
     const int body_bytes = nblk * BLOCK_BYTES;
@@ -439,13 +550,19 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     // 1-KB piece per wave-instruction, no VGPR staging); tiles past the end
     // re-load the last piece (keeps the per-wave vmcnt accounting uniform,
     // the data is never used).
+    // The prefetches run past the range (the main loop NSL - 1 tiles, the
+    // pre-pass (NSL - 1) * pstride): the tile is clamped to the catalog's last
+    // one before the 32-bit offset is formed, so a body just under 2 GiB
+    // (ip_check's limit) cannot wrap it negative.
+    const int last_tile = (nblk - 1) / TB;
     auto issue_tile = [&](int tt, int sl) {
         uint8_t* slot = smem + sl * TILE_BYTES;
+        const uint32_t ttc = (uint32_t)min(tt, last_tile);
 #pragma unroll
         for (int p = 0; p < LPT; ++p) {
             const int piece = p * NW + wave;
-            int off = tt * TILE_BYTES + piece * 1024;
-            off = off < body_bytes ? off : body_bytes - 1024;
+            uint32_t off = ttc * (uint32_t)TILE_BYTES + (uint32_t)piece * 1024u;
+            off = off < (uint32_t)body_bytes ? off : (uint32_t)body_bytes - 1024u;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(catalog + off + lane * 16),
                 (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16, 0, 0);
@@ -521,6 +638,70 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         constexpr bool MASK = decltype(mask_c)::value;
         u32x4 afp[DS];
         if constexpr (PF) pf_issue(sl, 0, afp);
+        if constexpr (SCAN_SWP && !FULLREAD) {
+            // Software pipeline over the TB x UG (block, group) steps: step j's
+            // DS MFMAs issue while step j - 1's 16 accumulators reduce, so the
+            // reduction VALU fills the MFMA shadows instead of waiting on the
+            // wave's own MFMA results; two accumulator sets instead of UG.
+            // The reduction is a depth-3 tree of v_max3 (max is order-free:
+            // the same maxima as a sequential chain).
+            auto red = [&](const f32x16& a, int bb, int gg) __attribute__((always_inline)) {
+                float x[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    x[r] = a[r];
+                    if constexpr (MASK) {
+                        const int row = (tt * TB + bb) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (row >= n_items) x[r] = -INFINITY;
+                    }
+                }
+                auto m3 = [](float p, float q, float s) { return fmaxf(fmaxf(p, q), s); };
+                const float m0 = m3(x[0], x[1], x[2]), m1 = m3(x[3], x[4], x[5]), m2 = m3(x[6], x[7], x[8]);
+                const float m4 = m3(x[9], x[10], x[11]), m5 = m3(x[12], x[13], x[14]);
+                mx[gg][bb] = fmaxf(m3(m0, m1, m2), m3(m4, m5, x[15]));
+            };
+            f32x16 acc0, acc1;
+            u32x4 afb[DS];
+            static_for<TB>([&](auto bc) {
+                constexpr int b = decltype(bc)::value;
+                if constexpr (PF) {
+                    u32x4 afn[DS];
+                    if constexpr (b + 1 < TB) pf_wait_issue(afp, sl, b + 1, afn);
+                    else pf_wait(afp);
+#pragma unroll
+                    for (int s = 0; s < DS; ++s) afb[s] = afp[s];
+                    if constexpr (b + 1 < TB) {
+#pragma unroll
+                        for (int s = 0; s < DS; ++s) afp[s] = afn[s];
+                    }
+                } else {
+                    read_block(sl, b, afb);
+                }
+                static_for<UG>([&](auto gc) {
+                    constexpr int g = decltype(gc)::value, j = b * UG + g;
+                    f32x16& A = (j & 1) ? acc1 : acc0;
+                    const f32x16& P = (j & 1) ? acc0 : acc1;
+                    A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[0]), ufrag[g][0],
+                                                               f32x16{}, 0, 0, 0);
+#pragma unroll
+                    for (int s = 1; s < DS; ++s)
+                        A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[s]), ufrag[g][s], A,
+                                                                   0, 0, 0);
+                    if constexpr (j > 0) red(P, (j - 1) / UG, (j - 1) % UG);
+                    // the order the scheduler must keep: each MFMA of step j
+                    // followed by its share of step j - 1's 8 reduction VALU
+                    if constexpr (!MASK) {
+#pragma unroll
+                        for (int s = 0; s < DS; ++s) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                            if (j > 0) __builtin_amdgcn_sched_group_barrier(0x002, (8 + DS - 1) / DS, 0);
+                        }
+                    }
+                });
+            });
+            red(((TB * UG - 1) & 1) ? acc1 : acc0, TB - 1, UG - 1);
+            return;
+        }
 #pragma unroll
         for (int b = 0; b < TB; ++b) {
             u32x4 afb[DS];
@@ -577,6 +758,15 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         const float tv = fmaxf(__builtin_fmaf(fabsf(c), -0x1p-22f, c) - 0x1p-120f, -FLT_MAX);
         tau[g] = live[g] ? tv : INFINITY;
     };
+    auto lazy_insert = [&](int g) __attribute__((always_inline)) {
+        const float v = pend[g];
+        pend[g] = -INFINITY;
+        const bool in = v > t[g][MT - 1];
+        if (__builtin_amdgcn_ballot_w64(in)) {
+            top_insert<MT>(t[g], in ? v : -INFINITY);
+            retau(g);
+        }
+    };
     auto book = [&](int tt, const float (&mx)[UG][TB], bool ins_ok) __attribute__((always_inline)) {
 #if NRK_SCAN_FLOOR  // dev floor builds (tools/scan_only.py): 1 = no bookkeeping, 2 = no appends, 3 = no inserts
         if constexpr (NRK_SCAN_FLOOR == 1) return;
@@ -618,7 +808,46 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
 #if NRK_SCAN_FLOOR == 2
         any_app = 0;
 #endif
-        if (any_app) {
+        if constexpr (APP && !TAPP && SCAN_APP_GRP && TB > 1 && (SCAN_BSEL || LDSAPP)) {
+            // round 5 form of the grouped appends (BSEL / LDSAPP, see above)
+            if (any_app) {
+                const uint32_t hb0 = (uint32_t)(tt * TB * 2) + (uint32_t)h;  // id of block 0's half-block
+                static_for<UG>([&](auto gc) {
+                    constexpr int g = decltype(gc)::value;
+                    uint64_t gm = 0, multi = 0;
+#pragma unroll
+                    for (int b = 0; b < TB; ++b) {
+                        multi |= gm & am[g][b];
+                        gm |= am[g][b];
+                    }
+                    if (gm) {
+                        // a lone append is the tile max's half-block (see below)
+                        const uint32_t fid = (first_set_block<TB>(am[g]) << 1) + hb0;
+                        const uint32_t p0 = LDSAPP ? nb[g] : pos[g];
+                        if constexpr (LDSAPP) stg_store_if(gc, gm, p0, __float_as_uint(vt[g]), fid);
+                        else app_store_if(gm, min(p0, lim[g]), make_uint2(__float_as_uint(vt[g]), fid));
+                        uint32_t p = add_if(p0, gm);
+                        if (multi) {
+                            p = p0;
+#pragma unroll
+                            for (int b = 0; b < TB; ++b) {
+                                const uint32_t idb = hb0 + 2u * b;
+                                if constexpr (LDSAPP) stg_store_if(gc, am[g][b] & multi, p, __float_as_uint(mx[g][b]), idb);
+                                else app_store_if(am[g][b] & multi, min(p, lim[g]), make_uint2(__float_as_uint(mx[g][b]), idb));
+                                p = add_if(p, am[g][b]);
+                            }
+                        }
+                        if constexpr (LDSAPP) {
+                            nb[g] = p;
+                            // room for the next tile's (up to TB) appends
+                            if (__builtin_amdgcn_ballot_w64(p > (uint32_t)(STG_C - TB))) stg_flush(gc);
+                        } else {
+                            pos[g] = p;
+                        }
+                    }
+                });
+            }
+        } else if (any_app) {
 #pragma unroll
             for (int g = 0; g < UG; ++g) {
                 if constexpr (TAPP) {
@@ -695,7 +924,21 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         //           loop) inserts the lane's largest max since its last
         //           insert (pend), -inf (a no-op) when it does not enter.
         SC_STAMP(3);
-        if (!ins_ok) {  // a pre-pass tile: its maxima are in the lists already
+        if constexpr (SCAN_LAZY && IE == 1) {
+            // LAZY: pend = the lane's largest tile max since its group's last
+            // insert (a pre-pass tile's maxima are in the lists already); group
+            // (tt mod UG) inserts it.  The list stays a set of distinct
+            // half-block maxima (one value per insert), and an inserted value
+            // beat the list minimum at its insert, which bounds every tau since
+            // its tile from above: it was appended at its tile.
+            if (ins_ok) {
+#pragma unroll
+                for (int g = 0; g < UG; ++g) pend[g] = fmaxf(pend[g], vt[g]);
+            }
+#pragma unroll
+            for (int g = 0; g < UG; ++g)
+                if ((tt & (UG - 1)) == g) lazy_insert(g);
+        } else if (!ins_ok) {  // a pre-pass tile: its maxima are in the lists already
         } else if constexpr (IE == 1) {
 #pragma unroll
             for (int g = 0; g < UG; ++g) {
@@ -765,7 +1008,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         SC_STAMP(0);
         __builtin_amdgcn_s_barrier();
         SC_STAMP(1);
-        issue_tile(tt + (NSL - 1) * tstep, (it + NSL - 1) % NSL);
+        issue_tile(tt + NSL - 1, (it + NSL - 1) % NSL);
         if (late && ptt >= 0) book(ptt, mx, pins);
         const int sl = it % NSL;
         u32x4 afr[FULLREAD ? TB * DS : 1];
@@ -816,12 +1059,17 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         }
     }
 #pragma unroll
-    for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p * tstep, p);
+    for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p, p);
 #if NRK_SCAN_PRIO
     if (late) __builtin_amdgcn_s_setprio(1);
 #endif
-    for (int tt = tile_lo, it = 0; tt < ntile; tt += tstep, ++it) step(tt, it);
+    for (int tt = tile_lo, it = 0; tt < ntile; ++tt, ++it) step(tt, it);
     if (late && ptt >= 0) book(ptt, mx, pins);
+    if constexpr (SCAN_LAZY && IE == 1 && APP) {
+#pragma unroll
+        for (int g = 0; g < UG; ++g) lazy_insert(g);  // the final lists hold every pending max
+    }
+    if constexpr (LDSAPP) static_for<UG>([&](auto gc) { stg_flush(gc); });
 #if NRK_SCAN_STAMP
     SC_STAMP(4);
     if ((threadIdx.x == 0 || threadIdx.x == NW / 2 * 64) && blockIdx.x < 1024 && APP)
@@ -837,167 +1085,6 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             acnt[(size_t)user * 2 + h] = (int)(pos[g] - (lim[g] + 1u - (uint32_t)m2));
             if (h == 0) uinfo[user] = make_float4(live[g] ? lb : -INFINITY, eps_s[g], scl[g], eps_u[g]);
         }
-    }
-}
-
-// Pass 2 of the two-pass screen: every tile of [tile_lo, tile_hi) against a
-// FIXED per-user threshold from pass 1's record, tau = lb - 2 eps rounded
-// down (ip_scan_kernel's retau) -- no register list, no inserts.  Per
-// (block, user group): 2 MFMAs (D = 32), 8 v_max3 and one compare; the
-// append branch runs only when some lane of the wave passes.  Correctness
-// is the one-pass scan's invariant with lb = pass 1's list bound: lb is a
-// lower bound of the user's k-th half-block maximum (its values are real
-// items' fp16 scores of the sample), and every half-block maximum >= tau is
-// appended, so the select's theta_lb / theta / band reasoning holds as is.
-// The fp16 user fragments are recomputed exactly as pass 1 computed them.
-template <int DP, int NW, int NSL, int UG, int WPE>
-__global__ __launch_bounds__(NW * 64, WPE) void ip_scan_fixed_kernel(
-    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items, int dim,
-    int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt, const float4* __restrict__ uinfo, int tile_lo,
-    int tile_hi) {
-    constexpr int DS = DP / 16;
-    constexpr int BLOCK_BYTES = 64 * DP;
-    constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
-    constexpr int TILE_BYTES = TB * BLOCK_BYTES;
-    constexpr int LPT = TILE_BYTES / (NW * 1024);
-    static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
-    static_assert(NSL >= 2, "ring");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[NSL * TILE_BYTES];
-
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
-    const int ubase = blockIdx.x * (NW * 32 * UG) + wave * (32 * UG);
-    const int nblk = (n_items + 31) >> 5;
-    const int ntile = tile_hi;
-
-    f16x8 ufrag[UG][DS];
-    float tau[UG];
-    int cnt[UG];
-    uint2* dst[UG];
-#pragma unroll
-    for (int g = 0; g < UG; ++g) {
-        const int user = ubase + g * 32 + q;
-        const bool active = user < n_users;
-        float uval[DS][8];
-        float nrm2 = 0.0f, uabs = 0.0f;
-        const float* urow = users + (size_t)(active ? user : 0) * dim;
-#pragma unroll
-        for (int s = 0; s < DS; ++s)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int d = 16 * s + 8 * h + e;
-                const float f = (active && d < dim) ? urow[d] : 0.0f;
-                uval[s][e] = f;
-                nrm2 += f * f;
-                uabs = fmaxf(uabs, fabsf(f));
-            }
-        nrm2 += __shfl_xor(nrm2, 32, WAVE);
-        uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
-        const float su = pow2_scale(uabs);
-#pragma unroll
-        for (int s = 0; s < DS; ++s)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) ufrag[g][s][e] = (_Float16)(uval[s][e] * su);
-        const float4 inf = uinfo[active ? user : 0];
-        const bool live = active && nrm2 > 0.0f;
-        tau[g] = !live ? INFINITY : inf.x == -INFINITY ? -FLT_MAX : round_down_sub(inf.x, 2.0f * inf.y);
-        cnt[g] = 0;
-        dst[g] = app + ((size_t)(active ? user : 0) * 2 + h) * (size_t)m2;
-    }
-
-    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
-    const int body_bytes = nblk * BLOCK_BYTES;
-    const int tail_blk = n_items >> 5;
-    auto issue_tile = [&](int tt, int sl) {
-        uint8_t* slot = smem + sl * TILE_BYTES;
-#pragma unroll
-        for (int p = 0; p < LPT; ++p) {
-            const int piece = p * NW + wave;
-            int off = tt * TILE_BYTES + piece * 1024;
-            off = off < body_bytes ? off : body_bytes - 1024;
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(catalog + off + lane * 16),
-                (__attribute__((address_space(3))) void*)(slot + piece * 1024), 16, 0, 0);
-        }
-    };
-    const uint32_t lds0 = lds_base + lane * 16;
-    auto read_block = [&](int sl, int b, u32x4 (&af)[DS]) {
-        const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
-        if constexpr (DS == 1) {
-            asm volatile("ds_read_b128 %0, %1 offset:0\n\ts_waitcnt lgkmcnt(0)" : "=&v"(af[0]) : "v"(base) : "memory");
-        } else {
-#pragma unroll
-            for (int s2 = 0; s2 < DS; s2 += 2)
-                asm volatile("ds_read_b128 %0, %2 offset:0\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
-                             : "=&v"(af[s2]), "=&v"(af[s2 + 1])
-                             : "v"(base + 1024u * s2)
-                             : "memory");
-        }
-    };
-    const int full_tiles = tail_blk / TB;
-    auto tile = [&](int tt, int sl, auto mask_c) {
-        constexpr bool MASK = decltype(mask_c)::value;
-#pragma unroll
-        for (int b = 0; b < TB; ++b) {
-            u32x4 afb[DS];
-            read_block(sl, b, afb);
-            f32x16 acc[UG];
-#pragma unroll
-            for (int g = 0; g < UG; ++g) acc[g] = f32x16{};
-#pragma unroll
-            for (int s = 0; s < DS; ++s)
-#pragma unroll
-                for (int g = 0; g < UG; ++g)
-                    acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[s]), ufrag[g][s],
-                                                                    acc[g], 0, 0, 0);
-            float mx[UG];
-            bool any = false;
-#pragma unroll
-            for (int g = 0; g < UG; ++g) {
-                if constexpr (MASK) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int row = (tt * TB + b) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        if (row >= n_items) acc[g][r] = -INFINITY;
-                    }
-                }
-                float v = fmaxf(fmaxf(acc[g][0], acc[g][1]), acc[g][2]);
-#pragma unroll
-                for (int r = 3; r < 15; r += 2) v = fmaxf(fmaxf(v, acc[g][r]), acc[g][r + 1]);
-                mx[g] = fmaxf(v, acc[g][15]);
-                any |= mx[g] >= tau[g];
-            }
-            // appends: the half-block maxima >= tau (the count runs past the
-            // capacity -- the select then sends the user to the exact path --
-            // and extra entries land on the last slot)
-            if (__builtin_amdgcn_ballot_w64(any)) {
-                const uint32_t id = (uint32_t)((tt * TB + b) * 2 + h);
-#pragma unroll
-                for (int g = 0; g < UG; ++g) {
-                    const bool a = mx[g] >= tau[g];
-                    if (a) dst[g][min(cnt[g], m2 - 1)] = make_uint2(__float_as_uint(mx[g]), id);
-                    cnt[g] += a ? 1 : 0;
-                }
-            }
-        }
-    };
-    auto step = [&](int tt, int it) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * (NSL - 2)) : "memory");
-        __builtin_amdgcn_s_barrier();
-        issue_tile(tt + NSL - 1, (it + NSL - 1) % NSL);
-        const int sl = it % NSL;
-        if (tt < full_tiles) tile(tt, sl, std::false_type{});
-        else tile(tt, sl, std::true_type{});
-    };
-#pragma unroll
-    for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p, p);
-    for (int tt = tile_lo, it = 0; tt < ntile; ++tt, ++it) step(tt, it);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-#pragma unroll
-    for (int g = 0; g < UG; ++g) {
-        const int user = ubase + g * 32 + q;
-        if (user < n_users) acnt[(size_t)user * 2 + h] = cnt[g];
     }
 }
 
@@ -1203,7 +1290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     const uint2* __restrict__ cand, int bandcap, const int32_t* __restrict__ cand_cnt,
     const float2* __restrict__ ucut, const int32_t* __restrict__ ovf_flag, int32_t* __restrict__ ovf_list,
     int32_t* __restrict__ ovf_count, float* __restrict__ out_s, int32_t* __restrict__ out_r,
-    double* __restrict__ out_e, const int64_t* __restrict__ band_off = nullptr, int n_src = 0,
+    double* __restrict__ out_e, int n_src = 0,
     int64_t src_users = 0, int x_cap = 0, const int32_t* __restrict__ src_cnt = nullptr) {
     constexpr int SE = SV / WAVE;
     __shared__ Cand surv[4][SV];
@@ -1218,7 +1305,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     // one round trip for the per-user state: the overflow flag, the band
     // count and cut, the user's row and (select slots) the first 32 band
     // entries are loaded together before anything branches on them
-    const bool slots = n_src == 0 && !band_off;  // kernel arguments: uniform
+    const bool slots = n_src == 0;  // kernel argument: uniform
     const float* uv = users + u * dim;
     const int32_t ovf_u = ovf_flag[u];
     const int nbd_slots = slots ? cand_cnt[u] : 0;
@@ -1227,9 +1314,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     // first 32 band slots (lanes 32-63 re-read slot 0: same line, no traffic)
     const uint2 ent0 = slots ? cand[(size_t)u * bandcap + (lane < 32 ? lane : 0)] : make_uint2(0u, 0u);
     if (ovf_u) return;
-    // band: per-user slots of the select (band_off == nullptr, n_src == 0), a
-    // CSR of every catalog shard's entries for this user (band_off), or the
-    // fixed-slot exchange (n_src > 0): source s's entries at
+    // band: per-user slots of the select (n_src == 0), or the fixed-slot
+    // exchange of the catalog-sharded owner protocol (n_src > 0): source s's
+    // entries at
     // cand[(s * src_users + u) * x_cap + j], j < src_cnt[s * src_users + u]
     int src_n = 0;  // lane s < n_src: source s's count
     int nsrc_tot = 0;
@@ -1241,7 +1328,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
             nsrc_tot += (int)wave_sum_f32((float)c);
         }
     }
-    if ((band_off && band_off[u + 1] - band_off[u] > IP_BQ) || nsrc_tot > IP_BQ) {
+    if (nsrc_tot > IP_BQ) {
         // more than the LDS holds: exact path
         if ((threadIdx.x & 63) == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
         return;
@@ -1263,8 +1350,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
         }
         return;
     }
-    const int nbd = n_src > 0 ? 0 : band_off ? (int)(band_off[u + 1] - band_off[u]) : nbd_slots;
-    const uint2* bd = band_off ? cand + band_off[u] : cand + (size_t)u * bandcap;
+    const int nbd = n_src > 0 ? 0 : nbd_slots;
+    const uint2* bd = cand + (size_t)u * bandcap;
     double thr = -INFINITY;
     if (ce.x != -INFINITY) {
         thr = (double)ce.x + (double)ce.y;
@@ -1912,42 +1999,6 @@ __global__ __launch_bounds__(256) void ip_apply_bound_kernel(float2* __restrict_
     }
 }
 
-// ------------------------------------------------ config-4 band exchange --
-// After the screen (+ nrk_ip_topk_apply_bound): per user the band entries
-// at or above the user's (raised) cut, compacted to out_ent[u * bandcap + j],
-// j < out_cnt[u]; out_cnt[u] = -1 when the user overflowed (the owner then
-// runs the exact fallback).  Entries keep the screen's scaled fp16 max and
-// the GLOBAL half-block id (every shard screens a range of one packed
-// catalog, so the scale is common).
-__global__ __launch_bounds__(256) void ip_band_pack_kernel(int64_t n_users, int bandcap, const uint2* __restrict__ cand,
-                                                           const int32_t* __restrict__ cand_cnt,
-                                                           const float2* __restrict__ ucut,
-                                                           const float4* __restrict__ uinfo,
-                                                           const int32_t* __restrict__ ovf_flag,
-                                                           uint2* __restrict__ out_ent, int32_t* __restrict__ out_cnt) {
-    const int lane = threadIdx.x & 63;
-    const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (u >= n_users) return;
-    if (ovf_flag[u]) {
-        if (lane == 0) out_cnt[u] = -1;
-        return;
-    }
-    const int n = cand_cnt[u];
-    const float2 ce = ucut[u];
-    const float cs = ce.x == -INFINITY ? -INFINITY : ce.x * uinfo[u].z;  // exact power-of-two rescale
-    int c = 0;
-    for (int b0 = 0; b0 < n; b0 += WAVE) {
-        const int e = b0 + lane;
-        uint2 ent = make_uint2(0u, 0u);
-        if (e < n) ent = cand[(size_t)u * bandcap + e];
-        const bool kp = e < n && !(__uint_as_float(ent.x) < cs);
-        const unsigned long long bal = __ballot(kp);
-        if (kp) out_ent[(size_t)u * bandcap + c + __popcll(bal & ((1ull << lane) - 1ull))] = ent;
-        c += __popcll(bal);
-    }
-    if (lane == 0) out_cnt[u] = c;
-}
-
 // ------------------------------------ config-4 shard path without a select --
 // A catalog shard does not need its own k-th largest maximum: the global
 // bound G of the exchange is higher on most users, and the scan's own list
@@ -2237,17 +2288,6 @@ static inline int next_pow2(int x) {
 
 // scan variants: (DP, waves per workgroup, ring slots, user groups per wave,
 // register list length, waves per SIMD)
-// Two-pass screen (large catalogs, k * SCAN_SAMPLE <= 256): pass 1 runs the
-// list scan over every SCAN_SAMPLE-th tile without appends; its list bound
-// (a valid lower bound of the k-th half-block maximum: the sample's items
-// are real items) becomes pass 2's fixed threshold over the whole range
-// (ip_scan_fixed_kernel: no inserts, the MFMA-paced loop).  Appends ~ the
-// half-blocks above the sample's k-th maximum (~ k * SCAN_SAMPLE / 2 per lane
-// half), the select's theta_lb filter keeps ~ k * SCAN_SAMPLE (<= IP_SEL).
-#ifndef NRK_SCAN_SAMPLE
-#define NRK_SCAN_SAMPLE 8
-#endif
-constexpr int SCAN_SAMPLE = NRK_SCAN_SAMPLE;
 // ring slots of the UG = 4 scan (config 2): 4 (one more tile in flight
 // than round 3's 3) since the bookkeeping got cheaper -- bench context, one
 // box, three pairs: scan 5.77 vs 5.80-5.86 ms
@@ -2265,17 +2305,6 @@ constexpr int SCAN_NSL4 = NRK_SCAN_NSL4;
 #define NRK_SCAN_PRE_DIV 6
 #endif
 constexpr int SCAN_PRE_MAX = NRK_SCAN_PRE_MAX, SCAN_PRE_MIN = 128, SCAN_PRE_DIV = NRK_SCAN_PRE_DIV;
-// dev builds only (`make dev`): the default library is built without it
-#ifndef NRK_SCAN_TWO_PASS
-#define NRK_SCAN_TWO_PASS 0
-#endif
-constexpr bool SCAN_TWO_PASS = NRK_SCAN_TWO_PASS;  // under evaluation (round 4)
-static inline bool scan_two_pass(int k, int tb, int t_lo, int t_hi) {
-    const int mt = (k + 1) / 2;
-    const int per_lane = tb * ((t_hi - t_lo) / SCAN_SAMPLE);  // pass-1 half-blocks per lane
-    return SCAN_TWO_PASS && k * SCAN_SAMPLE <= 256 && per_lane >= 32 * mt;
-}
-
 template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false>
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
@@ -2284,22 +2313,13 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
     const int nblk = (n_items + 31) / 32;
     const int t_lo = w.blk_lo / TB, t_hi = (std::min(w.blk_hi, nblk) + TB - 1) / TB;
     const unsigned grid = (unsigned)((n_users + per_wg - 1) / per_wg);
-    if (scan_two_pass(k, TB, t_lo, t_hi)) {
-        ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP, false><<<grid, NW * 64, 0, s>>>(
-            users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, SCAN_SAMPLE);
-        constexpr int NW2 = 8, NSL2 = 3, UG2 = DP <= 64 ? 4 : 2, WPE2 = 2;
-        const int per_wg2 = NW2 * 32 * UG2;
-        ip_scan_fixed_kernel<DP, NW2, NSL2, UG2, WPE2><<<(n_users + per_wg2 - 1) / per_wg2, NW2 * 64, 0, s>>>(
-            users, n_users, cat, n_items, dim, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi);
-        return;
-    }
     // the list pre-pass: up to 64 tiles spread over the range (+2.2% MFMA at
     // config 2, +17% on a config-4 shard, whose appends it cuts by 2/3)
     const int n = t_hi - t_lo;
     const int n_pre = (IE == 1 && n >= SCAN_PRE_MIN) ? std::min(SCAN_PRE_MAX, n / SCAN_PRE_DIV) : 0;
     const int pstride = n_pre > 0 ? n / n_pre : 1;
     ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<grid, NW * 64, 0, s>>>(
-        users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, 1, n_pre, pstride);
+        users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, n_pre, pstride);
 }
 
 template <int DP, int MT>
@@ -2509,14 +2529,6 @@ static int screen_phases(const float* users, int64_t n_users, const void* catalo
     return NRK_OK;
 }
 
-int nrk_ip_topk_screen_range(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
-                             int dim, int k, int64_t blk_lo, int64_t blk_hi, void* workspace,
-                             size_t workspace_bytes, nrk_stream_t stream) {
-    clear_error();
-    return screen_phases(users, n_users, catalog, n_items, dim, k, blk_lo, blk_hi, workspace, workspace_bytes, stream,
-                         3);
-}
-
 int nrk_ip_topk_scan(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim, int k,
                      void* workspace, size_t workspace_bytes, nrk_stream_t stream) {
     clear_error();
@@ -2534,8 +2546,9 @@ int nrk_ip_topk_select(const float* users, int64_t n_users, const void* catalog,
 int nrk_ip_topk_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items,
                        int dim, int k, void* workspace, size_t workspace_bytes,
                        nrk_stream_t stream) {
-    return nrk_ip_topk_screen_range(users, n_users, catalog, n_items, dim, k, 0, n_blocks_of(n_items), workspace,
-                                    workspace_bytes, stream);
+    clear_error();
+    return screen_phases(users, n_users, catalog, n_items, dim, k, 0, n_blocks_of(n_items), workspace,
+                         workspace_bytes, stream, 3);
 }
 
 int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
@@ -2643,21 +2656,6 @@ int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, i
     return NRK_OK;
 }
 
-int nrk_ip_topk_band_pack(int64_t n_users, int64_t n_items, int dim, int k, const void* workspace,
-                          size_t workspace_bytes, void* out_ent, int32_t* out_cnt, nrk_stream_t stream) {
-    clear_error();
-    NRK_REQUIRE(n_users >= 0 && n_items >= 0 && dim > 0 && dim <= 256, "bad sizes");
-    NRK_REQUIRE(k >= 1 && k <= IP_KMAX, "k out of range");
-    if (n_users == 0) return NRK_OK;
-    NRK_REQUIRE(workspace && out_ent && out_cnt, "null pointer");
-    NRK_REQUIRE(workspace_bytes >= ip_ws_layout(nullptr, n_users, n_items, k, dim).bytes, "workspace too small");
-    const IpWs w = ip_ws_layout(const_cast<void*>(workspace), n_users, n_items, k, dim);
-    ip_band_pack_kernel<<<(int)((n_users + 3) / 4), 256, 0, as_stream(stream)>>>(
-        n_users, w.bandcap, w.cand, w.cnt, w.ucut, w.uinfo, w.ovf_flag, reinterpret_cast<uint2*>(out_ent), out_cnt);
-    NRK_CHECK_LAUNCH();
-    return NRK_OK;
-}
-
 int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* catalog, int64_t n_items, int dim,
                              int k, int64_t blk_lo, int64_t blk_hi, int m, float* out_bound, void* workspace,
                              size_t workspace_bytes, nrk_stream_t stream) {
@@ -2705,50 +2703,6 @@ int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, con
     return NRK_OK;
 }
 
-int nrk_ip_topk_band_cap(int k) { return k >= 1 && k <= IP_KMAX ? ip_bandcap(k) : 0; }
-
-int nrk_ip_topk_refine_csr(const float* users, int64_t n_users, const float* items, const void* catalog,
-                           int64_t n_items, int dim, int k, int64_t row_offset, const int64_t* band_off,
-                           const void* band, const float* ucut, const int32_t* ovf_in, float* out_scores,
-                           int32_t* out_rows, double* out_exact, void* workspace, size_t workspace_bytes,
-                           nrk_stream_t stream) {
-    clear_error();
-    int rc = ip_check(users, n_users, items, items, n_items, dim, k, workspace, workspace_bytes);
-    if (rc != NRK_OK || n_users == 0) return rc;
-    NRK_REQUIRE(out_scores && out_rows && band_off && ucut, "null pointer");
-    if (k > IP_KFAST) NRK_UNSUPPORTED("the band refine needs k <= 128 (larger k: exact path, ovf_in = 1)");
-    const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
-    hipStream_t s = as_stream(stream);
-    if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
-        set_error("nrk_ip_topk_refine_csr: hipMemsetAsync failed");
-        return NRK_EHIP;
-    }
-    ip_ovf_collect_kernel<<<(int)std::min<int64_t>((n_users + 255) / 256, 4096), 256, 0, s>>>(
-        n_users, ovf_in, w.ovf_flag, w.ovf_list, w.ovf_count);
-    const int g2 = (int)((n_users + 3) / 4);
-    const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
-    const uint2* bd = reinterpret_cast<const uint2*>(band);
-    const float2* uc = reinterpret_cast<const float2*>(ucut);
-#define NRK_REFINE(DS4, SV)                                                                                   \
-    ip_refine_kernel<DS4, SV><<<g2, 256, 0, s>>>(users, n_users, items, cat, n_items, dim, k, row_offset, bd, 0, \
-                                                 nullptr, uc, w.ovf_flag, w.ovf_list, w.ovf_count, out_scores,   \
-                                                 out_rows, out_exact, band_off)
-#define NRK_REFINE_SV(DS4)                 \
-    do {                                   \
-        if (k <= 64) NRK_REFINE(DS4, 128); \
-        else NRK_REFINE(DS4, 256);         \
-    } while (0)
-    if (dim == 32) NRK_REFINE_SV(8);
-    else if (dim == 16) NRK_REFINE_SV(4);
-    else if (dim == 64) NRK_REFINE_SV(16);
-    else NRK_REFINE_SV(0);
-#undef NRK_REFINE_SV
-#undef NRK_REFINE
-    if (n_items > 0) launch_exact(users, n_users, items, n_items, dim, k, row_offset, w, out_scores, out_rows, out_exact, s);
-    NRK_CHECK_LAUNCH();
-    return NRK_OK;
-}
-
 int nrk_ip_topk_refine_x(const float* users, int64_t n_users, const float* items, const void* catalog,
                          int64_t n_items, int dim, int k, int64_t row_offset, const void* band, int n_src,
                          int64_t src_users, int x_cap, const int32_t* src_cnt, const float* ucut,
@@ -2775,7 +2729,7 @@ int nrk_ip_topk_refine_x(const float* users, int64_t n_users, const float* items
 #define NRK_REFINE(DS4, SV)                                                                                   \
     ip_refine_kernel<DS4, SV><<<g2, 256, 0, s>>>(users, n_users, items, cat, n_items, dim, k, row_offset, bd, 0, \
                                                  nullptr, uc, w.ovf_flag, w.ovf_list, w.ovf_count, out_scores,   \
-                                                 out_rows, out_exact, nullptr, n_src, src_users, x_cap, src_cnt)
+                                                 out_rows, out_exact, n_src, src_users, x_cap, src_cnt)
 #define NRK_REFINE_SV(DS4)                 \
     do {                                   \
         if (k <= 64) NRK_REFINE(DS4, 128); \

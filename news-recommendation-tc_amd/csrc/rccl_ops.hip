@@ -24,6 +24,18 @@ namespace nrk {
         }                                                                                          \
     } while (0)
 
+// the same inside ncclGroupStart / ncclGroupEnd: a failing call ends the
+// group before returning, so the communicator takes the caller's next call
+#define NRK_RCCL_G(call)                                                                            \
+    do {                                                                                           \
+        const ncclResult_t r_ = (call);                                                            \
+        if (r_ != ncclSuccess) {                                                                   \
+            (void)ncclGroupEnd();                                                                  \
+            ::nrk::set_error(std::string(__func__) + ": " #call ": " + ncclGetErrorString(r_)); \
+            return NRK_EHIP;                                                                       \
+        }                                                                                          \
+    } while (0)
+
 }  // namespace nrk
 
 using namespace nrk;
@@ -80,8 +92,8 @@ int nrk_rccl_topk_allgather(void* comm, const double* in_exact, const int32_t* i
     hipStream_t s = as_stream(stream);
     const size_t per = (size_t)n_users * (size_t)k_in;
     NRK_RCCL(ncclGroupStart());
-    NRK_RCCL(ncclAllGather(in_exact, gather_exact, per, ncclFloat64, c, s));
-    NRK_RCCL(ncclAllGather(in_rows, gather_rows, per, ncclInt32, c, s));
+    NRK_RCCL_G(ncclAllGather(in_exact, gather_exact, per, ncclFloat64, c, s));
+    NRK_RCCL_G(ncclAllGather(in_rows, gather_rows, per, ncclInt32, c, s));
     NRK_RCCL(ncclGroupEnd());
     return nrk_topk_merge(gather_exact, gather_rows, n_ranks, (int64_t)per, n_users, k_in, k_out, out_scores,
                           out_rows, out_exact, stream);
@@ -120,10 +132,10 @@ int nrk_rccl_band_alltoall(void* comm, const int32_t* cnt, const int32_t* ids, i
     const size_t pe = (size_t)per * x_cap;
     NRK_RCCL(ncclGroupStart());
     for (int p = 0; p < n_ranks; ++p) {
-        NRK_RCCL(ncclSend(cnt + (size_t)p * per, (size_t)per, ncclInt32, p, c, s));
-        NRK_RCCL(ncclRecv(out_cnt + (size_t)p * per, (size_t)per, ncclInt32, p, c, s));
-        NRK_RCCL(ncclSend(ids + (size_t)p * pe, pe, ncclInt32, p, c, s));
-        NRK_RCCL(ncclRecv(out_ids + (size_t)p * pe, pe, ncclInt32, p, c, s));
+        NRK_RCCL_G(ncclSend(cnt + (size_t)p * per, (size_t)per, ncclInt32, p, c, s));
+        NRK_RCCL_G(ncclRecv(out_cnt + (size_t)p * per, (size_t)per, ncclInt32, p, c, s));
+        NRK_RCCL_G(ncclSend(ids + (size_t)p * pe, pe, ncclInt32, p, c, s));
+        NRK_RCCL_G(ncclRecv(out_ids + (size_t)p * pe, pe, ncclInt32, p, c, s));
     }
     NRK_RCCL(ncclGroupEnd());
     return NRK_OK;

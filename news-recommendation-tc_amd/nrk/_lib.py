@@ -38,9 +38,6 @@ SIGNATURES = {
     "nrk_ip_topk_bound": (INT, [P, I64, P, I64, INT, INT, INT, P, P, SZ, P]),
     "nrk_ip_topk_apply_bound": (INT, [I64, P, INT, INT, INT, P, SZ, P]),
     "nrk_topk_merge": (INT, [P, P, INT, I64, I64, INT, INT, P, P, P, P]),
-    "nrk_ip_topk_screen_range": (INT, [P, I64, P, I64, INT, INT, I64, I64, P, SZ, P]),
-    "nrk_ip_topk_band_cap": (INT, [INT]),
-    "nrk_ip_topk_band_pack": (INT, [I64, I64, INT, INT, P, SZ, P, P, P]),
     "nrk_ip_topk_scan": (INT, [P, I64, P, I64, INT, INT, P, SZ, P]),
     "nrk_rccl_unique_id_bytes": (INT, []),
     "nrk_rccl_get_unique_id": (INT, [P]),
@@ -54,7 +51,6 @@ SIGNATURES = {
     "nrk_ip_topk_shard_band": (INT, [I64, I64, INT, INT, P, INT, INT, INT, P, SZ, P, P, P]),
     "nrk_ip_topk_refine_x": (INT, [P, I64, P, P, I64, INT, INT, I64, P, INT, I64, INT, P, P, P, P, P, P, P, SZ,
                                    P]),
-    "nrk_ip_topk_refine_csr": (INT, [P, I64, P, P, I64, INT, INT, I64, P, P, P, P, P, P, P, P, SZ, P]),
     "nrk_row_normalize": (INT, [P, I64, INT, P, P, P]),
     "nrk_itemcf_pair_offsets": (INT, [P, I64, P, P]),
     "nrk_itemcf_workspace_bytes": (SZ, [I64, I32]),

@@ -248,31 +248,10 @@ def ip_topk_bound(users, catalog: Catalog, k: int, m: int, workspace):
     return out
 
 
-def ip_topk_screen_range(users, catalog: Catalog, k: int, blk_lo: int, blk_hi: int, workspace):
-    """ip_topk_screen over the 32-item blocks [blk_lo, blk_hi) of the catalog
-    only (a config-4 shard of the shared packed catalog; global ids)."""
-    _dev(users, workspace)
-    n = users.shape[0]
-    _lib.call("nrk_ip_topk_screen_range", _ptr(users), n, _ptr(catalog.packed), catalog.n, catalog.d, int(k),
-              int(blk_lo), int(blk_hi), _ptr(workspace), workspace.numel(), _stream())
-
-
 def ip_topk_tile_blocks(d: int) -> int:
     """32-item blocks per screen tile (shard ranges start on a tile)."""
     dp = 16 if d <= 16 else 32 if d <= 32 else 64 if d <= 64 else 128 if d <= 128 else 256
     return max(1, 8192 // (64 * dp))
-
-
-def ip_topk_band_pack(n_users, catalog: Catalog, k: int, workspace):
-    """Per user the band entries at or above its (raised) cut: (cnt int32 [n]
-    (-1 = overflowed -> exact path), ent int64 [n, cap] (8-B entries))."""
-    cap = _lib.lib().nrk_ip_topk_band_cap(int(k))
-    dev = workspace.device
-    cnt = torch.empty(n_users, dtype=torch.int32, device=dev)
-    ent = torch.empty((n_users, cap), dtype=torch.int64, device=dev)
-    _lib.call("nrk_ip_topk_band_pack", n_users, catalog.n, catalog.d, int(k), _ptr(workspace), workspace.numel(),
-              _ptr(ent), _ptr(cnt), _stream())
-    return cnt, ent
 
 
 def ip_topk_shard_screen(users, catalog: Catalog, k: int, blk_lo: int, blk_hi: int, m: int, workspace):
@@ -339,31 +318,6 @@ def ip_topk_refine_x(users, catalog: Catalog, k: int, src_cnt, src_ent, ucut, ov
 def ip_topk_ucut(workspace, n_users):
     """The per-user (cut, eps) float32 [n, 2] of a top-k workspace (ip_ws_layout: after the 256-B header)."""
     return workspace[256: 256 + 8 * n_users].view(torch.float32).view(n_users, 2)
-
-
-def ip_topk_refine_csr(users, catalog: Catalog, k: int, band_off, band, ucut, ovf=None, row_offset: int = 0,
-                       workspace=None):
-    """Exact top-k of ``users`` from a CSR of band entries (every shard's
-    entries for each user): the config-4 owner's refine.  Returns (scores
-    f32 [n, k], rows i32 [n, k], exact f64 [n, k])."""
-    _dev(users, band_off, band, ucut, ovf)
-    n = users.shape[0]
-    _need(band_off, torch.int64, (n + 1,), "band_off")
-    _need(band, torch.int64, name="band")
-    _need(ucut, torch.float32, (n, 2), "ucut")
-    if ovf is not None:
-        _need(ovf, torch.int32, (n,), "ovf")
-    dev = users.device
-    s = torch.empty((n, k), dtype=torch.float32, device=dev)
-    r = torch.empty((n, k), dtype=torch.int32, device=dev)
-    e = torch.empty((n, k), dtype=torch.float64, device=dev)
-    nb = _lib.lib().nrk_ip_topk_workspace_bytes(n, catalog.n, catalog.d, k)
-    if workspace is None or workspace.numel() < nb:
-        workspace = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
-    _lib.call("nrk_ip_topk_refine_csr", _ptr(users), n, _ptr(catalog.items), _ptr(catalog.packed), catalog.n,
-              catalog.d, int(k), int(row_offset), _ptr(band_off), _ptr(band), _ptr(ucut), _ptr(ovf), _ptr(s),
-              _ptr(r), _ptr(e), _ptr(workspace), workspace.numel(), _stream())
-    return s, r, e
 
 
 def ip_topk_apply_bound(bounds, k: int, workspace):

@@ -289,10 +289,42 @@ def test_full_size_topk_properties(ops):
     torch.cuda.synchronize()
     assert bool((r >= 0).all()) and bool((r < I).all())
     assert bool((e[:, :-1] >= e[:, 1:]).all())
+    # the bench's launch sequence: the screen as scan + select, then finish
+    ws = ops.ip_topk_workspace(U, cat, K, users.device)
+    s2 = torch.empty_like(s)
+    r2 = torch.empty_like(r)
+    ops.ip_topk_scan(users, cat, K, ws)
+    ops.ip_topk_select(users, cat, K, ws)
+    ops.ip_topk_finish(users, cat, K, ws, s2, r2)
+    assert torch.equal(r2, r) and torch.equal(s2, s)
     sample = np.sort(rng.choice(U, 256, replace=False))
     so, ro = oracle.ip_topk(users[sample].cpu().numpy(), items.cpu().numpy(), K, nthreads=8)
     assert np.array_equal(r[sample].cpu().numpy().astype(np.int64), ro)
     assert np.array_equal(s[sample].cpu().numpy(), so)
+
+
+def test_ip_topk_catalog_body_near_2gib(ops):
+    """A packed catalog body just under ip_check's 2 GiB limit (33,554,000
+    items x 32 dims = 2,147,457,024 B): the scan's ring prefetches run past
+    the last tile (main loop: 3 tiles; list pre-pass: 3 strides of 4,096
+    tiles), and their 32-bit DMA offsets must not wrap (a wrapped
+    offset read ~2 GB before the buffer).  Rows and scores bit-exact against
+    the oracle for 64 users."""
+    from nrk import _lib
+
+    I, D, U, K = 33_554_000, 32, 64, 31
+    body = -(-I // 32) * 64 * 32
+    assert body < 2**31 and _lib.lib().nrk_ip_catalog_bytes(I, D) > 2 * body
+    g = torch.Generator(device="cuda").manual_seed(5)
+    items = torch.nn.functional.normalize(torch.randn(I, D, device="cuda", generator=g), dim=1).contiguous()
+    users = torch.nn.functional.normalize(torch.randn(U, D, device="cuda", generator=g), dim=1).contiguous()
+    cat = ops.Catalog(items)
+    s, r = ops.ip_topk(users, cat, K)
+    torch.cuda.synchronize()
+    so, ro = oracle.ip_topk(users.cpu().numpy(), items.cpu().numpy(), K, nthreads=16)
+    del cat, items
+    assert np.array_equal(r.cpu().numpy(), ro)
+    assert np.array_equal(s.cpu().numpy(), so)
 
 
 @pytest.mark.parametrize("n_shards", [2, 3, 8])
@@ -331,12 +363,12 @@ def test_catalog_shards_merge_equals_single(ops, n_shards):
 
 
 @pytest.mark.parametrize("d,k", [(32, 31), (32, 10), (16, 31), (64, 21), (32, 32)])
-def test_two_pass_screen_vs_oracle(ops, d, k):
-    """Catalogs large enough for the two-pass screen (pass 1: list scan of
-    every 8th tile, no appends; pass 2: fixed threshold over every tile,
-    ip_topk.hip scan_two_pass): rows and scores bit-exact vs the oracle for
-    every user, incl. exact duplicate items across the sampled / unsampled
-    tiles, a zero user, a user equal to an item and near-tie scores."""
+def test_one_pass_screen_150k_stress_vs_oracle(ops, d, k):
+    """The one-pass screen (list pre-pass over sampled tiles, then every
+    tile) on a 150k-item catalog: rows and scores bit-exact vs the oracle for
+    every user, incl. exact duplicate items in a pre-pass tile and elsewhere,
+    a run of duplicates inside one tile, a zero user, a user equal to an item
+    and near-tie scores."""
     rng = np.random.default_rng(d * 100 + k)
     n_items = 150_000
     users = _unit(rng.standard_normal((512, d)))
