@@ -1014,6 +1014,10 @@ def main(argv=None):
                            "ip_scan_kernel (fp16 MFMA 32x32x16 screen), HIP events around its launch"),
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_flop_per_launch": flops,
+                # the same flops over the whole timed step (tower + scan + select + finish on
+                # one GPU; this rank's screen share over the slowest rank's step at N > 1):
+                # the roofline fraction ``value`` itself achieves
+                "step_frac": round(flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                 "busy": pmc_busy(["nrk::ip_scan_kernel", "nrk::ip_select_kernel", "nrk::ip_refine_kernel",
                                   "nrk::tt_user_kernel"], default_cfg),
                 "busy_source": "profiles/r04_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "

@@ -45,6 +45,7 @@ namespace nrk {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int IP_KFAST = 128;   // largest k on the screen path
 constexpr int IP_KMAX = 2048;   // largest k at all (exact path above IP_KFAST)
@@ -376,7 +377,8 @@ template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true
 __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
     int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
-    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int n_pre = 0, int pstride = 1) {
+    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int n_pre = 0, int pstride = 1,
+    float* __restrict__ bnd = nullptr, int bnd_m = 0) {
     constexpr bool APP = true;  // (the two-pass screen's append-free pass 1 is gone)
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
@@ -1086,6 +1088,55 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             if (h == 0) uinfo[user] = make_float4(live[g] ? lb : -INFINITY, eps_s[g], scl[g], eps_u[g]);
         }
     }
+    // Config-4 shard (bnd != nullptr): per user the bnd_m largest values of
+    // its two lanes' final lists as exact lower bounds v / scl - eps (rounded
+    // down to fp32, descending, -inf padded) -- each list value is a distinct
+    // half-block's fp16 maximum of this range, so each bounds a distinct
+    // item's exact score from below.  The pair's lists (descending, +inf
+    // placeholders in front) are merged in registers: A . reverse(B) is
+    // bitonic, log2(2 MT) half-cleaner stages sort it.  Replaces a pass over
+    // the appended maxima (ip_shard_bound_kernel).
+    if (bnd != nullptr) {
+        const int nl = jk + 1;  // real list values per lane
+#pragma unroll
+        for (int g = 0; g < UG; ++g) {
+            float c[2 * MT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                c[i] = t[g][i];
+                c[2 * MT - 1 - i] = partner32f(t[g][i], h);
+            }
+#pragma unroll
+            for (int d = MT; d >= 1; d >>= 1)
+#pragma unroll
+                for (int i = 0; i < 2 * MT; ++i)
+                    if ((i & d) == 0) {
+                        const float x = c[i], y = c[i + d];
+                        c[i] = fmaxf(x, y);
+                        c[i + d] = fminf(x, y);
+                    }
+            const int user = ubase + g * 32 + q;
+            if (h == 0 && user < n_users) {
+                float* o = bnd + (size_t)user * bnd_m;
+                const int p0 = 2 * (MT - nl);  // the placeholders sort to the front
+                const double inv = 1.0 / (double)scl[g];  // exact power of two
+#pragma unroll
+                for (int j = 0; j < 2 * MT; ++j) {
+                    const int r = j - p0;
+                    if (r >= 0 && r < bnd_m) {
+                        float v = -INFINITY;
+                        if (live[g] && c[j] != -INFINITY) {
+                            const double tv = (double)c[j] * inv - (double)eps_u[g];
+                            v = (float)tv;
+                            if ((double)v > tv) v = nextafterf(v, -INFINITY);
+                        }
+                        o[r] = v;
+                    }
+                }
+                for (int r = 2 * nl; r < bnd_m; ++r) o[r] = -INFINITY;  // fewer values than bnd_m
+            }
+        }
+    }
 }
 
 // ordered uint32 key of a float (monotone; -inf > 0, padding key 0 below all)
@@ -1621,6 +1672,241 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
     }
 }
 
+// ----------------------------------------------- refine by half-block --
+// The one-GPU finish for dims 16 / 32 / 64 (the half-block-major copy), as
+// five light launches instead of ip_refine_kernel's wave per user.  The
+// per-user refine gathers every band half-block (1 KB of fp16 at D = 32) for
+// each of the ~32 band entries of each user: 8 GB of L2 / Infinity-Cache
+// gathers per config-2 launch, although the catalog has only 23 MB of them.
+// Inverted, each half-block is read once per bucket of the users whose band
+// holds it (about 350 at config 2), and the per-pair traffic is the user's
+// fp32 row (128 B):
+//   hb_count   -- li = atomicAdd(cnt[hb]) per band entry (its place in the
+//                 half-block's bucket);
+//   hb_scan    -- bucket offsets (exclusive scan of cnt);
+//   hb_scatter -- bucket[off[hb] + li] = (user, hb): users grouped by half-block;
+//   hb_score   -- one wave per 64 bucket entries: per half-block segment, the
+//                 16 items' fp16 A fragment once and the users in groups of 16
+//                 as the B operand of v_mfma_f32_16x16x32_f16 (16 items x 16
+//                 users per MFMA; the same fp16 values and scale as the screen,
+//                 fp32 accumulation in any order stays within eps); an item
+//                 reaching the user's cut gets the exact fp64 score (the
+//                 oracle's sequential sum), kept at >= cut + eps, appended to
+//                 the user's survivor list (atomic count, SVB slots);
+//   hb_final   -- per user: the survivors sorted (score desc, row asc), the
+//                 top k written; zero users answered directly; more than SVB
+//                 survivors -> the exact path, as in ip_refine_kernel.
+// Rows and scores are the refine's bit for bit: the same candidate set (every
+// band item with fp16 score >= cut and exact score >= cut + eps), the same
+// exact sums and order.
+struct Surv {
+    double s;
+    int32_t row;
+    int32_t pad;
+};
+
+// thread per user: each band slot j < cand_cnt[u] takes a place in its
+// half-block's bucket
+__global__ __launch_bounds__(256) void ip_hb_count_kernel(int64_t n_users, int bandcap, const uint2* __restrict__ cand,
+                                                          const int32_t* __restrict__ cand_cnt,
+                                                          int32_t* __restrict__ hb_cnt, int32_t* __restrict__ li) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_users;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        const int n = cand_cnt[u];
+        const size_t f0 = (size_t)u * bandcap;
+        for (int j = 0; j < n; ++j) li[f0 + j] = atomicAdd(&hb_cnt[cand[f0 + j].y], 1);
+    }
+}
+
+// exclusive scan of n counts -> off[0..n] (one 1024-thread workgroup: each
+// thread sums a contiguous chunk, the chunk sums are scanned in LDS)
+__global__ __launch_bounds__(1024) void ip_hb_scan_kernel(const int32_t* __restrict__ cnt, int64_t n,
+                                                          int32_t* __restrict__ off) {
+    __shared__ int32_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (n + 1023) / 1024, lo = t * per, hi = lo + per < n ? lo + per : n;
+    int32_t sum = 0;
+    for (int64_t i = lo; i < hi; ++i) sum += cnt[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int32_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int32_t run = part[t] - sum;  // exclusive prefix of this chunk
+    for (int64_t i = lo; i < hi; ++i) {
+        off[i] = run;
+        run += cnt[i];
+    }
+    if (t == 1023) off[n] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void ip_hb_scatter_kernel(int64_t n_users, int bandcap,
+                                                            const uint2* __restrict__ cand,
+                                                            const int32_t* __restrict__ cand_cnt,
+                                                            const int32_t* __restrict__ hb_off,
+                                                            const int32_t* __restrict__ li,
+                                                            uint2* __restrict__ bucket) {
+    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_users;
+         u += (int64_t)gridDim.x * blockDim.x) {
+        const int n = cand_cnt[u];
+        const size_t f0 = (size_t)u * bandcap;
+        for (int j = 0; j < n; ++j) {
+            const uint32_t hb = cand[f0 + j].y;
+            bucket[hb_off[hb] + li[f0 + j]] = make_uint2((uint32_t)u, hb);
+        }
+    }
+}
+
+// DP = 16, 32 or 64 (dim == DP): KS k-steps of 32 dims
+template <int DP>
+__global__ __launch_bounds__(256) void ip_hb_score_kernel(
+    const float* __restrict__ users, const float* __restrict__ items, const uint8_t* __restrict__ catalog,
+    int64_t n_items, const uint2* __restrict__ bucket, const int32_t* __restrict__ hb_total,
+    const float2* __restrict__ ucut, const float4* __restrict__ uinfo, int32_t* __restrict__ scnt,
+    Surv* __restrict__ surv, int svb) {
+    constexpr int KS = DP <= 32 ? 1 : DP / 32;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwin = ((int64_t)*hb_total + 63) / 64, nw = (int64_t)gridDim.x * 4;
+    const int64_t nblk = (n_items + 31) >> 5;
+    const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk * 64 * DP);
+    const float inv_cs = 1.0f / hdr->scale;  // exact: a power of two
+    const uint8_t* hbc = catalog + catalog_hb_offset(n_items, DP);
+    const int64_t tot = *hb_total;
+    const int col = lane & 15, kq = lane >> 4;
+    for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < nwin; w += nw) {
+        const int64_t e = w * 64 + lane;
+        const uint2 be = e < tot ? bucket[e] : make_uint2(0u, 0xFFFFFFFFu);
+        uint64_t todo = __ballot(e < tot);
+        while (todo) {
+            // one half-block segment (the bucket is grouped by half-block)
+            const int s0 = __ffsll((long long)todo) - 1;
+            const uint32_t hb = (uint32_t)__shfl((int)be.y, s0, WAVE);
+            const uint64_t seg = __ballot(be.y == hb) & todo;
+            todo &= ~seg;
+            const int nseg = __popcll(seg);
+            // A: item (lane & 15) of the half-block, dims 32 ks + 8 kq + [0, 8)
+            f16x8 afr[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int d0 = 32 * ks + 8 * kq;
+                if (d0 < DP)
+                    afr[ks] = __builtin_bit_cast(
+                        f16x8, *reinterpret_cast<const uint4*>(hbc + ((size_t)hb * 16 + col) * (2 * DP) + 2 * d0));
+                else
+                    afr[ks] = f16x8{};
+            }
+            // the lane's 4 items: rows 4 kq + i of the half-block
+            int32_t irow[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                irow[i] = (int32_t)((int64_t)(hb >> 1) * 32 + i + 8 * kq + 4 * (hb & 1));
+            for (int g0 = 0; g0 < nseg; g0 += 16) {
+                const int m = g0 + col;  // this lane's user: the segment's m-th entry
+                const bool vu = m < nseg;
+                const int src = vu ? s0 + m : s0;
+                const uint32_t u = (uint32_t)__shfl((int)be.x, src, WAVE);
+                const float* ur = users + (size_t)u * DP;
+                const float4 inf = uinfo[u];
+                const float2 cu = ucut[u];
+                const float su = inf.z * inv_cs;  // the screen's user scale (exact)
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const int d0 = 32 * ks + 8 * kq;
+                    f16x8 bfr = f16x8{};
+                    if (d0 < DP) {
+                        const float4 x0 = *reinterpret_cast<const float4*>(ur + d0);
+                        const float4 x1 = *reinterpret_cast<const float4*>(ur + d0 + 4);
+                        bfr[0] = (_Float16)(x0.x * su); bfr[1] = (_Float16)(x0.y * su);
+                        bfr[2] = (_Float16)(x0.z * su); bfr[3] = (_Float16)(x0.w * su);
+                        bfr[4] = (_Float16)(x1.x * su); bfr[5] = (_Float16)(x1.y * su);
+                        bfr[6] = (_Float16)(x1.z * su); bfr[7] = (_Float16)(x1.w * su);
+                    }
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(afr[ks], bfr, acc, 0, 0, 0);
+                }
+                const float pcut = cu.x * inf.z;  // the cut in the screen's scaled units (exact)
+                double thr = -INFINITY;
+                if (cu.x != -INFINITY) {
+                    thr = (double)cu.x + (double)cu.y;
+                    thr = thr - fabs(thr) * 1e-15 - 1e-300;  // round down (ip_refine_kernel's cut + eps)
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (vu && irow[i] < n_items && acc[i] >= pcut) {
+                        const double sd = exact_dot(ur, items + (int64_t)irow[i] * DP, DP);
+                        if (sd >= thr) {
+                            const int p = atomicAdd(&scnt[u], 1);
+                            if (p < svb) surv[(size_t)u * svb + p] = Surv{sd, irow[i], 0};
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// per user (persistent waves): sort the survivors, write the top k
+template <int SE>
+__global__ __launch_bounds__(256) void ip_hb_final_kernel(
+    const float* __restrict__ users, int64_t n_users, int64_t n_items, int dim, int k, int64_t row_offset,
+    const int32_t* __restrict__ ovf_flag, const int32_t* __restrict__ scnt, const Surv* __restrict__ surv,
+    int32_t* __restrict__ ovf_list, int32_t* __restrict__ ovf_count, float* __restrict__ out_s,
+    int32_t* __restrict__ out_r, double* __restrict__ out_e) {
+    constexpr int SV = SE * WAVE;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < n_users; u += nw) {
+        const int ov = ovf_flag[u];
+        const int cnt = scnt[u];
+        const float* uv = users + u * dim;
+        const float ul = lane < dim ? uv[lane] : 0.0f;
+        if (ov) continue;  // in ovf_list already: the exact path
+        float nz = fabsf(ul);
+        for (int d = lane + WAVE; d < dim; d += WAVE) nz += fabsf(uv[d]);
+        nz = wave_sum_f32(nz);
+        if (nz == 0.0f) {  // zero user: every score is exactly 0 -> the lowest rows
+            for (int i = lane; i < k; i += WAVE) {
+                const bool ok = i < n_items;
+                out_s[u * k + i] = ok ? 0.0f : -FLT_MAX;
+                out_r[u * k + i] = ok ? (int32_t)(i + row_offset) : -1;
+                if (out_e) out_e[u * k + i] = ok ? 0.0 : -INFINITY;
+            }
+            continue;
+        }
+        if (cnt > SV) {  // dense exact ties: the exact fallback
+            if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
+            continue;
+        }
+        Cand x[SE];
+#pragma unroll
+        for (int e = 0; e < SE; ++e) {
+            const int idx = e * 64 + lane;
+            if (idx < cnt) {
+                const Surv sv = surv[(size_t)u * SV + idx];
+                x[e].s = sv.s;
+                x[e].row = sv.row;
+            } else {
+                x[e].s = -INFINITY;
+                x[e].row = INT32_MAX;
+            }
+        }
+        wave_bitonic_sort<SE>(x);
+#pragma unroll
+        for (int e = 0; e < SE; ++e) {
+            const int idx = e * 64 + lane;
+            if (idx < k) {
+                const bool ok = x[e].row != INT32_MAX;
+                out_s[u * k + idx] = ok ? (float)x[e].s : -FLT_MAX;
+                out_r[u * k + idx] = ok ? (int32_t)(x[e].row + row_offset) : -1;
+                if (out_e) out_e[u * k + idx] = ok ? x[e].s : -INFINITY;
+            }
+        }
+    }
+}
+
 // -------------------------------------------------------------- fallback --
 __device__ __forceinline__ uint64_t okey(double s) {
     const uint64_t b = (uint64_t)__double_as_longlong(s);
@@ -2118,11 +2404,14 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
     int2 ac_n = make_int2(0, 0);
     float4 inf_n = make_float4(0.f, 0.f, 0.f, 0.f);
     int ov_n = 0, pc_n = 0;
+    // ovf_flag / pre == nullptr (the bounds came from the scan's lists): no
+    // pre-band, the whole append list; overflowed lists -> the exact path
+    auto ovf_of = [&](int64_t v, int2 ac) { return ovf_flag ? ovf_flag[v] : (ac.x > m2 || ac.y > m2) ? 1 : 0; };
     if (u < n_users) {
         ac_n = reinterpret_cast<const int2*>(acnt)[u];
         inf_n = uinfo[u];
-        ov_n = ovf_flag[u];
-        pc_n = pre_cnt[u];
+        ov_n = ovf_of(u, ac_n);
+        pc_n = pre ? pre_cnt[u] : -1;
     }
     for (; u < n_users; u += nw) {
         const int ov = ov_n, pc = pc_n;
@@ -2134,8 +2423,8 @@ __global__ __launch_bounds__(256) void ip_shard_band_kernel(int64_t n_users, int
         if (u + nw < n_users) {
             ac_n = reinterpret_cast<const int2*>(acnt)[u + nw];
             inf_n = uinfo[u + nw];
-            ov_n = ovf_flag[u + nw];
-            pc_n = pre_cnt[u + nw];
+            ov_n = ovf_of(u + nw, ac_n);
+            pc_n = pre ? pre_cnt[u + nw] : -1;
         }
         if (ov || inf.z <= 0.0f) {
             if (lane == 0) {
@@ -2212,6 +2501,19 @@ struct IpWs {
     int32_t* slow_list;  // exact path: users with too many fp32 ties (count at ovf_count[1])
     int bandcap, m2;
     int blk_lo, blk_hi;  // block range screened (config-4 shards), set by the caller
+    float* bnd = nullptr;  // config-4 shard: the scan's per-user bounds (ip_scan_kernel's bnd)
+    int bnd_m = 0;
+    // refine by half-block (screen path, k <= IP_KFAST): bucket counts /
+    // offsets per half-block, each band slot's place in its bucket, the
+    // buckets, and per user the survivor count and list (svb slots)
+    int32_t* hb_cnt = nullptr;
+    int32_t* hb_off = nullptr;
+    int32_t* hb_li = nullptr;
+    uint2* hb_bucket = nullptr;
+    int32_t* scnt = nullptr;
+    Surv* surv = nullptr;
+    int64_t n_hb = 0;
+    int svb = 0;
     size_t bytes;
 };
 
@@ -2276,6 +2578,22 @@ static IpWs ip_ws_layout(void* base, int64_t n_users, int64_t n_items, int k, in
     off += align256((size_t)std::min<int64_t>(n_users, FB_GRID) * (size_t)n_items * sizeof(uint32_t));
     w.slow_list = reinterpret_cast<int32_t*>(p + off);
     off += align256((size_t)n_users * sizeof(int32_t));
+    if (k <= IP_KFAST) {
+        w.n_hb = 2 * n_blocks_of(n_items);
+        w.svb = k <= 64 ? 128 : 256;  // ip_refine_kernel's SV
+        w.hb_cnt = reinterpret_cast<int32_t*>(p + off);
+        off += align256((size_t)(w.n_hb + 1) * sizeof(int32_t));
+        w.hb_off = reinterpret_cast<int32_t*>(p + off);
+        off += align256((size_t)(w.n_hb + 1) * sizeof(int32_t));
+        w.hb_li = reinterpret_cast<int32_t*>(p + off);
+        off += align256((size_t)n_users * w.bandcap * sizeof(int32_t));
+        w.hb_bucket = reinterpret_cast<uint2*>(p + off);
+        off += align256((size_t)n_users * w.bandcap * sizeof(uint2));
+        w.scnt = reinterpret_cast<int32_t*>(p + off);
+        off += align256((size_t)n_users * sizeof(int32_t));
+        w.surv = reinterpret_cast<Surv*>(p + off);
+        off += align256((size_t)n_users * w.svb * sizeof(Surv));
+    }
     w.bytes = off;
     return w;
 }
@@ -2319,7 +2637,8 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
     const int n_pre = (IE == 1 && n >= SCAN_PRE_MIN) ? std::min(SCAN_PRE_MAX, n / SCAN_PRE_DIV) : 0;
     const int pstride = n_pre > 0 ? n / n_pre : 1;
     ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<grid, NW * 64, 0, s>>>(
-        users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, n_pre, pstride);
+        users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, n_pre, pstride, w.bnd,
+        w.bnd_m);
 }
 
 template <int DP, int MT>
@@ -2377,6 +2696,18 @@ static int ip_range(IpWs& w, int64_t n_items, int dim, int64_t blk_lo, int64_t b
     w.blk_hi = (int)blk_hi;
     return NRK_OK;
 }
+
+// config-4 shard bounds from the scan's register lists (ip_scan_kernel's
+// epilogue) instead of a pass over the appended maxima (ip_shard_bound_kernel)
+#ifndef NRK_SHARD_LISTBOUND
+#define NRK_SHARD_LISTBOUND 1
+#endif
+constexpr bool SHARD_LISTBOUND = NRK_SHARD_LISTBOUND;
+// the one-GPU finish by half-block buckets (ip_hb_*) instead of ip_refine_kernel
+#ifndef NRK_HB_REFINE
+#define NRK_HB_REFINE 1
+#endif
+constexpr bool HB_REFINE = NRK_HB_REFINE;
 
 // persistent grid of the shard kernels: SH_WG_PER_CU 4-wave workgroups per CU
 static int sh_grid(int64_t n_users) {
@@ -2573,7 +2904,34 @@ int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
         if (k <= 64) NRK_REFINE(DS4, 128);          \
         else NRK_REFINE(DS4, 256);                  \
     } while (0)
-    if (k <= IP_KFAST || n_items == 0) {
+    const bool by_hb = HB_REFINE && k <= IP_KFAST && n_items > 0 && catalog != nullptr &&
+                       (dim == 16 || dim == 32 || dim == 64);
+    if (by_hb) {
+        if (hipMemsetAsync(w.hb_cnt, 0, (size_t)(w.n_hb + 1) * sizeof(int32_t), s) != hipSuccess ||
+            hipMemsetAsync(w.scnt, 0, (size_t)n_users * sizeof(int32_t), s) != hipSuccess) {
+            set_error("nrk_ip_topk_finish: hipMemsetAsync failed");
+            return NRK_EHIP;
+        }
+        const int gs = (int)std::min<int64_t>((n_users + 255) / 256, 16384);
+        ip_hb_count_kernel<<<gs, 256, 0, s>>>(n_users, w.bandcap, w.cand, w.cnt, w.hb_cnt, w.hb_li);
+        ip_hb_scan_kernel<<<1, 1024, 0, s>>>(w.hb_cnt, w.n_hb, w.hb_off);
+        ip_hb_scatter_kernel<<<gs, 256, 0, s>>>(n_users, w.bandcap, w.cand, w.cnt, w.hb_off, w.hb_li, w.hb_bucket);
+        const int gsc = sh_grid(n_users * 8);  // persistent 4-wave workgroups over the 64-entry windows
+#define NRK_HB_SCORE(DP)                                                                                      \
+    ip_hb_score_kernel<DP><<<gsc, 256, 0, s>>>(users, items, cat, n_items, w.hb_bucket, w.hb_off + w.n_hb, w.ucut, \
+                                               w.uinfo, w.scnt, w.surv, w.svb)
+        if (dim == 32) NRK_HB_SCORE(32);
+        else if (dim == 16) NRK_HB_SCORE(16);
+        else NRK_HB_SCORE(64);
+#undef NRK_HB_SCORE
+        const int gf = sh_grid(n_users);
+        if (w.svb == 128)
+            ip_hb_final_kernel<2><<<gf, 256, 0, s>>>(users, n_users, n_items, dim, k, row_offset, w.ovf_flag, w.scnt,
+                                                    w.surv, w.ovf_list, w.ovf_count, out_scores, out_rows, out_exact);
+        else
+            ip_hb_final_kernel<4><<<gf, 256, 0, s>>>(users, n_users, n_items, dim, k, row_offset, w.ovf_flag, w.scnt,
+                                                    w.surv, w.ovf_list, w.ovf_count, out_scores, out_rows, out_exact);
+    } else if (k <= IP_KFAST || n_items == 0) {
         if (dim == 32) NRK_REFINE_SV(8);
         else if (dim == 16) NRK_REFINE_SV(4);
         else if (dim == 64) NRK_REFINE_SV(16);
@@ -2671,14 +3029,27 @@ int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* ca
     rc = ip_range(w, n_items, dim, blk_lo, blk_hi);
     if (rc != NRK_OK) return rc;
     hipStream_t s = as_stream(stream);
+    if (SHARD_LISTBOUND) {
+        // the bounds come from the scan's own lists (its epilogue); an empty
+        // range has none
+        w.bnd = out_bound;
+        w.bnd_m = m;
+    }
     if (blk_lo == blk_hi || n_items == 0) {
         ip_empty_range_kernel<<<(int)std::min<int64_t>((n_users + 255) / 256, 4096), 256, 0, s>>>(n_users, w.acnt,
                                                                                                w.uinfo);
+        if (SHARD_LISTBOUND &&
+            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(out_bound), 0xFF800000u /* -inf */,
+                              (size_t)n_users * m, s) != hipSuccess) {
+            set_error("nrk_ip_topk_shard_screen: hipMemsetD32Async failed");
+            return NRK_EHIP;
+        }
     } else {
         scan_dispatch(users, (int)n_users, reinterpret_cast<const uint8_t*>(catalog), (int)n_items, dim, k, w, s);
     }
-    ip_shard_bound_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, w.m2, w.app, w.acnt, w.uinfo, m, out_bound,
-                                                           w.ovf_flag, w.bandcap, w.cand, w.cnt);
+    if (!SHARD_LISTBOUND)
+        ip_shard_bound_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, w.m2, w.app, w.acnt, w.uinfo, m, out_bound,
+                                                               w.ovf_flag, w.bandcap, w.cand, w.cnt);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
@@ -2698,7 +3069,8 @@ int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, con
     const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
     ip_shard_band_kernel<<<sh_grid(n_users), 256, 0, as_stream(stream)>>>(
         n_users, k, w.m2, w.app, w.acnt, w.uinfo, bounds, bounds ? n_lists : 0, bounds ? m : 1, w.bandcap,
-        w.ovf_flag, w.cand, w.cnt, w.ucut, reinterpret_cast<uint32_t*>(out_ent), out_cnt, x_cap);
+        SHARD_LISTBOUND ? nullptr : w.ovf_flag, SHARD_LISTBOUND ? nullptr : w.cand,
+        SHARD_LISTBOUND ? nullptr : w.cnt, w.ucut, reinterpret_cast<uint32_t*>(out_ent), out_cnt, x_cap);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }

@@ -407,9 +407,15 @@ class DinParams:
         starts = np.cumsum([0] + [pc.shape[0] for pc in pieces[:-1]]).astype(np.int64)
         fb = list(starts[:Fu + Fi]) + list(starts[Fu + Fi + (1 if kni > niv else 0):])  # per caller feature
         zero_row = int(starts[Fu + Fi]) if kni > niv else 0
-        base = ([fb[f] for f in range(Fu) for _ in range(m)]
-                + [fb[Fu + f] for f in range(Fi) for _ in range(m)] + [zero_row] * (kni - niv)
-                + [fb[Fu + Fi + f] for f in range(Fc) for _ in range(m)])
+        # virtual feature (f, hh) of a caller feature f: row fb[f] + hh + m i for caller
+        # index i -- base fb[f] + hh, virtual index m i -- so caller index 0 (the
+        # collate's padding) stays virtual index 0 in every half, which is what the
+        # position-major plan's padding test (mask 0, every index 0) and its pad row
+        # (row 0 of each feature) assume (with index m i + hh no padding
+        # row of a D > 32 model was ever recognised)
+        base = ([fb[f] + hh for f in range(Fu) for hh in range(m)]
+                + [fb[Fu + f] + hh for f in range(Fi) for hh in range(m)] + [zero_row] * (kni - niv)
+                + [fb[Fu + Fi + f] + hh for f in range(Fc) for hh in range(m)])
         table = torch.from_numpy(np.concatenate(pieces, 0))
         _finite(table, "DIN embedding tables")
         if table_dtype == "bf16":
@@ -426,7 +432,7 @@ class DinParams:
         def idx_map(F, pad_to):
             src = [f for f in range(F) for _ in range(m)] + [-1] * (pad_to - m * F)
             mul = [m] * (m * F) + [0] * (pad_to - m * F)
-            add = [h for _ in range(F) for h in range(m)] + [0] * (pad_to - m * F)
+            add = [0] * pad_to
             return torch.tensor([src, mul, add], dtype=torch.int32).to(device).contiguous()
 
         self.map_user = None if m == 1 else idx_map(Fu, m * Fu)

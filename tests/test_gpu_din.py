@@ -130,6 +130,7 @@ def test_din_vs_oracle(B, T, n_item, n_ctx, h1, h2, table_dtype):
         (16, 4, 50, 700, "bf16"),   # din_embedding_dim 16: tables zero-padded to 32
         (16, 3, 30, 300, "fp32"),   # 3 item features -> padded to 4 with the zero row
         (64, 4, 50, 700, "bf16"),   # 64 = two 32-wide virtual features each -> 8 item features
+        (64, 2, 50, 700, "bf16"),   # 2 x 2 = 4 virtual item features: the position-major path with padding rows
         (64, 2, 70, 257, "fp32"),   # T > 64 (general path) at 4 virtual item features
         (8, 1, 20, 129, "bf16"),    # tiny width, one item feature
         (48, 3, 50, 200, "bf16"),   # 48 -> 64 padded, 2 x 3 = 6 -> 8 item features
@@ -150,6 +151,35 @@ def test_din_embedding_dims_vs_oracle(dim, n_item, T, B, table_dtype):
                                    round_bf16=table_dtype == "bf16")
     np.testing.assert_allclose(probs, po, atol=TOL, rtol=0)
     np.testing.assert_allclose(lg, lo, atol=TOL, rtol=TOL)
+
+
+@pytest.mark.parametrize("dim,n_item", [(64, 2), (64, 1), (128, 1), (16, 3)])
+def test_din_virtual_indices_keep_padding_zero(dim, n_item):
+    """ops.DinParams' virtual-feature layout keeps the collate's padding (caller
+    index 0) at virtual index 0 in every 32-wide half, so the position-major
+    plan recognises padding rows (mask 0, every index 0) at any embedding width
+    (ADVICE r4), and every other caller index i of feature f addresses the rows
+    fb[f] + hh + m i of its halves."""
+    from nrk import ops
+
+    rng = np.random.default_rng(dim + n_item)
+    vu, vi, vc = [50, 300], [60, 900, 5000][:n_item], [12] * 2
+    sd, feats = synth_model(rng, vu, vi, vc, dim=dim)
+    p = ops.DinParams(sd, *feats, table_dtype="bf16", device="cuda")
+    b = synth_batch(rng, 64, 20, vu, vi, vc, p_empty=0.3)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v, np.int32)).cuda() for k, v in b.items() if k != "mask"}
+    _, _, hist, _ = p.kernel_indices(t["user"], t["item"], t["hist"], t["ctx"])
+    hist = hist.cpu().numpy()
+    pad = b["mask"] == 0
+    assert pad.any() and (hist[pad] == 0).all()
+    m = max(1, -(-dim // 32))
+    table = p.table.float().cpu().numpy()
+    rb = p.row_base.cpu().numpy()
+    emb = sd[f"item_embedding_dict.{feats[1][0]}.weight"]
+    r, tt = np.argwhere(~pad)[0]
+    i0 = int(b["hist"][r, tt, 0])
+    row = np.concatenate([table[rb[p.kn_user + hh] + hist[r, tt, hh]] for hh in range(m)])[:dim]
+    np.testing.assert_allclose(row, emb[i0], atol=1e-2)  # bf16 table
 
 
 def test_din_all_history_masked():
