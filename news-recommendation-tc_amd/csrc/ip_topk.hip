@@ -2578,7 +2578,7 @@ static IpWs ip_ws_layout(void* base, int64_t n_users, int64_t n_items, int k, in
     off += align256((size_t)std::min<int64_t>(n_users, FB_GRID) * (size_t)n_items * sizeof(uint32_t));
     w.slow_list = reinterpret_cast<int32_t*>(p + off);
     off += align256((size_t)n_users * sizeof(int32_t));
-    if (k <= IP_KFAST) {
+    if (k <= IP_KFAST && (dim == 16 || dim == 32 || dim == 64)) {  // nrk_ip_topk_finish's by_hb dims
         w.n_hb = 2 * n_blocks_of(n_items);
         w.svb = k <= 64 ? 128 : 256;  // ip_refine_kernel's SV
         w.hb_cnt = reinterpret_cast<int32_t*>(p + off);
