@@ -460,6 +460,7 @@ def run_fused(args, device, rank, world, dist):
 
     U = args.fused_users or (10_000_000 // world)
     I, D, T, k = args.fused_items, 128, 50, 30
+    chunk = min(args.fused_chunk, -(-U // 2048) * 2048)  # users per assemble -> DIN call (chunk * k % 4096 == 0)
     g = torch.Generator(device=device).manual_seed(1000 + rank)
     gi = torch.Generator(device=device).manual_seed(999)  # the catalog is the same on every rank
     items = torch.nn.functional.normalize(torch.randn(I, D, device=device, generator=gi), dim=1).contiguous()
@@ -476,7 +477,7 @@ def run_fused(args, device, rank, world, dist):
     if not args.fused_hash_ctx:
         ctx = fused_ctx_tables(users, items, user_hist, hist_len, device, gi, g)
     if ctx is None:
-        fused = FusedRecallRank(cat, p, user_feat, item_feat, user_hist, hist_len, k=k)
+        fused = FusedRecallRank(cat, p, user_feat, item_feat, user_hist, hist_len, k=k, chunk_users=chunk)
     else:
         # fit the binning + label codes on the first chunk's raw features
         # (the reference fits on its whole main_df, offline; untimed here)
@@ -494,7 +495,8 @@ def run_fused(args, device, rank, world, dist):
         cols = {f: (rawn[:, j] if f == "score" else rawn[:, j].astype(np.float32)) for j, f in enumerate(names)}
         cols["recall_in_user_cat"] = rawn[:, -1].astype(np.int8)
         spec = CtxSpec.fit(cols, names)
-        fused = FusedRecallRank(cat, p, user_feat, item_feat, user_hist, hist_len, k=k, ctx=(ctx[0], spec))
+        fused = FusedRecallRank(cat, p, user_feat, item_feat, user_hist, hist_len, k=k, ctx=(ctx[0], spec),
+                                chunk_users=chunk)
     probs = torch.empty(U * k, dtype=torch.float32, device=device)
 
     def step(ev=None):
@@ -842,6 +844,8 @@ def main(argv=None):
                     help="BASELINE config 5 instead: fused recall -> DIN, 10M users / N per rank x 5M items, D=128")
     ap.add_argument("--fused-users", type=int, default=0, help="users per rank for --fused (default 10M / N)")
     ap.add_argument("--fused-items", type=int, default=5_000_000)
+    ap.add_argument("--fused-chunk", type=int, default=32768,
+                    help="config 5: users per assemble / context / DIN call (a multiple of 2048: whole Dice batches)")
     ap.add_argument("--fused-hash-ctx", action="store_true",
                     help="config 5 with the synthetic hash-bin context instead of the real context features")
     ap.add_argument("--shard", choices=["users", "catalog"], default="catalog",

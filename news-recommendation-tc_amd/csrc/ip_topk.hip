@@ -307,12 +307,12 @@ constexpr bool SCAN_APP_ASM = NRK_SCAN_APP_ASM, SCAN_INS_BR = NRK_SCAN_INS_BR, S
 #define NRK_SCAN_LDSAPP 0
 #endif
 // SWP -- the tile's MFMAs software-pipelined against the half-block max
-// reductions (see tile())
+// reductions (see tile()); the value is the lag in (block, group) steps
 #ifndef NRK_SCAN_SWP
 #define NRK_SCAN_SWP 0
 #endif
-constexpr bool SCAN_LAZY = NRK_SCAN_LAZY, SCAN_BSEL = NRK_SCAN_BSEL, SCAN_LDSAPP = NRK_SCAN_LDSAPP,
-               SCAN_SWP = NRK_SCAN_SWP;
+constexpr bool SCAN_LAZY = NRK_SCAN_LAZY, SCAN_BSEL = NRK_SCAN_BSEL, SCAN_LDSAPP = NRK_SCAN_LDSAPP;
+constexpr int SCAN_SWP = NRK_SCAN_SWP;
 
 // (lane bit of m) ? T : F, one v_cndmask_b32 on the compare's SGPR lane mask
 // with inline constants (0..64); sel_mask_v: (lane bit of m) ? T : f
@@ -662,7 +662,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                 const float m4 = m3(x[9], x[10], x[11]), m5 = m3(x[12], x[13], x[14]);
                 mx[gg][bb] = fmaxf(m3(m0, m1, m2), m3(m4, m5, x[15]));
             };
-            f32x16 acc0, acc1;
+            // LAG = SCAN_SWP: step j reduces step j - LAG (LAG + 1 accumulator
+            // sets; LAG = 2 gives the reduced step's last MFMA a whole step to
+            // land before its first reduction VALU reads it)
+            constexpr int LAG = SCAN_SWP, NACC = LAG + 1, NSTEP = TB * UG;
+            f32x16 acc[NACC];
             u32x4 afb[DS];
             static_for<TB>([&](auto bc) {
                 constexpr int b = decltype(bc)::value;
@@ -681,27 +685,31 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                 }
                 static_for<UG>([&](auto gc) {
                     constexpr int g = decltype(gc)::value, j = b * UG + g;
-                    f32x16& A = (j & 1) ? acc1 : acc0;
-                    const f32x16& P = (j & 1) ? acc0 : acc1;
+                    f32x16& A = acc[j % NACC];
                     A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[0]), ufrag[g][0],
                                                                f32x16{}, 0, 0, 0);
 #pragma unroll
                     for (int s = 1; s < DS; ++s)
                         A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[s]), ufrag[g][s], A,
                                                                    0, 0, 0);
-                    if constexpr (j > 0) red(P, (j - 1) / UG, (j - 1) % UG);
+                    if constexpr (j >= LAG) red(acc[(j - LAG) % NACC], (j - LAG) / UG, (j - LAG) % UG);
                     // the order the scheduler must keep: each MFMA of step j
-                    // followed by its share of step j - 1's 8 reduction VALU
+                    // followed by its share of step j - LAG's 8 reduction VALU
                     if constexpr (!MASK) {
 #pragma unroll
                         for (int s = 0; s < DS; ++s) {
                             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                            if (j > 0) __builtin_amdgcn_sched_group_barrier(0x002, (8 + DS - 1) / DS, 0);
+                            if (j >= LAG) __builtin_amdgcn_sched_group_barrier(0x002, (8 + DS - 1) / DS, 0);
                         }
+                        // a fence per step: step j - LAG's reduction stays beside step j's MFMAs
+                        if constexpr (LAG > 1) __builtin_amdgcn_sched_barrier(0);
                     }
                 });
             });
-            red(((TB * UG - 1) & 1) ? acc1 : acc0, TB - 1, UG - 1);
+            static_for<LAG>([&](auto lc) {
+                constexpr int j = NSTEP - LAG + decltype(lc)::value;
+                red(acc[j % NACC], j / UG, j % UG);
+            });
             return;
         }
 #pragma unroll
@@ -1095,8 +1103,10 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     // item's exact score from below.  The pair's lists (descending, +inf
     // placeholders in front) are merged in registers: A . reverse(B) is
     // bitonic, log2(2 MT) half-cleaner stages sort it.  Replaces a pass over
-    // the appended maxima (ip_shard_bound_kernel).
-    if (bnd != nullptr) {
+    // the appended maxima (ip_shard_bound_kernel).  Lists of up to 32 (k <=
+    // 64; longer ones would spill the merge -- those shards keep the pass).
+    if constexpr (MT > 32) {
+    } else if (bnd != nullptr) {
         const int nl = jk + 1;  // real list values per lane
 #pragma unroll
         for (int g = 0; g < UG; ++g) {
@@ -2703,6 +2713,8 @@ static int ip_range(IpWs& w, int64_t n_items, int dim, int64_t blk_lo, int64_t b
 #define NRK_SHARD_LISTBOUND 1
 #endif
 constexpr bool SHARD_LISTBOUND = NRK_SHARD_LISTBOUND;
+// the scan's epilogue merges lists of up to 32 per lane (k <= 64)
+static inline bool shard_listbound(int k) { return SHARD_LISTBOUND && (k + 1) / 2 <= 32; }
 // the one-GPU finish by half-block buckets (ip_hb_*) instead of ip_refine_kernel
 #ifndef NRK_HB_REFINE
 #define NRK_HB_REFINE 1
@@ -3029,7 +3041,8 @@ int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* ca
     rc = ip_range(w, n_items, dim, blk_lo, blk_hi);
     if (rc != NRK_OK) return rc;
     hipStream_t s = as_stream(stream);
-    if (SHARD_LISTBOUND) {
+    const bool lbnd = shard_listbound(k);
+    if (lbnd) {
         // the bounds come from the scan's own lists (its epilogue); an empty
         // range has none
         w.bnd = out_bound;
@@ -3038,7 +3051,7 @@ int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* ca
     if (blk_lo == blk_hi || n_items == 0) {
         ip_empty_range_kernel<<<(int)std::min<int64_t>((n_users + 255) / 256, 4096), 256, 0, s>>>(n_users, w.acnt,
                                                                                                w.uinfo);
-        if (SHARD_LISTBOUND &&
+        if (lbnd &&
             hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(out_bound), 0xFF800000u /* -inf */,
                               (size_t)n_users * m, s) != hipSuccess) {
             set_error("nrk_ip_topk_shard_screen: hipMemsetD32Async failed");
@@ -3047,7 +3060,7 @@ int nrk_ip_topk_shard_screen(const float* users, int64_t n_users, const void* ca
     } else {
         scan_dispatch(users, (int)n_users, reinterpret_cast<const uint8_t*>(catalog), (int)n_items, dim, k, w, s);
     }
-    if (!SHARD_LISTBOUND)
+    if (!lbnd)
         ip_shard_bound_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, w.m2, w.app, w.acnt, w.uinfo, m, out_bound,
                                                                w.ovf_flag, w.bandcap, w.cand, w.cnt);
     NRK_CHECK_LAUNCH();
@@ -3069,8 +3082,8 @@ int nrk_ip_topk_shard_band(int64_t n_users, int64_t n_items, int dim, int k, con
     const IpWs w = ip_ws_layout(workspace, n_users, n_items, k, dim);
     ip_shard_band_kernel<<<sh_grid(n_users), 256, 0, as_stream(stream)>>>(
         n_users, k, w.m2, w.app, w.acnt, w.uinfo, bounds, bounds ? n_lists : 0, bounds ? m : 1, w.bandcap,
-        SHARD_LISTBOUND ? nullptr : w.ovf_flag, SHARD_LISTBOUND ? nullptr : w.cand,
-        SHARD_LISTBOUND ? nullptr : w.cnt, w.ucut, reinterpret_cast<uint32_t*>(out_ent), out_cnt, x_cap);
+        shard_listbound(k) ? nullptr : w.ovf_flag, shard_listbound(k) ? nullptr : w.cand,
+        shard_listbound(k) ? nullptr : w.cnt, w.ucut, reinterpret_cast<uint32_t*>(out_ent), out_cnt, x_cap);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
