@@ -313,7 +313,22 @@ constexpr bool SCAN_APP_ASM = NRK_SCAN_APP_ASM, SCAN_INS_BR = NRK_SCAN_INS_BR, S
 #endif
 constexpr bool SCAN_LAZY = NRK_SCAN_LAZY, SCAN_BSEL = NRK_SCAN_BSEL, SCAN_LDSAPP = NRK_SCAN_LDSAPP;
 constexpr int SCAN_SWP = NRK_SCAN_SWP;
+// the one-GPU scan fills every CU (FLAT ip_scan_kernel)
+#ifndef NRK_SCAN_FLAT
+#define NRK_SCAN_FLAT 1
+#endif
+constexpr bool SCAN_FLAT = NRK_SCAN_FLAT;
 
+// list pre-pass of the one-pass scan: n_pre = min(SCAN_PRE_MAX, n / 6) tiles
+// of an n-tile range, none below SCAN_PRE_MIN tiles (dev: -DNRK_SCAN_PRE_MAX=0
+// turns it off)
+#ifndef NRK_SCAN_PRE_MAX
+#define NRK_SCAN_PRE_MAX 64
+#endif
+#ifndef NRK_SCAN_PRE_DIV
+#define NRK_SCAN_PRE_DIV 6
+#endif
+constexpr int SCAN_PRE_MAX = NRK_SCAN_PRE_MAX, SCAN_PRE_MIN = 128, SCAN_PRE_DIV = NRK_SCAN_PRE_DIV;
 // (lane bit of m) ? T : F, one v_cndmask_b32 on the compare's SGPR lane mask
 // with inline constants (0..64); sel_mask_v: (lane bit of m) ? T : f
 template <int F, int T>
@@ -373,12 +388,36 @@ __device__ unsigned long long scan_stamps[1024 * 16];
 // Scan: NW waves x UG x 32 users per workgroup share one NSL-slot LDS ring of
 // catalog tiles (8 KB, or one 16-KB block at dim 256).  Per tile every wave
 // reads the tile's A fragments once and runs TB x DS x UG MFMAs.
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false>
-__global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
+// One segment: user block ub over the tiles [tile_lo, tile_hi).  FLAT (see
+// ip_scan_kernel): seg 1 is the second part of a user block split between
+// two workgroups -- its appends fill the lists from their last slot down, its
+// counts go to acnt1 and its list bound to lb1; a workgroup that scans a
+// whole block (whole) clears the block's seg-1 outputs.
+// the scan's LDS: the NSL-tile ring and the LDS append stage (LDSAPP): per
+// (wave, group) STG_C entry slots x 64 lanes x 8 B, entry-major (slot e of
+// lane l at e * 512 + l * 8: any mix of per-lane slots is bank-conflict
+// free), sized to what the ring leaves of the CU's LDS share
+template <int DP, int NW, int NSL, int UG, int WPE, bool TAPP>
+struct ScanLds {
+    static constexpr int BLOCK_BYTES = 64 * DP;
+    static constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
+    static constexpr int TILE_BYTES = TB * BLOCK_BYTES;
+    static constexpr int WG_PER_CU = (WPE * 4) / NW > 0 ? (WPE * 4) / NW : 1;
+    static constexpr int STG_RAW = (163840 / WG_PER_CU - NSL * TILE_BYTES) / (NW * UG * 512);
+    static constexpr bool LDSAPP = SCAN_LDSAPP && !TAPP && SCAN_APP_GRP && TB > 1 && STG_RAW >= TB + 1;
+    static constexpr int STG_C = LDSAPP ? (STG_RAW < 8 ? STG_RAW : 8) : 1;
+    static constexpr int RING = NSL * TILE_BYTES;
+    static constexpr int STG = LDSAPP ? NW * UG * STG_C * 512 : 16;
+};
+
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD, int IE, bool TAPP, bool FLAT,
+          bool DOWN = false>
+__device__ __forceinline__ void ip_scan_seg(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
     int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
-    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int n_pre = 0, int pstride = 1,
-    float* __restrict__ bnd = nullptr, int bnd_m = 0) {
+    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int n_pre, int pstride,
+    float* __restrict__ bnd, int bnd_m, int ub, int seg, bool whole, int32_t* __restrict__ acnt1,
+    float* __restrict__ lb1, uint8_t* smem, uint8_t* stg) {
     constexpr bool APP = true;  // (the two-pass screen's append-free pass 1 is gone)
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
@@ -388,20 +427,14 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
     static_assert(!FULLREAD || (TB * DS) % 8 == 0, "fragment groups of 8");
     static_assert(NSL >= 2, "ring");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[NSL * TILE_BYTES];
-    // LDS append stage (LDSAPP): per (wave, group) STG_C entry slots x 64
-    // lanes x 8 B, entry-major (slot e of lane l at e * 512 + l * 8: any mix
-    // of per-lane slots is bank-conflict free), sized to what the ring leaves
-    // of the CU's LDS share
-    constexpr int WG_PER_CU = (WPE * 4) / NW > 0 ? (WPE * 4) / NW : 1;
-    constexpr int STG_RAW = (163840 / WG_PER_CU - NSL * TILE_BYTES) / (NW * UG * 512);
-    constexpr bool LDSAPP = SCAN_LDSAPP && APP && !TAPP && SCAN_APP_GRP && TB > 1 && STG_RAW >= TB + 1;
-    constexpr int STG_C = LDSAPP ? (STG_RAW < 8 ? STG_RAW : 8) : 1;
-    __shared__ __attribute__((aligned(16))) uint8_t stg[LDSAPP ? NW * UG * STG_C * 512 : 16];
+    // smem: the ring (NSL tiles); stg: the LDS append stage (LDSAPP) -- both
+    // declared by ip_scan_kernel (scan_lds)
+    constexpr bool LDSAPP = ScanLds<DP, NW, NSL, UG, WPE, TAPP>::LDSAPP;
+    constexpr int STG_C = ScanLds<DP, NW, NSL, UG, WPE, TAPP>::STG_C;
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
-    const int ubase = blockIdx.x * (NW * 32 * UG) + wave * (32 * UG);
+    const int ubase = ub * (NW * 32 * UG) + wave * (32 * UG);
 #if NRK_SCAN_STAMP
     uint64_t sstp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t t_prev = 0;
@@ -418,7 +451,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     // B operands: 32 users x DP dims per group, fp16 (scaled by a power of
     // two); lane holds user q of the group, dims 16s + 8h + [0, 8).
     f16x8 ufrag[UG][DS];
-    float eps_s[UG], eps_u[UG], scl[UG], tau[UG];
+    float eps_s[UG], tau[UG];
     float t[UG][MT];
     bool live[UG];
 #pragma unroll
@@ -462,9 +495,11 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         const float ceps = 3.0517578e-5f + (float)DP * 1.1920929e-7f;
         const float eps = (nrm2 == 0.0f) ? 0.0f
                                          : (ndu * vmax + nu * dvmax + ndu * dvmax + ceps * nu * vmax) * 1.0001f + 1e-30f;
-        scl[g] = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
-        eps_s[g] = eps * scl[g];
-        eps_u[g] = eps;
+        const float scl = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
+        eps_s[g] = eps * scl;
+        // the user's record now (its list bound .x at the end; a tail part
+        // writes none): scl and eps are not held through the scan
+        if (!DOWN && h == 0 && active) uinfo[user] = make_float4(-INFINITY, eps_s[g], scl, eps);
         // zero users (all scores exactly 0) are answered by the refine directly
         live[g] = active && nrm2 > 0.0f;
         tau[g] = live[g] ? -FLT_MAX : INFINITY;
@@ -477,7 +512,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     // the capacity -- the select then sends the user to the exact fallback
     // -- and extra entries land on the last slot).  Users past n_users are
     // not live: tau = +inf, they never append.
-    uint2* const wapp = app + (size_t)(blockIdx.x * (NW * 32 * UG) + __builtin_amdgcn_readfirstlane(wave) * (32 * UG)) *
+    uint2* const wapp = app + (size_t)(ub * (NW * 32 * UG) + __builtin_amdgcn_readfirstlane(wave) * (32 * UG)) *
                                   2 * (size_t)m2;
     uint32_t pos[UG], lim[UG];
 #pragma unroll
@@ -485,6 +520,14 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         pos[g] = (uint32_t)((g * 32 + q) * 2 + h) * (uint32_t)m2;
         lim[g] = pos[g] + (uint32_t)m2 - 1u;
     }
+    // the list slot of position x (seg 1 of a FLAT launch: from the last slot down)
+    constexpr bool down = FLAT && DOWN;
+    (void)seg;
+    auto slot = [&](uint32_t x, int g) -> uint32_t {
+        const uint32_t m = min(x, lim[g]);
+        if constexpr (down) return lim[g] + (lim[g] + 1u - (uint32_t)m2) - m;
+        return m;
+    };
     auto app_store = [&](uint32_t e, uint2 v) {
         *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(wapp) + (e << 3)) = v;
     };
@@ -539,7 +582,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                          : "=v"(d)
                          : "v"(stg_lane + e * 512u), "n"(G * STG_C * 512)
                          : "memory");
-            app_store_if(m, min(pos[G] + e, lim[G]), make_uint2((uint32_t)d, (uint32_t)(d >> 32)));
+            app_store_if(m, slot(pos[G] + e, G), make_uint2((uint32_t)d, (uint32_t)(d >> 32)));
         }
         pos[G] += nb[G];
         nb[G] = 0u;
@@ -835,7 +878,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                         const uint32_t fid = (first_set_block<TB>(am[g]) << 1) + hb0;
                         const uint32_t p0 = LDSAPP ? nb[g] : pos[g];
                         if constexpr (LDSAPP) stg_store_if(gc, gm, p0, __float_as_uint(vt[g]), fid);
-                        else app_store_if(gm, min(p0, lim[g]), make_uint2(__float_as_uint(vt[g]), fid));
+                        else app_store_if(gm, slot(p0, g), make_uint2(__float_as_uint(vt[g]), fid));
                         uint32_t p = add_if(p0, gm);
                         if (multi) {
                             p = p0;
@@ -843,7 +886,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                             for (int b = 0; b < TB; ++b) {
                                 const uint32_t idb = hb0 + 2u * b;
                                 if constexpr (LDSAPP) stg_store_if(gc, am[g][b] & multi, p, __float_as_uint(mx[g][b]), idb);
-                                else app_store_if(am[g][b] & multi, min(p, lim[g]), make_uint2(__float_as_uint(mx[g][b]), idb));
+                                else app_store_if(am[g][b] & multi, slot(p, g), make_uint2(__float_as_uint(mx[g][b]), idb));
                                 p = add_if(p, am[g][b]);
                             }
                         }
@@ -894,7 +937,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                         for (int b = TB - 2; b >= 0; --b)
                             fid = mx[g][b] >= tau[g] ? (uint32_t)((tt * TB + b) * 2 + h) : fid;
                         const uint32_t p0 = pos[g];
-                        app_store_if(gm, min(p0, lim[g]), make_uint2(__float_as_uint(vt[g]), fid));
+                        app_store_if(gm, slot(p0, g), make_uint2(__float_as_uint(vt[g]), fid));
                         pos[g] = add_if(p0, gm);  // one append per lane, unless multi
                         if (multi) {
                             // p ends at p0 + the lane's append count: the same
@@ -902,7 +945,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                             uint32_t p = p0;
 #pragma unroll
                             for (int b = 0; b < TB; ++b) {
-                                app_store_if(am[g][b] & multi, min(p, lim[g]),
+                                app_store_if(am[g][b] & multi, slot(p, g),
                                              make_uint2(__float_as_uint(mx[g][b]), (uint32_t)((tt * TB + b) * 2 + h)));
                                 p = add_if(p, am[g][b]);
                             }
@@ -914,9 +957,9 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                     for (int b = 0; b < TB; ++b) {
                         const uint2 ev = make_uint2(__float_as_uint(mx[g][b]), (uint32_t)((tt * TB + b) * 2 + h));
                         if constexpr (SCAN_APP_ASM) {
-                            app_store_if(am[g][b], min(pos[g], lim[g]), ev);
+                            app_store_if(am[g][b], slot(pos[g], g), ev);
                         } else {
-                            if (mx[g][b] >= tau[g]) app_store(min(pos[g], lim[g]), ev);
+                            if (mx[g][b] >= tau[g]) app_store(slot(pos[g], g), ev);
                         }
                         pos[g] = add_if(pos[g], am[g][b]);
                     }
@@ -1092,8 +1135,18 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         const float lb = pair_min32(t[g][MT - 1]);
         const int user = ubase + g * 32 + q;
         if (user < n_users) {
-            acnt[(size_t)user * 2 + h] = (int)(pos[g] - (lim[g] + 1u - (uint32_t)m2));
-            if (h == 0) uinfo[user] = make_float4(live[g] ? lb : -INFINITY, eps_s[g], scl[g], eps_u[g]);
+            const int cnt_g = (int)(pos[g] - (lim[g] + 1u - (uint32_t)m2));
+            if (FLAT && down) {
+                acnt1[(size_t)user * 2 + h] = cnt_g;
+                if (h == 0) lb1[user] = live[g] ? lb : -INFINITY;
+            } else {
+                acnt[(size_t)user * 2 + h] = cnt_g;
+                if (h == 0) reinterpret_cast<float*>(uinfo + user)[0] = live[g] ? lb : -INFINITY;
+                if (FLAT && whole) {  // no second part
+                    acnt1[(size_t)user * 2 + h] = 0;
+                    if (h == 0) lb1[user] = -INFINITY;
+                }
+            }
         }
     }
     // Config-4 shard (bnd != nullptr): per user the bnd_m largest values of
@@ -1129,14 +1182,15 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             if (h == 0 && user < n_users) {
                 float* o = bnd + (size_t)user * bnd_m;
                 const int p0 = 2 * (MT - nl);  // the placeholders sort to the front
-                const double inv = 1.0 / (double)scl[g];  // exact power of two
+                const float4 ui = uinfo[user];  // this lane's own record (scl, eps)
+                const double inv = 1.0 / (double)ui.z;  // exact power of two
 #pragma unroll
                 for (int j = 0; j < 2 * MT; ++j) {
                     const int r = j - p0;
                     if (r >= 0 && r < bnd_m) {
                         float v = -INFINITY;
                         if (live[g] && c[j] != -INFINITY) {
-                            const double tv = (double)c[j] * inv - (double)eps_u[g];
+                            const double tv = (double)c[j] * inv - (double)ui.w;
                             v = (float)tv;
                             if ((double)v > tv) v = nextafterf(v, -INFINITY);
                         }
@@ -1146,6 +1200,56 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
                 for (int r = 2 * nl; r < bnd_m; ++r) o[r] = -INFINITY;  // fewer values than bnd_m
             }
         }
+    }
+}
+
+// The scan launch.  Not FLAT: workgroup b scans user block b over the whole
+// range.  FLAT (head > 0): the grid fills every workgroup slot of the chip
+// although the user blocks do not divide among them (config 2: 245 blocks,
+// 256 CUs, so 11 CUs sat idle): workgroup b < n_blocks scans the head of
+// block b (tiles [0, head)), workgroup n_blocks + b its tail ([head, T)),
+// with head = c T / (c + 1) rounded up, c = ceil(n_blocks / E), E = the
+// slots the heads leave free: the E free CUs run c tails each while the
+// heads run, so every CU runs about the same number of tiles.  A block has two parts; the tail's appends share the
+// lists with the head's (filling them from the last slot down), its counts
+// go to acnt1 and its list bound to lb1, and the select merges both (each
+// part is a complete one-pass scan of its own tiles with its own list
+// pre-pass, so each part's bound is valid for the user, and the larger is
+// the user's).
+template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false,
+          bool FLAT = false>
+__global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
+    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
+    int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
+    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int n_pre = 0, int pstride = 1,
+    float* __restrict__ bnd = nullptr, int bnd_m = 0, int head = 0, int32_t* __restrict__ acnt1 = nullptr,
+    float* __restrict__ lb1 = nullptr) {
+    using L = ScanLds<DP, NW, NSL, UG, WPE, TAPP>;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[L::RING];
+    __shared__ __attribute__((aligned(16))) uint8_t stg[L::STG];
+    if constexpr (!FLAT) {
+        ip_scan_seg<DP, NW, NSL, UG, MT, WPE, FULLREAD, IE, TAPP, false>(
+            users, n_users, catalog, n_items, dim, k, m2, app, acnt, uinfo, tile_lo, tile_hi, n_pre, pstride, bnd,
+            bnd_m, blockIdx.x, 0, true, nullptr, nullptr, smem, stg);
+    } else {
+        // workgroup w < n_blocks: the head of block w; the others: the tail of
+        // block w - n_blocks (dispatched after the heads, onto the CUs the
+        // heads leave free, then onto each CU a tail frees)
+        const int T = tile_hi - tile_lo;
+        const int nub = (n_users + NW * 32 * UG - 1) / (NW * 32 * UG);
+        const bool tail = (int)blockIdx.x >= nub;
+        const int b = tail ? (int)blockIdx.x - nub : (int)blockIdx.x;
+        const int t0 = tail ? head : 0, t1 = tail ? T : head, n = t1 - t0;
+        const int np = IE == 1 && n >= (tail ? 32 : SCAN_PRE_MIN) ? min(SCAN_PRE_MAX, n / SCAN_PRE_DIV) : 0;
+        // two copies (the tail's list slots run down): compile-time, no extra registers
+        if (tail)
+            ip_scan_seg<DP, NW, NSL, UG, MT, WPE, FULLREAD, IE, TAPP, true, true>(
+                users, n_users, catalog, n_items, dim, k, m2, app, acnt, uinfo, tile_lo + t0, tile_lo + t1, np,
+                np > 0 ? n / np : 1, nullptr, 0, b, 1, false, acnt1, lb1, smem, stg);
+        else
+            ip_scan_seg<DP, NW, NSL, UG, MT, WPE, FULLREAD, IE, TAPP, true, false>(
+                users, n_users, catalog, n_items, dim, k, m2, app, acnt, uinfo, tile_lo + t0, tile_lo + t1, np,
+                np > 0 ? n / np : 1, nullptr, 0, b, 0, head >= T, acnt1, lb1, smem, stg);
     }
 }
 
@@ -1229,36 +1333,57 @@ __global__ __launch_bounds__(256) void ip_select_kernel(
     int64_t n_users, int k, int m2, int bandcap, const uint2* __restrict__ app,
     const int32_t* __restrict__ acnt, const float4* __restrict__ uinfo, uint2* __restrict__ cand,
     int32_t* __restrict__ cand_cnt, float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag,
-    int32_t* __restrict__ ovf_list, int32_t* __restrict__ ovf_count) {
+    int32_t* __restrict__ ovf_list, int32_t* __restrict__ ovf_count, const int32_t* __restrict__ acnt1,
+    const float* __restrict__ lb1) {
     __shared__ __attribute__((aligned(16))) uint32_t sel[4][IP_SEL + 4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * 4;
     const unsigned long long lt = (1ull << lane) - 1ull;
     // persistent waves (see the shard kernels): the next user's counts and
-    // record load during this one; entries load SH_ENT x 64 at a time
+    // record load during this one; entries load SH_ENT x 64 at a time.  A
+    // FLAT scan's tail part (acnt1, lb1; zeros / -inf otherwise) fills each
+    // list from its last slot down: the user's entries are list 0 [0, a0),
+    // list 1 [0, a1), then the tails, and the list bound is the larger one.
     int64_t u = (int64_t)blockIdx.x * 4 + wave;
-    int2 ac_n = make_int2(0, 0);
+    int2 ac_n = make_int2(0, 0), ad_n = make_int2(0, 0);
     float4 inf_n = make_float4(0.f, 0.f, 0.f, 0.f);
+    float lb1_n = -INFINITY;
     if (u < n_users) {
         ac_n = reinterpret_cast<const int2*>(acnt)[u];
+        ad_n = reinterpret_cast<const int2*>(acnt1)[u];
         inf_n = uinfo[u];
+        lb1_n = lb1[u];
     }
     for (; u < n_users; u += nw) {
-        const int a0 = ac_n.x, a1 = ac_n.y;
-        const float4 inf = inf_n;
+        const int a0 = ac_n.x, a1 = ac_n.y, d0 = ad_n.x, d1 = ad_n.y;
+        float4 inf = inf_n;
+        inf.x = fmaxf(inf.x, lb1_n);
         if (u + nw < n_users) {
             ac_n = reinterpret_cast<const int2*>(acnt)[u + nw];
+            ad_n = reinterpret_cast<const int2*>(acnt1)[u + nw];
             inf_n = uinfo[u + nw];
+            lb1_n = lb1[u + nw];
         }
-        bool ovf = a0 > m2 || a1 > m2;
-        const int n = ovf ? 0 : a0 + a1;
+        bool ovf = a0 + d0 > m2 || a1 + d1 > m2;
+        const int n = ovf ? 0 : a0 + a1 + d0 + d1;
         const uint2* s0 = app + (size_t)(2 * u) * m2;
         const uint2* s1 = s0 + m2;
+        auto sh_load = [&](int n_, int b0, int lane_, uint2 (&ent)[SH_ENT]) {
+#pragma unroll
+            for (int j = 0; j < SH_ENT; ++j) {
+                const int e = b0 + j * WAVE + lane_;
+                const uint2* src = e < a0 ? s0 + e
+                                   : e < a0 + a1 ? s1 + (e - a0)
+                                   : e < a0 + a1 + d0 ? s0 + (m2 - 1 - (e - a0 - a1))
+                                                      : s1 + (m2 - 1 - (e - a0 - a1 - d0));
+                ent[j] = e < n_ ? *src : make_uint2(0u, 0u);
+            }
+        };
         // pass 1: keys of the entries >= theta_lb
         int c = 0;
         uint2 ent[SH_ENT];
         for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
-            sh_load(s0, s1, a0, n, b0, lane, ent);
+            sh_load(n, b0, lane, ent);
 #pragma unroll
             for (int j = 0; j < SH_ENT; ++j) {
                 const int e = b0 + j * WAVE + lane;
@@ -1284,7 +1409,7 @@ __global__ __launch_bounds__(256) void ip_select_kernel(
         int nb = 0;
         uint2* bd = cand + (size_t)u * bandcap;
         for (int b0 = 0; b0 < n; b0 += SH_ENT * WAVE) {
-            if (n > SH_ENT * WAVE) sh_load(s0, s1, a0, n, b0, lane, ent);
+            if (n > SH_ENT * WAVE) sh_load(n, b0, lane, ent);
 #pragma unroll
             for (int j = 0; j < SH_ENT; ++j) {
                 const int e = b0 + j * WAVE + lane;
@@ -2524,6 +2649,13 @@ struct IpWs {
     Surv* surv = nullptr;
     int64_t n_hb = 0;
     int svb = 0;
+    // FLAT scan (ip_scan_kernel): the tail parts' counts and list bounds;
+    // flat_ok = the caller's select reads them (the one-GPU screen), flat_used
+    // = the scan launch split blocks (set by launch_scan_v)
+    int32_t* acnt1 = nullptr;
+    float* lb1 = nullptr;
+    bool flat_ok = false;
+    mutable bool flat_used = false;
     size_t bytes;
 };
 
@@ -2580,6 +2712,10 @@ static IpWs ip_ws_layout(void* base, int64_t n_users, int64_t n_items, int k, in
     off += align256((size_t)n_users * sizeof(float4));
     w.acnt = reinterpret_cast<int32_t*>(p + off);
     off += align256((size_t)n_users * 2 * sizeof(int32_t));
+    w.acnt1 = reinterpret_cast<int32_t*>(p + off);
+    off += align256((size_t)n_users * 2 * sizeof(int32_t));
+    w.lb1 = reinterpret_cast<float*>(p + off);
+    off += align256((size_t)n_users * sizeof(float));
     w.cand = reinterpret_cast<uint2*>(p + off);
     off += align256((size_t)n_users * w.bandcap * sizeof(uint2));
     w.app = reinterpret_cast<uint2*>(p + off);
@@ -2614,6 +2750,16 @@ static inline int next_pow2(int x) {
     return p;
 }
 
+// compute units of the current device (the persistent grids, the FLAT scan)
+static int n_cus() {
+    static const int n_cu = [] {
+        int dev = 0, cu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+        return cu > 0 ? cu : 256;
+    }();
+    return n_cu;
+}
+
 // scan variants: (DP, waves per workgroup, ring slots, user groups per wave,
 // register list length, waves per SIMD)
 // ring slots of the UG = 4 scan (config 2): 4 (one more tile in flight
@@ -2623,16 +2769,6 @@ static inline int next_pow2(int x) {
 #define NRK_SCAN_NSL4 4
 #endif
 constexpr int SCAN_NSL4 = NRK_SCAN_NSL4;
-// list pre-pass of the one-pass scan: n_pre = min(SCAN_PRE_MAX, n / 6) tiles
-// of an n-tile range, none below SCAN_PRE_MIN tiles (dev: -DNRK_SCAN_PRE_MAX=0
-// turns it off)
-#ifndef NRK_SCAN_PRE_MAX
-#define NRK_SCAN_PRE_MAX 64
-#endif
-#ifndef NRK_SCAN_PRE_DIV
-#define NRK_SCAN_PRE_DIV 6
-#endif
-constexpr int SCAN_PRE_MAX = NRK_SCAN_PRE_MAX, SCAN_PRE_MIN = 128, SCAN_PRE_DIV = NRK_SCAN_PRE_DIV;
 template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false>
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
@@ -2646,6 +2782,21 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
     const int n = t_hi - t_lo;
     const int n_pre = (IE == 1 && n >= SCAN_PRE_MIN) ? std::min(SCAN_PRE_MAX, n / SCAN_PRE_DIV) : 0;
     const int pstride = n_pre > 0 ? n / n_pre : 1;
+    // FLAT: every workgroup slot of the chip busy (see ip_scan_kernel)
+    constexpr int WG_CU = (WPE * 4) / NW > 0 ? (WPE * 4) / NW : 1;
+    const int slots = n_cus() * WG_CU, nub = (int)grid;
+    w.flat_used = false;
+    if (SCAN_FLAT && w.flat_ok && w.bnd == nullptr && nub < slots && n >= 64) {
+        const int E = slots - nub, c = (nub + E - 1) / E;
+        const int head = (int)(((int64_t)c * n + c) / (c + 1));  // ceil(c n / (c + 1))
+        if (head < n) {
+            ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP, true><<<2 * nub, NW * 64, 0, s>>>(
+                users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, 0, 1, nullptr, 0,
+                head, w.acnt1, w.lb1);
+            w.flat_used = true;
+            return;
+        }
+    }
     ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<grid, NW * 64, 0, s>>>(
         users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, n_pre, pstride, w.bnd,
         w.bnd_m);
@@ -2723,12 +2874,7 @@ constexpr bool HB_REFINE = NRK_HB_REFINE;
 
 // persistent grid of the shard kernels: SH_WG_PER_CU 4-wave workgroups per CU
 static int sh_grid(int64_t n_users) {
-    static const int n_cu = [] {
-        int dev = 0, cu = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
-        return cu > 0 ? cu : 256;
-    }();
-    return (int)std::max<int64_t>(1, std::min<int64_t>((n_users + 3) / 4, (int64_t)n_cu * SH_WG_PER_CU));
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n_users + 3) / 4, (int64_t)n_cus() * SH_WG_PER_CU));
 }
 
 // empty shard range: no appends, uinfo.z = 0 (shard_band: no band, no cut)
@@ -2848,7 +2994,17 @@ static int screen_phases(const float* users, int64_t n_users, const void* catalo
     if (blk_hi == blk_lo) n_items = 0;  // empty range: every output row is padding
     hipStream_t s = as_stream(stream);
     const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
-    if ((phases & 1) && n_items > 0 && k <= IP_KFAST) scan_dispatch(users, (int)n_users, cat, (int)n_items, dim, k, w, s);
+    if ((phases & 1) && n_items > 0 && k <= IP_KFAST) {
+        w.flat_ok = true;  // this select reads the tail parts' counts and bounds
+        scan_dispatch(users, (int)n_users, cat, (int)n_items, dim, k, w, s);
+        if (!w.flat_used &&
+            (hipMemsetAsync(w.acnt1, 0, (size_t)n_users * 2 * sizeof(int32_t), s) != hipSuccess ||
+             hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.lb1), 0xFF800000u /* -inf */, (size_t)n_users, s) !=
+                 hipSuccess)) {
+            set_error("nrk_ip_topk_scan: hipMemsetAsync failed");
+            return NRK_EHIP;
+        }
+    }
     if (phases & 2) {
         if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
             set_error("nrk_ip_topk_screen: hipMemsetAsync failed");
@@ -2865,7 +3021,7 @@ static int screen_phases(const float* users, int64_t n_users, const void* catalo
         } else {
             ip_select_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt, w.uinfo,
                                                               w.cand, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,
-                                                              w.ovf_count);
+                                                              w.ovf_count, w.acnt1, w.lb1);
         }
     }
     NRK_CHECK_LAUNCH();
