@@ -301,7 +301,7 @@ constexpr bool SCAN_APP_ASM = NRK_SCAN_APP_ASM, SCAN_INS_BR = NRK_SCAN_INS_BR, S
 #define NRK_SCAN_LAZY 0
 #endif
 #ifndef NRK_SCAN_BSEL
-#define NRK_SCAN_BSEL 0
+#define NRK_SCAN_BSEL 1
 #endif
 #ifndef NRK_SCAN_LDSAPP
 #define NRK_SCAN_LDSAPP 0
@@ -309,13 +309,13 @@ constexpr bool SCAN_APP_ASM = NRK_SCAN_APP_ASM, SCAN_INS_BR = NRK_SCAN_INS_BR, S
 // SWP -- the tile's MFMAs software-pipelined against the half-block max
 // reductions (see tile()); the value is the lag in (block, group) steps
 #ifndef NRK_SCAN_SWP
-#define NRK_SCAN_SWP 0
+#define NRK_SCAN_SWP 2
 #endif
 constexpr bool SCAN_LAZY = NRK_SCAN_LAZY, SCAN_BSEL = NRK_SCAN_BSEL, SCAN_LDSAPP = NRK_SCAN_LDSAPP;
 constexpr int SCAN_SWP = NRK_SCAN_SWP;
 // the one-GPU scan fills every CU (FLAT ip_scan_kernel)
 #ifndef NRK_SCAN_FLAT
-#define NRK_SCAN_FLAT 1
+#define NRK_SCAN_FLAT 0
 #endif
 constexpr bool SCAN_FLAT = NRK_SCAN_FLAT;
 
@@ -1329,6 +1329,7 @@ __device__ __forceinline__ void sh_load(const uint2* s0, const uint2* s1, int a0
 // band = every appended entry >= cut = theta - 2 eps (rounded down); an
 // item with exact score >= cut + eps has an fp16 score >= cut, so its
 // half-block max was >= every tau of the scan and was appended.
+template <bool FLAT>
 __global__ __launch_bounds__(256) void ip_select_kernel(
     int64_t n_users, int k, int m2, int bandcap, const uint2* __restrict__ app,
     const int32_t* __restrict__ acnt, const float4* __restrict__ uinfo, uint2* __restrict__ cand,
@@ -1350,19 +1351,19 @@ __global__ __launch_bounds__(256) void ip_select_kernel(
     float lb1_n = -INFINITY;
     if (u < n_users) {
         ac_n = reinterpret_cast<const int2*>(acnt)[u];
-        ad_n = reinterpret_cast<const int2*>(acnt1)[u];
+        if (FLAT) ad_n = reinterpret_cast<const int2*>(acnt1)[u];
         inf_n = uinfo[u];
-        lb1_n = lb1[u];
+        if (FLAT) lb1_n = lb1[u];
     }
     for (; u < n_users; u += nw) {
         const int a0 = ac_n.x, a1 = ac_n.y, d0 = ad_n.x, d1 = ad_n.y;
         float4 inf = inf_n;
-        inf.x = fmaxf(inf.x, lb1_n);
+        if (FLAT) inf.x = fmaxf(inf.x, lb1_n);
         if (u + nw < n_users) {
             ac_n = reinterpret_cast<const int2*>(acnt)[u + nw];
-            ad_n = reinterpret_cast<const int2*>(acnt1)[u + nw];
+            if (FLAT) ad_n = reinterpret_cast<const int2*>(acnt1)[u + nw];
             inf_n = uinfo[u + nw];
-            lb1_n = lb1[u + nw];
+            if (FLAT) lb1_n = lb1[u + nw];
         }
         bool ovf = a0 + d0 > m2 || a1 + d1 > m2;
         const int n = ovf ? 0 : a0 + a1 + d0 + d1;
@@ -1372,10 +1373,14 @@ __global__ __launch_bounds__(256) void ip_select_kernel(
 #pragma unroll
             for (int j = 0; j < SH_ENT; ++j) {
                 const int e = b0 + j * WAVE + lane_;
-                const uint2* src = e < a0 ? s0 + e
-                                   : e < a0 + a1 ? s1 + (e - a0)
-                                   : e < a0 + a1 + d0 ? s0 + (m2 - 1 - (e - a0 - a1))
-                                                      : s1 + (m2 - 1 - (e - a0 - a1 - d0));
+                const uint2* src;
+                if constexpr (FLAT)
+                    src = e < a0 ? s0 + e
+                          : e < a0 + a1 ? s1 + (e - a0)
+                          : e < a0 + a1 + d0 ? s0 + (m2 - 1 - (e - a0 - a1))
+                                             : s1 + (m2 - 1 - (e - a0 - a1 - d0));
+                else
+                    src = e < a0 ? s0 + e : s1 + (e - a0);
                 ent[j] = e < n_ ? *src : make_uint2(0u, 0u);
             }
         };
@@ -2868,7 +2873,7 @@ constexpr bool SHARD_LISTBOUND = NRK_SHARD_LISTBOUND;
 static inline bool shard_listbound(int k) { return SHARD_LISTBOUND && (k + 1) / 2 <= 32; }
 // the one-GPU finish by half-block buckets (ip_hb_*) instead of ip_refine_kernel
 #ifndef NRK_HB_REFINE
-#define NRK_HB_REFINE 1
+#define NRK_HB_REFINE 0
 #endif
 constexpr bool HB_REFINE = NRK_HB_REFINE;
 
@@ -2997,7 +3002,7 @@ static int screen_phases(const float* users, int64_t n_users, const void* catalo
     if ((phases & 1) && n_items > 0 && k <= IP_KFAST) {
         w.flat_ok = true;  // this select reads the tail parts' counts and bounds
         scan_dispatch(users, (int)n_users, cat, (int)n_items, dim, k, w, s);
-        if (!w.flat_used &&
+        if (SCAN_FLAT && !w.flat_used &&
             (hipMemsetAsync(w.acnt1, 0, (size_t)n_users * 2 * sizeof(int32_t), s) != hipSuccess ||
              hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.lb1), 0xFF800000u /* -inf */, (size_t)n_users, s) !=
                  hipSuccess)) {
@@ -3019,9 +3024,15 @@ static int screen_phases(const float* users, int64_t n_users, const void* catalo
             const int grid = (int)std::min<int64_t>((n_users + 255) / 256, 4096);
             ip_all_exact_kernel<<<grid, 256, 0, s>>>(n_users, w.cnt, w.ovf_flag, w.ovf_list, w.ovf_count);
         } else {
-            ip_select_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt, w.uinfo,
-                                                              w.cand, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,
-                                                              w.ovf_count, w.acnt1, w.lb1);
+            // FLAT builds read the tail parts (zeros / -inf when the scan did not split)
+            if (SCAN_FLAT)
+                ip_select_kernel<true><<<sh_grid(n_users), 256, 0, s>>>(
+                    n_users, k, w.m2, w.bandcap, w.app, w.acnt, w.uinfo, w.cand, w.cnt, w.ucut, w.ovf_flag,
+                    w.ovf_list, w.ovf_count, w.acnt1, w.lb1);
+            else
+                ip_select_kernel<false><<<sh_grid(n_users), 256, 0, s>>>(
+                    n_users, k, w.m2, w.bandcap, w.app, w.acnt, w.uinfo, w.cand, w.cnt, w.ucut, w.ovf_flag,
+                    w.ovf_list, w.ovf_count, nullptr, nullptr);
         }
     }
     NRK_CHECK_LAUNCH();
