@@ -393,6 +393,55 @@ __device__ unsigned long long scan_stamps[1024 * 16];
 // two workgroups -- its appends fill the lists from their last slot down, its
 // counts go to acnt1 and its list bound to lb1; a workgroup that scans a
 // whole block (whole) clears the block's seg-1 outputs.
+// Config-4 shard list bound of one user (lane pair (q, h)): the bnd_m largest
+// values of its two lanes' final lists (t: descending, +inf placeholders in
+// front, jk + 1 real values) as exact lower bounds v / scl - eps (rounded down
+// to fp32, descending, -inf padded) -- each list value is a distinct
+// half-block's fp16 maximum of this range, so each bounds a distinct item's
+// exact score from below.  The pair's lists are merged in registers: A .
+// reverse(B) is bitonic, log2(2 MT) half-cleaner stages sort it.  Reads the
+// user's record (scl, eps) back from uinfo (written by this lane at setup).
+template <int MT>
+__device__ __forceinline__ void list_bound_out(const float (&t)[MT], bool live, int h, int user, int n_users, int jk,
+                                               float* __restrict__ bnd, int bnd_m, const float4* __restrict__ uinfo) {
+    const int nl = jk + 1;  // real list values per lane
+    float c[2 * MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        c[i] = t[i];
+        c[2 * MT - 1 - i] = partner32f(t[i], h);
+    }
+#pragma unroll
+    for (int d = MT; d >= 1; d >>= 1)
+#pragma unroll
+        for (int i = 0; i < 2 * MT; ++i)
+            if ((i & d) == 0) {
+                const float x = c[i], y = c[i + d];
+                c[i] = fmaxf(x, y);
+                c[i + d] = fminf(x, y);
+            }
+    if (h == 0 && user < n_users) {
+        float* o = bnd + (size_t)user * bnd_m;
+        const int p0 = 2 * (MT - nl);  // the placeholders sort to the front
+        const float4 ui = uinfo[user];
+        const double inv = 1.0 / (double)ui.z;  // exact power of two
+#pragma unroll
+        for (int j = 0; j < 2 * MT; ++j) {
+            const int r = j - p0;
+            if (r >= 0 && r < bnd_m) {
+                float v = -INFINITY;
+                if (live && c[j] != -INFINITY) {
+                    const double tv = (double)c[j] * inv - (double)ui.w;
+                    v = (float)tv;
+                    if ((double)v > tv) v = nextafterf(v, -INFINITY);
+                }
+                o[r] = v;
+            }
+        }
+        for (int r = 2 * nl; r < bnd_m; ++r) o[r] = -INFINITY;  // fewer values than bnd_m
+    }
+}
+
 // the scan's LDS: the NSL-tile ring and the LDS append stage (LDSAPP): per
 // (wave, group) STG_C entry slots x 64 lanes x 8 B, entry-major (slot e of
 // lane l at e * 512 + l * 8: any mix of per-lane slots is bank-conflict
@@ -1160,46 +1209,9 @@ __device__ __forceinline__ void ip_scan_seg(
     // 64; longer ones would spill the merge -- those shards keep the pass).
     if constexpr (MT > 32) {
     } else if (bnd != nullptr) {
-        const int nl = jk + 1;  // real list values per lane
 #pragma unroll
-        for (int g = 0; g < UG; ++g) {
-            float c[2 * MT];
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                c[i] = t[g][i];
-                c[2 * MT - 1 - i] = partner32f(t[g][i], h);
-            }
-#pragma unroll
-            for (int d = MT; d >= 1; d >>= 1)
-#pragma unroll
-                for (int i = 0; i < 2 * MT; ++i)
-                    if ((i & d) == 0) {
-                        const float x = c[i], y = c[i + d];
-                        c[i] = fmaxf(x, y);
-                        c[i + d] = fminf(x, y);
-                    }
-            const int user = ubase + g * 32 + q;
-            if (h == 0 && user < n_users) {
-                float* o = bnd + (size_t)user * bnd_m;
-                const int p0 = 2 * (MT - nl);  // the placeholders sort to the front
-                const float4 ui = uinfo[user];  // this lane's own record (scl, eps)
-                const double inv = 1.0 / (double)ui.z;  // exact power of two
-#pragma unroll
-                for (int j = 0; j < 2 * MT; ++j) {
-                    const int r = j - p0;
-                    if (r >= 0 && r < bnd_m) {
-                        float v = -INFINITY;
-                        if (live[g] && c[j] != -INFINITY) {
-                            const double tv = (double)c[j] * inv - (double)ui.w;
-                            v = (float)tv;
-                            if ((double)v > tv) v = nextafterf(v, -INFINITY);
-                        }
-                        o[r] = v;
-                    }
-                }
-                for (int r = 2 * nl; r < bnd_m; ++r) o[r] = -INFINITY;  // fewer values than bnd_m
-            }
-        }
+        for (int g = 0; g < UG; ++g)
+            list_bound_out<MT>(t[g], live[g], h, ubase + g * 32 + q, n_users, jk, bnd, bnd_m, uinfo);
     }
 }
 
@@ -1250,6 +1262,654 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
             ip_scan_seg<DP, NW, NSL, UG, MT, WPE, FULLREAD, IE, TAPP, true, false>(
                 users, n_users, catalog, n_items, dim, k, m2, app, acnt, uinfo, tile_lo + t0, tile_lo + t1, np,
                 np > 0 ? n / np : 1, nullptr, 0, b, 0, head >= T, acnt1, lb1, smem, stg);
+    }
+}
+
+// One user's scan setup (lane pair (q, h) of a 32-user group): the fp16 B
+// operand (scaled by a power of two su), and the screen's error bound eps
+// (see ip_scan_seg); returns the user's scaled record.
+template <int DS>
+__device__ __forceinline__ void scan_user_setup(const float* __restrict__ users, int n_users, int dim, int user,
+                                                int h, float vmax, float dvmax, float sv_scale, f16x8 (&uf)[DS],
+                                                float& eps, float& scl, bool& live) {
+    constexpr int DP = DS * 16;
+    const bool active = user < n_users;
+    float uval[DS][8];
+    float nrm2 = 0.0f, uabs = 0.0f;
+    const float* urow = users + (size_t)(active ? user : 0) * dim;
+#pragma unroll
+    for (int s = 0; s < DS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int d = 16 * s + 8 * h + e;
+            const float f = (active && d < dim) ? urow[d] : 0.0f;
+            uval[s][e] = f;
+            nrm2 += f * f;
+            uabs = fmaxf(uabs, fabsf(f));
+        }
+    nrm2 += __shfl_xor(nrm2, 32, WAVE);
+    uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
+    const float su = pow2_scale(uabs);
+    float du2 = 0.0f;
+#pragma unroll
+    for (int s = 0; s < DS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float a = uval[s][e] * su;
+            uf[s][e] = (_Float16)a;
+            const float d = (float)uf[s][e] - a;
+            du2 += d * d;
+        }
+    du2 += __shfl_xor(du2, 32, WAVE);
+    const float nu = sqrtf(nrm2), ndu = sqrtf(du2) / su;
+    const float ceps = 3.0517578e-5f + (float)DP * 1.1920929e-7f;
+    eps = (nrm2 == 0.0f) ? 0.0f : (ndu * vmax + nu * dvmax + ndu * dvmax + ceps * nu * vmax) * 1.0001f + 1e-30f;
+    scl = su * sv_scale;
+    live = active && nrm2 > 0.0f;
+}
+
+// Warp-specialized scan (WS): the same one-pass screen as ip_scan_seg (same
+// lists, taus, appended entries and bounds, bit for bit) with the work of a
+// SIMD split between its two waves instead of both doing both halves.
+// Waves 0-3 (one per SIMD, the MFMA waves) run every MFMA of a tile for 256
+// users (8 groups) and write the half-block maxima (8 groups x TB per lane)
+// to an LDS slot; waves 4-7 (the book waves, one per SIMD) read the previous
+// tile's maxima of the same 256 users and do the appends and list inserts.
+// Per tile barrier the MFMA wave of a SIMD issues 64 back-to-back MFMAs with
+// its reductions in their shadows, and the book wave's VALU fills the issue
+// slots beside them -- the matrix pipe no longer waits for either wave's
+// bookkeeping (round 5, config 2: the mixed waves spent 46% of their cycles
+// outside the tile).  The pre-pass tiles and the main pass are one tile
+// sequence over one ring; every wave loads one 1-KB piece of every tile.
+// LDS: the NSL-tile ring + 2 maxima slots x 4 pairs x 8 groups x 64 lanes x
+// TB floats (64 KB at TB = 4).
+#ifndef NRK_SCAN_WS
+#define NRK_SCAN_WS 1
+#endif
+#ifndef NRK_SCAN_WS_PRIO
+#define NRK_SCAN_WS_PRIO 2
+#endif
+#ifndef NRK_SCAN_WS_BF
+#define NRK_SCAN_WS_BF 0
+#endif
+#ifndef NRK_SCAN_WS_BPRIO
+#define NRK_SCAN_WS_BPRIO 0
+#endif
+#ifndef NRK_SCAN_WS_INSP
+#define NRK_SCAN_WS_INSP 8
+#endif
+#ifndef NRK_SCAN_WS_NORED  // dev timing: the MFMA waves skip the reductions
+#define NRK_SCAN_WS_NORED 0
+#endif
+#ifndef NRK_SCAN_WS_R3
+#define NRK_SCAN_WS_R3 0
+#endif
+#ifndef NRK_SCAN_WS_YPRIO
+#define NRK_SCAN_WS_YPRIO 0
+#endif
+#ifndef NRK_SCAN_WS_STAMPW
+#define NRK_SCAN_WS_STAMPW 4
+#endif
+#ifndef NRK_SCAN_WS_FLOOR
+#define NRK_SCAN_WS_FLOOR 0
+#endif
+#ifndef NRK_SCAN_WS_TPS
+#define NRK_SCAN_WS_TPS 2
+#endif
+// book waves per MFMA wave (1: 8-wave workgroups, 2: 12)
+#ifndef NRK_SCAN_WS_NB
+#define NRK_SCAN_WS_NB 2
+#endif
+constexpr bool SCAN_WS = NRK_SCAN_WS, SCAN_WS_BF = NRK_SCAN_WS_BF, SCAN_WS_R3 = NRK_SCAN_WS_R3;
+constexpr int SCAN_WS_NB = NRK_SCAN_WS_NB;
+template <int DP, int NSL, int MT, int NB>
+__global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws_kernel(
+    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items, int dim, int k,
+    int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt, float4* __restrict__ uinfo, int tile_lo,
+    int tile_hi, int n_pre, int pstride, float* __restrict__ bnd, int bnd_m) {
+    constexpr int NPW = 4, UG = 8, UGB = UG / NB, DS = DP / 16;
+    constexpr int BLOCK_BYTES = 64 * DP;
+    constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
+    constexpr int TILE_BYTES = TB * BLOCK_BYTES;
+    constexpr int NPC = TILE_BYTES / 1024;  // 1-KB pieces per tile: waves 0 .. NPC - 1 load one each
+    static_assert(TB == 4 && DS == 2 && NPC == 8 && (NB == 1 || NB == 2), "WS scan: 8-KB tiles of four blocks at DP = 32");
+    // TPS tiles per barrier step: at step p the MFMA waves run tiles TPS p ..
+    // TPS p + TPS - 1 and the book waves book step p - 1's.  Maxima slot:
+    // [pair][block][group quad][lane] x 4 floats (the quad's groups); 2 TPS
+    // slots.  Only the MFMA waves load the ring (LPW pieces per tile each,
+    // DAHEAD steps ahead), so the book waves' appends never gate a barrier.
+    constexpr int TPS = NRK_SCAN_WS_TPS, NMX = 2 * TPS, LPW = NPC / NPW, DAHEAD = NSL / TPS - 1;
+    static_assert(NSL % TPS == 0 && DAHEAD >= 1, "ring of whole steps, one step ahead at least");
+    constexpr int MXP = TB * 2 * 1024, MXS = NPW * MXP;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NSL * TILE_BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t mxb[NMX * MXS];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const bool mfma_role = wv < NPW;
+    const int pw = wv & (NPW - 1);
+    const int ubase = (int)blockIdx.x * (NPW * UG * 32) + pw * (UG * 32);
+#if NRK_SCAN_STAMP
+    // dev stamps (waves 0 and 4): 0 sync; MFMA wave: 1 tile, 7 maxima write
+    // + issue, 2 end; book wave: 1 maxima read, 2 appends, 4 inserts, 5 loop
+    uint64_t sstp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t_prev = __builtin_readcyclecounter();
+    auto stamp_out = [&]() {
+        if ((threadIdx.x == 0 || threadIdx.x == NRK_SCAN_WS_STAMPW * 64) && blockIdx.x < 1024)
+            for (int c = 0; c < 8; ++c) scan_stamps[blockIdx.x * 16 + (threadIdx.x ? 8 : 0) + c] = sstp[c];
+    };
+#endif
+
+    const int nblk = (n_items + 31) >> 5;
+    const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk * BLOCK_BYTES);
+    const float vmax = hdr->max_norm, sv_scale = hdr->scale, dvmax = hdr->max_dnorm;
+    const int jk = (k + 1) / 2 - 1;
+    const int n_main = tile_hi - tile_lo, nseq = n_pre + n_main;
+    auto seq = [&](int i) { return i < n_pre ? tile_lo + i * pstride : tile_lo + (i - n_pre); };
+
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
+    const uint32_t mx_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(mxb) +
+                             (uint32_t)(pw * MXP) + lane * 16;
+    const int body_bytes = nblk * BLOCK_BYTES;
+    const int tail_blk = n_items >> 5;
+    const int full_tiles = tail_blk / TB;
+    const int last_tile = (nblk - 1) / TB;
+    // MFMA wave wv loads pieces LPW wv .. LPW wv + LPW - 1 of every tile (see
+    // ip_scan_seg's issue_tile)
+    auto issue_tile = [&](int tt, int sl) {
+        const uint32_t ttc = (uint32_t)min(tt, last_tile);
+#pragma unroll
+        for (int c = 0; c < LPW; ++c) {
+            const int piece = wv * LPW + c;
+            uint32_t off = ttc * (uint32_t)TILE_BYTES + (uint32_t)piece * 1024u;
+            off = off < (uint32_t)body_bytes ? off : (uint32_t)body_bytes - 1024u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(catalog + off + lane * 16),
+                (__attribute__((address_space(3))) void*)(smem + sl * TILE_BYTES + piece * 1024), 16, 0, 0);
+        }
+    };
+    auto issue_step = [&](int p) {  // the TPS tiles of step p (past the end: dummies, uniform vmcnt)
+#pragma unroll
+        for (int t = 0; t < TPS; ++t) {
+            const int i = TPS * p + t;
+            issue_tile(seq(min(i, nseq - 1)), i % NSL);
+        }
+    };
+    // MFMA waves: own pieces of this step's tiles landed (DAHEAD - 1 steps
+    // still in flight), the previous step's maxima written; book waves: their
+    // maxima reads done.  Then the barrier publishes both.
+    auto sync = [&]() {
+        if (mfma_role) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(LPW * TPS * (DAHEAD - 1)) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    const int NP = (nseq + TPS - 1) / TPS;  // steps
+
+    if (mfma_role) {
+        // ---------------------------------------------------- MFMA waves --
+        f16x8 ufrag[UG][DS];
+#pragma unroll
+        for (int g = 0; g < UG; ++g) {
+            float eps, scl;
+            bool live;
+            scan_user_setup<DS>(users, n_users, dim, ubase + g * 32 + q, h, vmax, dvmax, sv_scale, ufrag[g], eps, scl,
+                                live);
+        }
+#if NRK_SCAN_WS_PRIO
+        __builtin_amdgcn_s_setprio(NRK_SCAN_WS_PRIO);
+#endif
+        const uint32_t lds0 = lds_base + lane * 16;
+        auto pf_issue = [&](int sl, int b, u32x4 (&af)[DS]) {
+            const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
+            asm volatile("ds_read_b128 %0, %2 offset:0\n\tds_read_b128 %1, %2 offset:1024"
+                         : "=&v"(af[0]), "=&v"(af[1])
+                         : "v"(base)
+                         : "memory");
+        };
+        auto pf_wait_issue = [&](u32x4 (&cur)[DS], int sl, int b, u32x4 (&nxt)[DS]) {
+            const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b128 %0, %4 offset:0\n\tds_read_b128 %1, %4 offset:1024"
+                         : "=&v"(nxt[0]), "=&v"(nxt[1]), "+v"(cur[0]), "+v"(cur[1])
+                         : "v"(base)
+                         : "memory");
+        };
+        auto pf_wait = [&](u32x4 (&cur)[DS]) {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1])::"memory");
+        };
+        // tile tt in ring slot sl -> the half-block maxima, written to maxima
+        // slot ms block by block (software pipeline of ip_scan_seg's tile():
+        // step j = (block, group) issues its MFMAs while step j - 2 reduces;
+        // block b's maxima are complete after step 8 b + 9)
+        // NT tiles (tt[t] in ring slot sl[t], maxima to slot ms[t]) as one
+        // software pipeline over their NT TB blocks: no refill between them
+        auto tile = [&](auto nt_c, const int (&tt)[TPS], const int (&sl)[TPS], const uint32_t (&ms)[TPS],
+                        auto mask_c) __attribute__((always_inline)) {
+            constexpr int NT = decltype(nt_c)::value, NBK = NT * TB;
+            constexpr bool MASK = decltype(mask_c)::value;
+            float mx[2][UG];  // by block parity
+            // the half-block max of a step's 16 accumulators in two levels:
+            // red1 (6 VALU) folds them into 5 partial maxima, red2 (2 VALU)
+            // finishes; step j issues its first MFMA, then step j - 2's red2,
+            // its second MFMA, then step j - 1's red1 -- red1 reads an
+            // accumulator whose last MFMA is two issue slots back (no hazard
+            // wait states), each gap's VALU fits the MFMA's 32 cycles, and only
+            // two accumulator sets are live
+            using P5 = float[5];
+            auto red1 = [&](const f32x16& a, int bb, P5& pm) __attribute__((always_inline)) {
+                float x[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    x[r] = a[r];
+                    if constexpr (MASK) {
+                        const int row = (tt[bb / TB] * TB + bb % TB) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (row >= n_items) x[r] = -INFINITY;
+                    }
+                }
+                auto m3 = [](float p, float s, float u) { return fmaxf(fmaxf(p, s), u); };
+                pm[0] = m3(x[0], x[1], x[2]);
+                pm[1] = m3(x[3], x[4], x[5]);
+                pm[2] = m3(x[6], x[7], x[8]);
+                pm[3] = m3(x[9], x[10], x[11]);
+                pm[4] = fmaxf(m3(x[12], x[13], x[14]), x[15]);
+            };
+            auto red2 = [&](const P5& pm, int bb, int gg) __attribute__((always_inline)) {
+                mx[bb & 1][gg] = fmaxf(fmaxf(fmaxf(fmaxf(pm[0], pm[1]), pm[2]), pm[3]), pm[4]);  // 2 v_max3
+            };
+            auto put = [&](int bb) __attribute__((always_inline)) {
+                const f32x4 v0 = {mx[bb & 1][0], mx[bb & 1][1], mx[bb & 1][2], mx[bb & 1][3]};
+                const f32x4 v1 = {mx[bb & 1][4], mx[bb & 1][5], mx[bb & 1][6], mx[bb & 1][7]};
+                asm volatile("ds_write_b128 %0, %1 offset:0\n\tds_write_b128 %0, %2 offset:1024" ::"v"(
+                                 ms[bb / TB] + (uint32_t)((bb % TB) * 2048)),
+                             "v"(v0), "v"(v1)
+                             : "memory");
+            };
+            auto slb = [&](int bb) { return sl[bb / TB]; };
+            constexpr int NSTEP = NBK * UG;
+            if constexpr (SCAN_WS_R3) {
+                // R3: three accumulator sets; each step's 8 reduction VALU split
+                // 4 + 4 over the two MFMA gaps: after step j's second MFMA,
+                // red_a(j - 1) folds acc[0..11] of step j - 1 into 4 partials;
+                // after step j + 1's first MFMA, red_b(j - 1) folds the rest
+                // (acc[12..15], three MFMAs back) and the partials into its max.
+                // Fragments double-buffered by block parity (no copies).
+                f32x16 acc[3];
+                float pa[2][4];
+                u32x4 af[2][DS];
+                auto red_a = [&](const f32x16& A, int jj) __attribute__((always_inline)) {
+                    float x[12];
+#pragma unroll
+                    for (int r = 0; r < 12; ++r) {
+                        x[r] = A[r];
+                        if constexpr (MASK) {
+                            const int bb = jj / UG;
+                            const int row = (tt[bb / TB] * TB + bb % TB) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                            if (row >= n_items) x[r] = -INFINITY;
+                        }
+                    }
+                    auto m3 = [](float p, float s, float u) { return fmaxf(fmaxf(p, s), u); };
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) pa[jj & 1][c] = m3(x[3 * c], x[3 * c + 1], x[3 * c + 2]);
+                };
+                auto red_b = [&](const f32x16& A, int jj) __attribute__((always_inline)) {
+                    float x[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        x[r] = A[12 + r];
+                        if constexpr (MASK) {
+                            const int bb = jj / UG, rr = 12 + r;
+                            const int row = (tt[bb / TB] * TB + bb % TB) * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
+                            if (row >= n_items) x[r] = -INFINITY;
+                        }
+                    }
+                    auto m3 = [](float p, float s, float u) { return fmaxf(fmaxf(p, s), u); };
+                    const float* q = pa[jj & 1];
+                    const float y0 = m3(x[0], x[1], x[2]), y1 = m3(q[0], q[1], q[2]);
+                    mx[(jj / UG) & 1][jj % UG] = m3(y0, y1, fmaxf(q[3], x[3]));
+                };
+                pf_issue(slb(0), 0, af[0]);
+                static_for<NBK>([&](auto bc) {
+                    constexpr int bb = decltype(bc)::value, cur = bb & 1;
+                    if constexpr (bb + 1 < NBK) pf_wait_issue(af[cur], slb(bb + 1), (bb + 1) % TB, af[cur ^ 1]);
+                    else pf_wait(af[cur]);
+                    static_for<UG>([&](auto gc) {
+                        constexpr int g = decltype(gc)::value, j = bb * UG + g;
+                        f32x16& A = acc[j % 3];
+                        A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, af[cur][0]), ufrag[g][0],
+                                                                   f32x16{}, 0, 0, 0);
+                        if constexpr (j >= 2) red_b(acc[(j - 2) % 3], j - 2);
+                        if constexpr (!MASK) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                            if constexpr (j >= 2) __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+                        }
+                        A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, af[cur][1]), ufrag[g][1], A,
+                                                                   0, 0, 0);
+                        if constexpr (j >= 1) red_a(acc[(j - 1) % 3], j - 1);
+                        if constexpr (bb > 0 && g == 2) put(bb - 1);  // block bb - 1 complete (its last red_b at g = 1)
+                        if constexpr (!MASK) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                            if constexpr (j >= 1) __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    });
+                });
+                red_b(acc[(NSTEP - 2) % 3], NSTEP - 2);
+                red_a(acc[(NSTEP - 1) % 3], NSTEP - 1);
+                red_b(acc[(NSTEP - 1) % 3], NSTEP - 1);
+                put(NBK - 1);
+                return;
+            }
+            f32x16 acc[2];
+            float pm[2][5];  // partial maxima by step parity
+            u32x4 afp[DS], afb[DS];
+            pf_issue(slb(0), 0, afp);
+            static_for<NBK>([&](auto bc) {
+                constexpr int bb = decltype(bc)::value;
+                u32x4 afn[DS];
+                if constexpr (bb + 1 < NBK) pf_wait_issue(afp, slb(bb + 1), (bb + 1) % TB, afn);
+                else pf_wait(afp);
+#pragma unroll
+                for (int s = 0; s < DS; ++s) afb[s] = afp[s];
+                if constexpr (bb + 1 < NBK) {
+#pragma unroll
+                    for (int s = 0; s < DS; ++s) afp[s] = afn[s];
+                }
+                static_for<UG>([&](auto gc) {
+                    constexpr int g = decltype(gc)::value, j = bb * UG + g;
+                    f32x16& A = acc[j & 1];
+                    A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[0]), ufrag[g][0],
+                                                               f32x16{}, 0, 0, 0);
+                    if constexpr (j >= 2 && !NRK_SCAN_WS_NORED) red2(pm[j & 1], (j - 2) / UG, (j - 2) % UG);
+                    if constexpr (!MASK) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        if constexpr (j >= 2) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                    }
+                    A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[1]), ufrag[g][1], A, 0,
+                                                               0, 0);
+                    if constexpr (j >= 1 && !NRK_SCAN_WS_NORED) red1(acc[(j - 1) & 1], (j - 1) / UG, pm[(j - 1) & 1]);
+                    if constexpr (bb > 0 && g == 2) put(bb - 1);  // block bb - 1 complete (its last red2 at g = 1)
+                    if constexpr (!MASK) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        if constexpr (j >= 1) __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                });
+            });
+            red2(pm[(NSTEP - 2) & 1], (NSTEP - 2) / UG, (NSTEP - 2) % UG);
+            red1(acc[(NSTEP - 1) & 1], (NSTEP - 1) / UG, pm[(NSTEP - 1) & 1]);
+            red2(pm[(NSTEP - 1) & 1], (NSTEP - 1) / UG, (NSTEP - 1) % UG);
+            put(NBK - 1);
+        };
+#pragma unroll
+        for (int p = 0; p < DAHEAD; ++p) issue_step(p);
+        for (int p = 0; p <= NP; ++p) {
+            SC_STAMP(7);
+            sync();
+            SC_STAMP(0);
+            issue_step(p + DAHEAD);
+            int tts[TPS], sls[TPS];
+            uint32_t mss[TPS];
+#pragma unroll
+            for (int t = 0; t < TPS; ++t) {
+                const int i = min(TPS * p + t, nseq - 1);
+                tts[t] = seq(i);
+                sls[t] = (TPS * p + t) % NSL;
+                mss[t] = mx_base + (uint32_t)(((p & 1) * TPS + t) * MXS);
+            }
+            if (TPS * p + TPS <= nseq) {  // a whole step: one pipeline over its TPS tiles
+                bool full = true;
+#pragma unroll
+                for (int t = 0; t < TPS; ++t) full = full && tts[t] < full_tiles;
+                if (full) tile(std::integral_constant<int, TPS>{}, tts, sls, mss, std::false_type{});
+                else tile(std::integral_constant<int, TPS>{}, tts, sls, mss, std::true_type{});
+            } else if (TPS * p < nseq) {  // a short last step: its first tile
+                tile(std::integral_constant<int, 1>{}, tts, sls, mss, std::true_type{});
+            }
+            SC_STAMP(1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if NRK_SCAN_STAMP
+        SC_STAMP(2);
+        stamp_out();
+#endif
+        return;
+    }
+
+    // --------------------------------------------------------- book waves --
+    // book wave wv books groups [gb, gb + UGB) of pair pw
+    const int gb = ((wv - NPW) / NPW) * UGB;
+    float eps_s[UGB], tau[UGB];
+    float t[UGB][MT];
+    bool live[UGB];
+#pragma unroll
+    for (int g = 0; g < UGB; ++g) {
+        f16x8 uf[DS];
+        float eps, scl;
+        const int user = ubase + (gb + g) * 32 + q;
+        scan_user_setup<DS>(users, n_users, dim, user, h, vmax, dvmax, sv_scale, uf, eps, scl, live[g]);
+        eps_s[g] = eps * scl;
+        if (h == 0 && user < n_users) uinfo[user] = make_float4(-INFINITY, eps_s[g], scl, eps);
+        tau[g] = live[g] ? -FLT_MAX : INFINITY;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) t[g][i] = (live[g] && i >= MT - 1 - jk) ? -INFINITY : INFINITY;
+    }
+    uint2* const wapp = app + (size_t)(ubase + gb * 32) * 2 * (size_t)m2;
+    const uint32_t pos0 = (uint32_t)(q * 2 + h) * (uint32_t)m2;  // group 0's first slot
+    const uint32_t gstride = 64u * (uint32_t)m2;                  // + g * gstride for group g
+    uint32_t pos[UGB];
+#pragma unroll
+    for (int g = 0; g < UGB; ++g) pos[g] = pos0 + (uint32_t)g * gstride;
+    auto slot = [&](uint32_t x, int g) { return min(x, pos0 + (uint32_t)g * gstride + (uint32_t)m2 - 1u); };
+    auto app_store_if = [&](uint64_t m, uint32_t e, uint2 v) {
+        const uint32_t off = e << 3;
+        const uint64_t d = ((uint64_t)v.y << 32) | v.x;
+        uint64_t sv;
+        asm volatile(
+            "s_and_saveexec_b64 %0, %1\n\t"
+            "global_store_dwordx2 %2, %3, %4\n\t"
+            "s_mov_b64 exec, %0"
+            : "=&s"(sv)
+            : "s"(m), "v"(off), "v"(d), "s"(wapp)
+            : "memory", "scc");
+    };
+    auto retau = [&](int g) {
+        const float lb = pair_min32(t[g][MT - 1]);
+        const float c = lb - 2.0f * eps_s[g];
+        const float tv = fmaxf(__builtin_fmaf(fabsf(c), -0x1p-22f, c) - 0x1p-120f, -FLT_MAX);
+        tau[g] = live[g] ? tv : INFINITY;
+    };
+    int next_s = n_pre > 0 ? tile_lo : INT_MAX, left_s = n_pre;
+#if NRK_SCAN_WS_BPRIO
+    __builtin_amdgcn_s_setprio(NRK_SCAN_WS_BPRIO);
+#endif
+#if NRK_SCAN_WS_YPRIO  // the younger book waves (8 - 11) lose every age tie
+    if (wv >= 2 * NPW) __builtin_amdgcn_s_setprio(NRK_SCAN_WS_YPRIO);
+#endif
+#if NRK_SCAN_STAMP
+    t_prev = __builtin_readcyclecounter();
+#endif
+    const uint32_t mq = mx_base + (uint32_t)(gb / 4) * 1024u;  // this wave's first group quad
+    // r[b][c]: block b's maxima of group quad c of this wave
+    f32x4 rr[TPS][TB][UGB / 4];
+    auto read_issue = [&](int t, uint32_t a) {
+        if constexpr (NB == 2) {
+            asm volatile(
+                "ds_read_b128 %0, %4 offset:0\n\tds_read_b128 %1, %4 offset:2048\n\t"
+                "ds_read_b128 %2, %4 offset:4096\n\tds_read_b128 %3, %4 offset:6144"
+                : "=&v"(rr[t][0][0]), "=&v"(rr[t][1][0]), "=&v"(rr[t][2][0]), "=&v"(rr[t][3][0])
+                : "v"(a)
+                : "memory");
+        } else {
+            asm volatile(
+                "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:1024\n\t"
+                "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
+                "ds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:5120\n\t"
+                "ds_read_b128 %6, %8 offset:6144\n\tds_read_b128 %7, %8 offset:7168"
+                : "=&v"(rr[t][0][0]), "=&v"(rr[t][0][1]), "=&v"(rr[t][1][0]), "=&v"(rr[t][1][1]),
+                  "=&v"(rr[t][2][0]), "=&v"(rr[t][2][1]), "=&v"(rr[t][3][0]), "=&v"(rr[t][3][1])
+                : "v"(a)
+                : "memory");
+        }
+    };
+    // tile t's reads landed with `left' later reads still in flight (LDS
+    // reads return in order: left = 0 or the reads of one more tile, TPS <= 2);
+    // the wait ties rr[t], so nothing copies it earlier
+    static_assert(TPS <= 2, "read_wait");
+    auto read_wait = [&](int t, bool left) {
+        constexpr int L1 = TB * (UGB / 4);
+        if constexpr (NB == 2) {
+            if (left)
+                asm volatile("s_waitcnt lgkmcnt(%4)"
+                             : "+v"(rr[t][0][0]), "+v"(rr[t][1][0]), "+v"(rr[t][2][0]), "+v"(rr[t][3][0])
+                             : "n"(L1)
+                             : "memory");
+            else
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(rr[t][0][0]), "+v"(rr[t][1][0]), "+v"(rr[t][2][0]), "+v"(rr[t][3][0])::"memory");
+        } else {
+            if (left)
+                asm volatile("s_waitcnt lgkmcnt(%8)"
+                             : "+v"(rr[t][0][0]), "+v"(rr[t][0][1]), "+v"(rr[t][1][0]), "+v"(rr[t][1][1]),
+                               "+v"(rr[t][2][0]), "+v"(rr[t][2][1]), "+v"(rr[t][3][0]), "+v"(rr[t][3][1])
+                             : "n"(L1)
+                             : "memory");
+            else
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(rr[t][0][0]), "+v"(rr[t][0][1]), "+v"(rr[t][1][0]), "+v"(rr[t][1][1]),
+                               "+v"(rr[t][2][0]), "+v"(rr[t][2][1]), "+v"(rr[t][3][0]), "+v"(rr[t][3][1])::"memory");
+        }
+    };
+    // inserts every INSP tiles (INSP a multiple of TPS, or 1)
+    constexpr int INSP = NRK_SCAN_WS_INSP;
+    static_assert(INSP == 1 || (INSP % TPS == 0 && (INSP & (INSP - 1)) == 0), "insert period");
+    float vtp[UGB];  // INSP > 1: the largest tile maximum since the last insert, per group (-inf: none)
+#pragma unroll
+    for (int g = 0; g < UGB; ++g) vtp[g] = -INFINITY;
+    for (int p = 0; p <= NP; ++p) {
+        SC_STAMP(5);
+        sync();
+        SC_STAMP(0);
+        if (p == 0) continue;
+        const int p1 = p - 1;
+#pragma unroll
+        for (int t = 0; t < TPS; ++t)
+            if (TPS * p1 + t < nseq) read_issue(t, mq + (uint32_t)(((p1 & 1) * TPS + t) * MXS));
+        static_for<TPS>([&](auto tc) {
+        constexpr int T = decltype(tc)::value;
+        const int j = TPS * p1 + T;
+        if (j >= nseq) return;
+        read_wait(T, T + 1 < TPS && j + 1 < nseq);  // tile T + 1's reads may stay in flight
+        const int tt = seq(j);
+        const bool pre = j < n_pre;
+        if (j == n_pre) {  // the first main-pass tile: tau from the pre-pass lists
+#pragma unroll
+            for (int g = 0; g < UGB; ++g) retau(g);
+        }
+        bool ins_ok = true;
+        if (!pre && tt == next_s) {  // a sampled tile: its maxima are in the lists already
+            ins_ok = false;
+            next_s = --left_s > 0 ? next_s + pstride : INT_MAX;
+        }
+        const auto& r = rr[T];
+        SC_STAMP(1);
+#if NRK_SCAN_WS_FLOOR  // dev timing floor: the book waves only read the maxima
+        if (r[0][0][0] != 12345.0f) return;
+#endif
+        const uint32_t hb0 = (uint32_t)(tt * TB * 2) + (uint32_t)h;
+        // group g of the tile; BF: no branch on the lane masks (a store with
+        // no lane is a no-op, an insert of -inf changes nothing, retau is
+        // idempotent)
+        static_for<UGB>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            float mx[TB];
+#pragma unroll
+            for (int b = 0; b < TB; ++b) mx[b] = r[b][g / 4][g % 4];
+            const float vt = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
+            if (!pre) {
+                // appends (ip_scan_seg's BSEL form): every half-block max >= tau
+                uint64_t am[TB], gm = 0, multi = 0;
+#pragma unroll
+                for (int b = 0; b < TB; ++b) {
+                    am[b] = __builtin_amdgcn_ballot_w64(mx[b] >= tau[g]);
+                    multi |= gm & am[b];
+                    gm |= am[b];
+                }
+                if (SCAN_WS_BF || gm) {
+                    const uint32_t fid = (first_set_block<TB>(am) << 1) + hb0;
+                    const uint32_t p0 = pos[g];
+                    app_store_if(gm, slot(p0, g), make_uint2(__float_as_uint(vt), fid));
+                    uint32_t p = add_if(p0, gm);
+                    if (multi) {
+                        p = p0;
+#pragma unroll
+                        for (int b = 0; b < TB; ++b) {
+                            app_store_if(am[b] & multi, slot(p, g), make_uint2(__float_as_uint(mx[b]), hb0 + 2u * b));
+                            p = add_if(p, am[b]);
+                        }
+                    }
+                    pos[g] = p;
+                }
+            }
+            SC_STAMP(2);
+            if (INSP > 1 && pre) {
+                // pre-pass tiles insert every tile (they fill the list)
+                const bool in = vt > t[g][MT - 1];
+                if (__builtin_amdgcn_ballot_w64(in)) top_insert<MT>(t[g], in ? vt : -INFINITY);
+            } else if constexpr (INSP > 1) {
+                // main pass: one insert per INSP tiles, the largest of their
+                // tile maxima (a sampled tile's counts as -inf); the list stays
+                // a set of distinct appended half-block maxima, so its (jk +
+                // 1)-th largest stays a lower bound -- only tau lags by < INSP
+                // tiles
+                const float vi = fmaxf(ins_ok ? vt : -INFINITY, vtp[g]);
+                if (T + 1 < TPS || (INSP > TPS && ((j - n_pre) & (INSP - 1)) < INSP - TPS)) {
+                    vtp[g] = vi;
+                } else {
+                    vtp[g] = -INFINITY;
+                    const bool in = vi > t[g][MT - 1];
+                    if (__builtin_amdgcn_ballot_w64(in)) {
+                        top_insert<MT>(t[g], in ? vi : -INFINITY);
+                        if (!pre) retau(g);
+                    }
+                }
+            } else if (ins_ok) {
+                const bool in = vt > t[g][MT - 1];
+                if (SCAN_WS_BF || __builtin_amdgcn_ballot_w64(in)) {
+                    top_insert<MT>(t[g], in ? vt : -INFINITY);
+                    if (!pre) retau(g);
+                }
+            }
+            SC_STAMP(4);
+        });
+        });
+    }
+    if constexpr (INSP > 1) {  // the maxima since the last insert
+#pragma unroll
+        for (int g = 0; g < UGB; ++g) {
+            const bool in = vtp[g] > t[g][MT - 1];
+            top_insert<MT>(t[g], in ? vtp[g] : -INFINITY);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if NRK_SCAN_STAMP
+    SC_STAMP(3);
+    stamp_out();
+#endif
+#pragma unroll
+    for (int g = 0; g < UGB; ++g) {
+        const float lb = pair_min32(t[g][MT - 1]);
+        const int user = ubase + (gb + g) * 32 + q;
+        if (user < n_users) {
+            acnt[(size_t)user * 2 + h] = (int)(pos[g] - (pos0 + (uint32_t)g * gstride));
+            if (h == 0) reinterpret_cast<float*>(uinfo + user)[0] = live[g] ? lb : -INFINITY;
+        }
+    }
+    if constexpr (MT <= 32) {
+        if (bnd != nullptr) {
+#pragma unroll
+            for (int g = 0; g < UGB; ++g)
+                list_bound_out<MT>(t[g], live[g], h, ubase + (gb + g) * 32 + q, n_users, jk, bnd, bnd_m, uinfo);
+        }
     }
 }
 
@@ -2791,6 +3451,12 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
     constexpr int WG_CU = (WPE * 4) / NW > 0 ? (WPE * 4) / NW : 1;
     const int slots = n_cus() * WG_CU, nub = (int)grid;
     w.flat_used = false;
+    if constexpr (SCAN_WS && DP == 32 && MT == 16 && NW == 8 && UG == 4) {
+        // the warp-specialized form of this variant (same users per workgroup)
+        ip_scan_ws_kernel<DP, NSL, MT, SCAN_WS_NB><<<grid, 256 * (1 + SCAN_WS_NB), 0, s>>>(users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt,
+                                                           w.uinfo, t_lo, t_hi, n_pre, pstride, w.bnd, w.bnd_m);
+        return;
+    }
     if (SCAN_FLAT && w.flat_ok && w.bnd == nullptr && nub < slots && n >= 64) {
         const int E = slots - nub, c = (nub + E - 1) / E;
         const int head = (int)(((int64_t)c * n + c) / (c + 1));  // ceil(c n / (c + 1))
