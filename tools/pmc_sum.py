@@ -1,24 +1,31 @@
-#!/usr/bin/env python3
-"""dev: mean per-dispatch counter values of the kernels whose name contains
-PATTERN, from a rocprofv3 --pmc csv directory.  usage: pmc_sum.py DIR PATTERN"""
+"""Average every counter per kernel over the passes under DIR (dev tool).
+usage: pmc_sum.py DIR REGEX"""
 import csv
 import glob
 import os
+import re
 import sys
 from collections import defaultdict
 
-d, pat = sys.argv[1], sys.argv[2]
-files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-vals = defaultdict(lambda: defaultdict(list))
-for f in files:
-    with open(f) as fh:
-        for r in csv.DictReader(fh):
-            name = r.get("Kernel_Name", "")
-            if pat not in name:
-                continue
-            key = name.split("(")[0][:70]
-            vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, cs in vals.items():
-    print(k)
-    for c, v in sorted(cs.items()):
-        print(f"  {c:28s} n={len(v):3d} mean={sum(v) / len(v):.4g}")
+
+def main(root, pat):
+    per = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        disp = defaultdict(lambda: defaultdict(float))
+        names = {}
+        for r in csv.DictReader(open(f)):
+            d = (f, int(r["Dispatch_Id"]))
+            names[d] = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            disp[d][r["Counter_Name"]] += float(r["Counter_Value"])
+        for d, cs in disp.items():
+            if re.search(pat, names[d]):
+                for c, v in cs.items():
+                    per[names[d]][c].append(v)
+    for k, cs in sorted(per.items()):
+        print(k[:90])
+        for c, v in sorted(cs.items()):
+            print(f"   {c:24s} {sum(v) / len(v):16.1f}  (n={len(v)})")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:3])
