@@ -27,7 +27,7 @@ layouts are BASELINE's (layout_plan):
 The timed regions are bracketed by barriers and the max over ranks is used.
 
 Extra fields on the JSON line: "roofline" for the dominant kernel (the
-fp16 MFMA screen, ip_scan_kernel), "cpu_baseline" (the oracle's per-user
+fp16 MFMA screen, ip_scan_ws_kernel), "cpu_baseline" (the oracle's per-user
 exact scan -- the reference's nq=1 IndexFlatIP shape -- on a bounded user
 sample, rank 0, N=1), "din" (BASELINE config 3, DIN scored pairs/s),
 "itemcf" and "plugins" (N=1 only).
@@ -53,8 +53,9 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04_traffic.json")
-BUSY_FILE = os.path.join(REPO, "profiles", "r04_busy.json")
+PROFILE_ROUND = "r05"
+TRAFFIC_FILE = os.path.join(REPO, "profiles", PROFILE_ROUND + "_traffic.json")
+BUSY_FILE = os.path.join(REPO, "profiles", PROFILE_ROUND + "_busy.json")
 CSRC = os.path.join(REPO, "news-recommendation-tc_amd", "csrc")
 
 
@@ -667,7 +668,7 @@ def run_din(args, device, rank, world):
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": din_traffic,
                         "traffic_unit": "bytes per pass, every launch of one nrk_din_forward_segments call "
-                                        "(profiles/r04_traffic.json din_pass)",
+                                        "(profiles/" + PROFILE_ROUND + "_traffic.json din_pass)",
                         "kernel": f"nrk_din_forward_segments ({n_loc} samples in Dice batches of {B}, one call)",
                         "kernel_ms": round(pass_ms, 4),
                         "algorithmic_bytes_per_launch": DIN_BYTES_PER_PAIR * n_loc,
@@ -1007,24 +1008,26 @@ def main(argv=None):
     kernel_ms = screen_ms if catalog_mode else scan_ms
     achieved = flops / (kernel_ms * 1e-3) / 1e12
     default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and world == 1
-    traffic = pmc_traffic(["nrk::ip_scan_kernel<"], default_cfg)
+    # the config-2 scan runs the warp-specialized kernel (ip_scan_ws_kernel)
+    # unless built with -DNRK_SCAN_WS=0
+    traffic = pmc_traffic(["nrk::ip_scan_ws_kernel<"], default_cfg) or pmc_traffic(["nrk::ip_scan_kernel<"], default_cfg)
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                 "traffic": round(traffic) if traffic else None,
-                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r04_traffic.json; "
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/" + PROFILE_ROUND + "_traffic.json; "
                                 "null when absent or measured on other kernel sources)",
-                "kernel": ("ip_scan_kernel (fp16 MFMA 32x32x16 screen) + ip_shard_bound_kernel + bound all_gather, "
+                "kernel": ("ip_scan_ws_kernel (warp-specialized fp16 MFMA 32x32x16 screen) + bound all_gather, "
                            "this rank's item blocks" if catalog_mode else
-                           "ip_scan_kernel (fp16 MFMA 32x32x16 screen), HIP events around its launch"),
+                           "ip_scan_ws_kernel (warp-specialized fp16 MFMA 32x32x16 screen), HIP events around its launch"),
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_flop_per_launch": flops,
                 # the same flops over the whole timed step (tower + scan + select + finish on
                 # one GPU; this rank's screen share over the slowest rank's step at N > 1):
                 # the roofline fraction ``value`` itself achieves
                 "step_frac": round(flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-                "busy": pmc_busy(["nrk::ip_scan_kernel", "nrk::ip_select_kernel", "nrk::ip_refine_kernel",
+                "busy": pmc_busy(["nrk::ip_scan_ws_kernel", "nrk::ip_select_kernel", "nrk::ip_refine_kernel",
                                   "nrk::tt_user_kernel"], default_cfg),
-                "busy_source": "profiles/r04_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
+                "busy_source": "profiles/" + PROFILE_ROUND + "_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
                                "SQ_WAIT_ANY, GRBM_GUI_ACTIVE passes; tools/pmc_busy.py, calibrated by "
                                "tools/calib)"}
 
