@@ -328,7 +328,11 @@ constexpr bool SCAN_FLAT = NRK_SCAN_FLAT;
 #ifndef NRK_SCAN_PRE_DIV
 #define NRK_SCAN_PRE_DIV 6
 #endif
-constexpr int SCAN_PRE_MAX = NRK_SCAN_PRE_MAX, SCAN_PRE_MIN = 128, SCAN_PRE_DIV = NRK_SCAN_PRE_DIV;
+#ifndef NRK_SCAN_SHARD_PRE_DIV
+#define NRK_SCAN_SHARD_PRE_DIV 6
+#endif
+constexpr int SCAN_PRE_MAX = NRK_SCAN_PRE_MAX, SCAN_PRE_MIN = 128, SCAN_PRE_DIV = NRK_SCAN_PRE_DIV,
+              SCAN_SHARD_PRE_DIV = NRK_SCAN_SHARD_PRE_DIV;
 // (lane bit of m) ? T : F, one v_cndmask_b32 on the compare's SGPR lane mask
 // with inline constants (0..64); sel_mask_v: (lane bit of m) ? T : f
 template <int F, int T>
@@ -1308,44 +1312,32 @@ __device__ __forceinline__ void scan_user_setup(const float* __restrict__ users,
     live = active && nrm2 > 0.0f;
 }
 
-// Warp-specialized scan (WS): the same one-pass screen as ip_scan_seg (same
-// lists, taus, appended entries and bounds, bit for bit) with the work of a
-// SIMD split between its two waves instead of both doing both halves.
-// Waves 0-3 (one per SIMD, the MFMA waves) run every MFMA of a tile for 256
-// users (8 groups) and write the half-block maxima (8 groups x TB per lane)
-// to an LDS slot; waves 4-7 (the book waves, one per SIMD) read the previous
-// tile's maxima of the same 256 users and do the appends and list inserts.
-// Per tile barrier the MFMA wave of a SIMD issues 64 back-to-back MFMAs with
-// its reductions in their shadows, and the book wave's VALU fills the issue
-// slots beside them -- the matrix pipe no longer waits for either wave's
-// bookkeeping (round 5, config 2: the mixed waves spent 46% of their cycles
-// outside the tile).  The pre-pass tiles and the main pass are one tile
-// sequence over one ring; every wave loads one 1-KB piece of every tile.
-// LDS: the NSL-tile ring + 2 maxima slots x 4 pairs x 8 groups x 64 lanes x
-// TB floats (64 KB at TB = 4).
+// Warp-specialized scan (WS, round 5; D = 32, k <= 32: config 2 and every
+// config-4 shard): the one-pass screen of ip_scan_seg -- same lists, taus,
+// append format and list bounds; the appended set differs only by the insert
+// period below -- with the work of a SIMD split by role.  12 waves, 1,024
+// users per workgroup, one workgroup per CU.  Waves 0-3 (one per SIMD, the
+// MFMA waves) hold the fp16 B fragments of 256 users (8 groups), run every
+// MFMA of a tile for them, reduce each (block, group) to the lane's half-block
+// maximum and write the maxima to LDS; they alone load the ring.  Waves 4-11
+// (two book waves per SIMD, 4 groups each) read the maxima one barrier step
+// later and do the appends and list inserts, so the matrix pipe never waits
+// for bookkeeping and an append store never gates a barrier.  One barrier per
+// step of TPS = 2 tiles (the MFMA waves pipeline both tiles as one block
+// sequence); main-pass inserts every insp tiles (the largest tile maximum
+// since the last insert: the list stays a set of distinct appended
+// half-block maxima, so its (jk + 1)-th largest stays a lower bound; only tau
+// lags), pre-pass tiles every tile.  LDS: the 4-tile ring (32 KB) + 2 TPS
+// maxima slots x 4 pairs x 4 blocks x 2 group quads x 64 lanes x 16 B (128 KB).
+// Config 2, one box: 5.08 vs 5.41 ms for ip_scan_kernel.
 #ifndef NRK_SCAN_WS
 #define NRK_SCAN_WS 1
 #endif
 #ifndef NRK_SCAN_WS_PRIO
 #define NRK_SCAN_WS_PRIO 2
 #endif
-#ifndef NRK_SCAN_WS_BF
-#define NRK_SCAN_WS_BF 0
-#endif
-#ifndef NRK_SCAN_WS_BPRIO
-#define NRK_SCAN_WS_BPRIO 0
-#endif
 #ifndef NRK_SCAN_WS_INSP
 #define NRK_SCAN_WS_INSP 8
-#endif
-#ifndef NRK_SCAN_WS_NORED  // dev timing: the MFMA waves skip the reductions
-#define NRK_SCAN_WS_NORED 0
-#endif
-#ifndef NRK_SCAN_WS_R3
-#define NRK_SCAN_WS_R3 0
-#endif
-#ifndef NRK_SCAN_WS_YPRIO
-#define NRK_SCAN_WS_YPRIO 0
 #endif
 #ifndef NRK_SCAN_WS_STAMPW
 #define NRK_SCAN_WS_STAMPW 4
@@ -1360,13 +1352,20 @@ __device__ __forceinline__ void scan_user_setup(const float* __restrict__ users,
 #ifndef NRK_SCAN_WS_NB
 #define NRK_SCAN_WS_NB 2
 #endif
-constexpr bool SCAN_WS = NRK_SCAN_WS, SCAN_WS_BF = NRK_SCAN_WS_BF, SCAN_WS_R3 = NRK_SCAN_WS_R3;
+constexpr bool SCAN_WS = NRK_SCAN_WS;
 constexpr int SCAN_WS_NB = NRK_SCAN_WS_NB;
+#ifndef NRK_SCAN_WS_SHARD_INSP
+#define NRK_SCAN_WS_SHARD_INSP 4
+#endif
+constexpr int SCAN_WS_INSP = NRK_SCAN_WS_INSP, SCAN_WS_SHARD_INSP = NRK_SCAN_WS_SHARD_INSP;
+static_assert((SCAN_WS_INSP & (SCAN_WS_INSP - 1)) == 0 && SCAN_WS_INSP >= 2 &&
+                  (SCAN_WS_SHARD_INSP & (SCAN_WS_SHARD_INSP - 1)) == 0 && SCAN_WS_SHARD_INSP >= 2,
+              "insert periods: powers of two >= the two tiles of a step");
 template <int DP, int NSL, int MT, int NB>
 __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws_kernel(
     const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items, int dim, int k,
     int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt, float4* __restrict__ uinfo, int tile_lo,
-    int tile_hi, int n_pre, int pstride, float* __restrict__ bnd, int bnd_m) {
+    int tile_hi, int n_pre, int pstride, float* __restrict__ bnd, int bnd_m, int insp) {
     constexpr int NPW = 4, UG = 8, UGB = UG / NB, DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
     constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
@@ -1526,79 +1525,6 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
             };
             auto slb = [&](int bb) { return sl[bb / TB]; };
             constexpr int NSTEP = NBK * UG;
-            if constexpr (SCAN_WS_R3) {
-                // R3: three accumulator sets; each step's 8 reduction VALU split
-                // 4 + 4 over the two MFMA gaps: after step j's second MFMA,
-                // red_a(j - 1) folds acc[0..11] of step j - 1 into 4 partials;
-                // after step j + 1's first MFMA, red_b(j - 1) folds the rest
-                // (acc[12..15], three MFMAs back) and the partials into its max.
-                // Fragments double-buffered by block parity (no copies).
-                f32x16 acc[3];
-                float pa[2][4];
-                u32x4 af[2][DS];
-                auto red_a = [&](const f32x16& A, int jj) __attribute__((always_inline)) {
-                    float x[12];
-#pragma unroll
-                    for (int r = 0; r < 12; ++r) {
-                        x[r] = A[r];
-                        if constexpr (MASK) {
-                            const int bb = jj / UG;
-                            const int row = (tt[bb / TB] * TB + bb % TB) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                            if (row >= n_items) x[r] = -INFINITY;
-                        }
-                    }
-                    auto m3 = [](float p, float s, float u) { return fmaxf(fmaxf(p, s), u); };
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) pa[jj & 1][c] = m3(x[3 * c], x[3 * c + 1], x[3 * c + 2]);
-                };
-                auto red_b = [&](const f32x16& A, int jj) __attribute__((always_inline)) {
-                    float x[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        x[r] = A[12 + r];
-                        if constexpr (MASK) {
-                            const int bb = jj / UG, rr = 12 + r;
-                            const int row = (tt[bb / TB] * TB + bb % TB) * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
-                            if (row >= n_items) x[r] = -INFINITY;
-                        }
-                    }
-                    auto m3 = [](float p, float s, float u) { return fmaxf(fmaxf(p, s), u); };
-                    const float* q = pa[jj & 1];
-                    const float y0 = m3(x[0], x[1], x[2]), y1 = m3(q[0], q[1], q[2]);
-                    mx[(jj / UG) & 1][jj % UG] = m3(y0, y1, fmaxf(q[3], x[3]));
-                };
-                pf_issue(slb(0), 0, af[0]);
-                static_for<NBK>([&](auto bc) {
-                    constexpr int bb = decltype(bc)::value, cur = bb & 1;
-                    if constexpr (bb + 1 < NBK) pf_wait_issue(af[cur], slb(bb + 1), (bb + 1) % TB, af[cur ^ 1]);
-                    else pf_wait(af[cur]);
-                    static_for<UG>([&](auto gc) {
-                        constexpr int g = decltype(gc)::value, j = bb * UG + g;
-                        f32x16& A = acc[j % 3];
-                        A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, af[cur][0]), ufrag[g][0],
-                                                                   f32x16{}, 0, 0, 0);
-                        if constexpr (j >= 2) red_b(acc[(j - 2) % 3], j - 2);
-                        if constexpr (!MASK) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                            if constexpr (j >= 2) __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-                        }
-                        A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, af[cur][1]), ufrag[g][1], A,
-                                                                   0, 0, 0);
-                        if constexpr (j >= 1) red_a(acc[(j - 1) % 3], j - 1);
-                        if constexpr (bb > 0 && g == 2) put(bb - 1);  // block bb - 1 complete (its last red_b at g = 1)
-                        if constexpr (!MASK) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                            if constexpr (j >= 1) __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-                            __builtin_amdgcn_sched_barrier(0);
-                        }
-                    });
-                });
-                red_b(acc[(NSTEP - 2) % 3], NSTEP - 2);
-                red_a(acc[(NSTEP - 1) % 3], NSTEP - 1);
-                red_b(acc[(NSTEP - 1) % 3], NSTEP - 1);
-                put(NBK - 1);
-                return;
-            }
             f32x16 acc[2];
             float pm[2][5];  // partial maxima by step parity
             u32x4 afp[DS], afb[DS];
@@ -1619,14 +1545,14 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
                     f32x16& A = acc[j & 1];
                     A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[0]), ufrag[g][0],
                                                                f32x16{}, 0, 0, 0);
-                    if constexpr (j >= 2 && !NRK_SCAN_WS_NORED) red2(pm[j & 1], (j - 2) / UG, (j - 2) % UG);
+                    if constexpr (j >= 2) red2(pm[j & 1], (j - 2) / UG, (j - 2) % UG);
                     if constexpr (!MASK) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                         if constexpr (j >= 2) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
                     }
                     A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[1]), ufrag[g][1], A, 0,
                                                                0, 0);
-                    if constexpr (j >= 1 && !NRK_SCAN_WS_NORED) red1(acc[(j - 1) & 1], (j - 1) / UG, pm[(j - 1) & 1]);
+                    if constexpr (j >= 1) red1(acc[(j - 1) & 1], (j - 1) / UG, pm[(j - 1) & 1]);
                     if constexpr (bb > 0 && g == 2) put(bb - 1);  // block bb - 1 complete (its last red2 at g = 1)
                     if constexpr (!MASK) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1719,12 +1645,6 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
         tau[g] = live[g] ? tv : INFINITY;
     };
     int next_s = n_pre > 0 ? tile_lo : INT_MAX, left_s = n_pre;
-#if NRK_SCAN_WS_BPRIO
-    __builtin_amdgcn_s_setprio(NRK_SCAN_WS_BPRIO);
-#endif
-#if NRK_SCAN_WS_YPRIO  // the younger book waves (8 - 11) lose every age tie
-    if (wv >= 2 * NPW) __builtin_amdgcn_s_setprio(NRK_SCAN_WS_YPRIO);
-#endif
 #if NRK_SCAN_STAMP
     t_prev = __builtin_readcyclecounter();
 #endif
@@ -1779,9 +1699,8 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
                                "+v"(rr[t][2][0]), "+v"(rr[t][2][1]), "+v"(rr[t][3][0]), "+v"(rr[t][3][1])::"memory");
         }
     };
-    // inserts every INSP tiles (INSP a multiple of TPS, or 1)
-    constexpr int INSP = NRK_SCAN_WS_INSP;
-    static_assert(INSP == 1 || (INSP % TPS == 0 && (INSP & (INSP - 1)) == 0), "insert period");
+    // main-pass inserts every insp tiles (a power of two >= TPS; the host's
+    // choice, see launch_scan_v)
     float vtp[UGB];  // INSP > 1: the largest tile maximum since the last insert, per group (-inf: none)
 #pragma unroll
     for (int g = 0; g < UGB; ++g) vtp[g] = -INFINITY;
@@ -1816,9 +1735,7 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
         if (r[0][0][0] != 12345.0f) return;
 #endif
         const uint32_t hb0 = (uint32_t)(tt * TB * 2) + (uint32_t)h;
-        // group g of the tile; BF: no branch on the lane masks (a store with
-        // no lane is a no-op, an insert of -inf changes nothing, retau is
-        // idempotent)
+        // group g of the tile
         static_for<UGB>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
             float mx[TB];
@@ -1834,7 +1751,7 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
                     multi |= gm & am[b];
                     gm |= am[b];
                 }
-                if (SCAN_WS_BF || gm) {
+                if (gm) {
                     const uint32_t fid = (first_set_block<TB>(am) << 1) + hb0;
                     const uint32_t p0 = pos[g];
                     app_store_if(gm, slot(p0, g), make_uint2(__float_as_uint(vt), fid));
@@ -1851,18 +1768,18 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
                 }
             }
             SC_STAMP(2);
-            if (INSP > 1 && pre) {
+            if (pre) {
                 // pre-pass tiles insert every tile (they fill the list)
                 const bool in = vt > t[g][MT - 1];
                 if (__builtin_amdgcn_ballot_w64(in)) top_insert<MT>(t[g], in ? vt : -INFINITY);
-            } else if constexpr (INSP > 1) {
+            } else {
                 // main pass: one insert per INSP tiles, the largest of their
                 // tile maxima (a sampled tile's counts as -inf); the list stays
                 // a set of distinct appended half-block maxima, so its (jk +
                 // 1)-th largest stays a lower bound -- only tau lags by < INSP
                 // tiles
                 const float vi = fmaxf(ins_ok ? vt : -INFINITY, vtp[g]);
-                if (T + 1 < TPS || (INSP > TPS && ((j - n_pre) & (INSP - 1)) < INSP - TPS)) {
+                if (T + 1 < TPS || ((j - n_pre) & (insp - 1)) < insp - TPS) {
                     vtp[g] = vi;
                 } else {
                     vtp[g] = -INFINITY;
@@ -1872,18 +1789,12 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
                         if (!pre) retau(g);
                     }
                 }
-            } else if (ins_ok) {
-                const bool in = vt > t[g][MT - 1];
-                if (SCAN_WS_BF || __builtin_amdgcn_ballot_w64(in)) {
-                    top_insert<MT>(t[g], in ? vt : -INFINITY);
-                    if (!pre) retau(g);
-                }
             }
             SC_STAMP(4);
         });
         });
     }
-    if constexpr (INSP > 1) {  // the maxima since the last insert
+    {  // the maxima since the last insert
 #pragma unroll
         for (int g = 0; g < UGB; ++g) {
             const bool in = vtp[g] > t[g][MT - 1];
@@ -3445,7 +3356,8 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
     // the list pre-pass: up to 64 tiles spread over the range (+2.2% MFMA at
     // config 2, +17% on a config-4 shard, whose appends it cuts by 2/3)
     const int n = t_hi - t_lo;
-    const int n_pre = (IE == 1 && n >= SCAN_PRE_MIN) ? std::min(SCAN_PRE_MAX, n / SCAN_PRE_DIV) : 0;
+    const int pre_div = w.bnd != nullptr ? SCAN_SHARD_PRE_DIV : SCAN_PRE_DIV;  // a catalog shard's own
+    const int n_pre = (IE == 1 && n >= SCAN_PRE_MIN) ? std::min(SCAN_PRE_MAX, n / pre_div) : 0;
     const int pstride = n_pre > 0 ? n / n_pre : 1;
     // FLAT: every workgroup slot of the chip busy (see ip_scan_kernel)
     constexpr int WG_CU = (WPE * 4) / NW > 0 ? (WPE * 4) / NW : 1;
@@ -3453,8 +3365,12 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
     w.flat_used = false;
     if constexpr (SCAN_WS && DP == 32 && MT == 16 && NW == 8 && UG == 4) {
         // the warp-specialized form of this variant (same users per workgroup)
-        ip_scan_ws_kernel<DP, NSL, MT, SCAN_WS_NB><<<grid, 256 * (1 + SCAN_WS_NB), 0, s>>>(users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt,
-                                                           w.uinfo, t_lo, t_hi, n_pre, pstride, w.bnd, w.bnd_m);
+        // a catalog shard (list bounds) inserts more often: its appended
+        // maxima are what the band pass reads
+        const int insp = w.bnd != nullptr ? SCAN_WS_SHARD_INSP : SCAN_WS_INSP;
+        ip_scan_ws_kernel<DP, NSL, MT, SCAN_WS_NB><<<grid, 256 * (1 + SCAN_WS_NB), 0, s>>>(
+            users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, n_pre, pstride, w.bnd,
+            w.bnd_m, insp);
         return;
     }
     if (SCAN_FLAT && w.flat_ok && w.bnd == nullptr && nub < slots && n >= 64) {
