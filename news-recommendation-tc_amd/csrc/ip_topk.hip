@@ -347,16 +347,6 @@ __device__ __forceinline__ uint32_t sel_mask_v(uint64_t m, uint32_t f) {
     asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "n"(T), "s"(m));
     return r;
 }
-// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): unrolled
-// with the index usable as a constant expression (asm "n" operands)
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
 // the first b < TB whose lane bit is set in am[b] (TB - 1 if none):
 // TB - 1 v_cndmask_b32 on the compare masks
 template <int TB>
@@ -2363,6 +2353,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
         return;
     }
     wave_sync_lds();
+    // survivors ordered (score desc, row asc); the first k are the output
+    auto emit = [&](const Cand* x, int ne) {
+        for (int e = 0; e < ne; ++e) {
+            const int idx = e * 64 + lane;
+            if (idx < k) {
+                const bool ok = x[e].row != INT32_MAX;
+                out_s[u * k + idx] = ok ? (float)x[e].s : -FLT_MAX;
+                out_r[u * k + idx] = ok ? (int32_t)(x[e].row + row_offset) : -1;
+                if (out_e) out_e[u * k + idx] = ok ? x[e].s : -INFINITY;
+            }
+        }
+    };
+    if (SE > 1 && cnt <= WAVE && k <= WAVE) {
+        // up to 64 survivors (nearly every user at config 2): one per lane, a
+        // 64-wide sort -- 21 shuffle stages instead of the SV-wide sort's 28 x
+        // SE (finish 1.27 -> 0.93 ms; rank counting over LDS broadcasts: 0.94)
+        Cand x1[1];
+        if (lane < cnt) x1[0] = surv[wave][lane];
+        else { x1[0].s = -INFINITY; x1[0].row = INT32_MAX; }
+        wave_bitonic_sort<1>(x1);
+        emit(x1, 1);
+        return;
+    }
     Cand x[SE];
 #pragma unroll
     for (int e = 0; e < SE; ++e) {
@@ -2371,16 +2384,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
         else { x[e].s = -INFINITY; x[e].row = INT32_MAX; }
     }
     wave_bitonic_sort<SE>(x);
-#pragma unroll
-    for (int e = 0; e < SE; ++e) {
-        const int idx = e * 64 + lane;
-        if (idx < k) {
-            const bool ok = x[e].row != INT32_MAX;
-            out_s[u * k + idx] = ok ? (float)x[e].s : -FLT_MAX;
-            out_r[u * k + idx] = ok ? (int32_t)(x[e].row + row_offset) : -1;
-            if (out_e) out_e[u * k + idx] = ok ? x[e].s : -INFINITY;
-        }
-    }
+    emit(x, SE);
 }
 
 // ----------------------------------------------- refine by half-block --

@@ -6,6 +6,8 @@
 
 #include <cstdio>
 #include <string>
+#include <type_traits>
+#include <utility>
 
 #include "../../include/nrk.h"
 
@@ -70,24 +72,62 @@ __device__ __forceinline__ Cand shfl_xor_cand(const Cand& c, int m) {
     return o;
 }
 
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): unrolled
+// with the index usable as a constant expression (asm / DPP operands)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// value of lane ^ J (J < 64) without ds_bpermute's address VGPR: DPP
+// quad_perm for J = 1, 2; ds_swizzle's xor mode (within 32 lanes) for 4, 8;
+// the gfx950 row / half swaps for 16, 32 (vdst = src = v: one result holds
+// the even rows' / lower half's values in both, the other the odd / upper)
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+    static_assert(J == 1 || J == 2 || J == 4 || J == 8 || J == 16 || J == 32, "lane_xor");
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (J == 4 || J == 8) {
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (J << 10) | 0x1F);  // and 0x1F, xor J
+    } else if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (threadIdx.x & 16) ? (uint32_t)r[0] : (uint32_t)r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32) ? (uint32_t)r[0] : (uint32_t)r[1];
+    }
+}
+template <int J>
+__device__ __forceinline__ double lane_xor_f64(double d) {
+    const uint64_t b = (uint64_t)__double_as_longlong(d);
+    const uint32_t lo = lane_xor<J>((uint32_t)b), hi = lane_xor<J>((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // Wave-wide bitonic sort of E*64 candidates, best first.  Element index
-// i = e*64 + lane.  E is a compile-time power of two; every loop has a
-// compile-time trip count so x[] stays in registers.
+// i = e*64 + lane.  E is a compile-time power of two; every stage is
+// unrolled at compile time (lane_xor needs constant distances), so x[]
+// stays in registers.
 template <int E>
 __device__ __forceinline__ void wave_bitonic_sort(Cand (&x)[E]) {
     const int lane = threadIdx.x & (WAVE - 1);
-    // fully unrolled: E = 8 already costs minutes of compile time per
-    // instantiation, so larger sorts go through wave_lds_sort
+    // E = 8 already costs minutes of compile time per instantiation, so
+    // larger sorts go through wave_lds_sort
     static_assert(E == 1 || E == 2 || E == 4, "E must be 1, 2 or 4 (wave_lds_sort beyond)");
     constexpr int LOGN = (E == 1 ? 6 : E == 2 ? 7 : 8);
-#pragma unroll
-    for (int kl = 1; kl <= LOGN; ++kl) {
-        const int k = 1 << kl;
-#pragma unroll
-        for (int jl = kl - 1; jl >= 0; --jl) {
-            const int j = 1 << jl;
-            if (jl >= 6) {
-                const int jj = j >> 6;
+    static_for<LOGN>([&](auto klc) {
+        constexpr int kl = decltype(klc)::value + 1, k = 1 << kl;
+        static_for<kl>([&](auto jc) {
+            constexpr int jl = kl - 1 - decltype(jc)::value, j = 1 << jl;
+            if constexpr (jl >= 6) {
+                constexpr int jj = j >> 6;
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
                     if ((e & jj) == 0) {
@@ -106,8 +146,8 @@ __device__ __forceinline__ void wave_bitonic_sort(Cand (&x)[E]) {
                 const bool lower = (lane & j) == 0;
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-                    const double ys = __shfl_xor(x[e].s, j, WAVE);
-                    const int32_t yr = __shfl_xor(x[e].row, j, WAVE);
+                    const double ys = lane_xor_f64<j>(x[e].s);
+                    const int32_t yr = (int32_t)lane_xor<j>((uint32_t)x[e].row);
                     const bool up = (((e * WAVE + lane) & k) == 0);
                     const bool keep_better = (lower == up);
                     const bool xb = x[e].s > ys || (x[e].s == ys && x[e].row < yr);
@@ -116,8 +156,8 @@ __device__ __forceinline__ void wave_bitonic_sort(Cand (&x)[E]) {
                     x[e].row = take ? yr : x[e].row;
                 }
             }
-        }
-    }
+        });
+    });
 }
 
 __device__ __forceinline__ void wave_sync_lds() {
