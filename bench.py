@@ -845,8 +845,9 @@ def main(argv=None):
                     help="BASELINE config 5 instead: fused recall -> DIN, 10M users / N per rank x 5M items, D=128")
     ap.add_argument("--fused-users", type=int, default=0, help="users per rank for --fused (default 10M / N)")
     ap.add_argument("--fused-items", type=int, default=5_000_000)
-    ap.add_argument("--fused-chunk", type=int, default=32768,
-                    help="config 5: users per assemble / context / DIN call (a multiple of 2048: whole Dice batches)")
+    ap.add_argument("--fused-chunk", type=int, default=131072,
+                    help="config 5: users per assemble / context / DIN call (a multiple of 2048: whole Dice batches; "
+                         "rank side 359 / 366 / 372 ms per 1.25M-user step at 131072 / 65536 / 32768)")
     ap.add_argument("--fused-hash-ctx", action="store_true",
                     help="config 5 with the synthetic hash-bin context instead of the real context features")
     ap.add_argument("--shard", choices=["users", "catalog"], default="catalog",

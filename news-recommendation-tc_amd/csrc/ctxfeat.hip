@@ -50,6 +50,7 @@ struct PwPlan {
     int b[4], n[4];
 };
 __device__ __forceinline__ PwPlan pw_plan(int n) {
+    // every store at a constant index (a run-time index puts the plan in scratch)
     PwPlan p{};
     if (n <= 128) {
         p.nl = 1;
@@ -57,76 +58,35 @@ __device__ __forceinline__ PwPlan pw_plan(int n) {
         p.n[0] = n;
         return p;
     }
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    int k = 0;
-    const int lb[2] = {0, n2}, ln[2] = {n2, n - n2};
-    bool split[2];
-    for (int h = 0; h < 2; ++h) {
-        split[h] = ln[h] > 128;
-        if (!split[h]) {
-            p.b[k] = lb[h];
-            p.n[k++] = ln[h];
-        } else {
-            int m2 = ln[h] / 2;
-            m2 -= m2 % 8;
-            p.b[k] = lb[h];
-            p.n[k++] = m2;
-            p.b[k] = lb[h] + m2;
-            p.n[k++] = ln[h] - m2;
-        }
+    const int n2 = n / 2 - (n / 2) % 8, r1 = n - n2;  // numpy's halves
+    const int m0 = n2 / 2 - (n2 / 2) % 8, m1 = r1 / 2 - (r1 / 2) % 8;
+    const bool s0 = n2 > 128, s1 = r1 > 128;  // a half above 128 splits once more
+    if (!s0 && !s1) {
+        p.nl = 2;
+        p.b[0] = 0, p.n[0] = n2;
+        p.b[1] = n2, p.n[1] = r1;
+        p.shape = 1;
+    } else if (s0 && !s1) {
+        p.nl = 3;
+        p.b[0] = 0, p.n[0] = m0;
+        p.b[1] = m0, p.n[1] = n2 - m0;
+        p.b[2] = n2, p.n[2] = r1;
+        p.shape = 2;
+    } else if (!s0 && s1) {
+        p.nl = 3;
+        p.b[0] = 0, p.n[0] = n2;
+        p.b[1] = n2, p.n[1] = m1;
+        p.b[2] = n2 + m1, p.n[2] = r1 - m1;
+        p.shape = 3;
+    } else {
+        p.nl = 4;
+        p.b[0] = 0, p.n[0] = m0;
+        p.b[1] = m0, p.n[1] = n2 - m0;
+        p.b[2] = n2, p.n[2] = m1;
+        p.b[3] = n2 + m1, p.n[3] = r1 - m1;
+        p.shape = 4;
     }
-    p.nl = k;
-    p.shape = (split[0] && split[1]) ? 4 : split[0] ? 2 : split[1] ? 3 : 1;
     return p;
-}
-
-// word_diff of one (recalled row, history item) task on a half-wave (32
-// lanes): lane (leaf l, j) keeps numpy's j-th leaf accumulator (elements
-// b + j, b + j + 8, ...: 8 lanes read 64 consecutive bytes of the item row),
-// a xor-1/2/4 butterfly is the leaf's ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)),
-// lane j = 0 adds the leaf's tail in order, and the leaves combine by the
-// plan's shape -- the same operations in the same order as pw_sum64<2>, so
-// the result is bit-identical to the per-lane loop (and to numpy).
-__device__ __forceinline__ double coop_word_diff(const PwPlan& pl, const double* __restrict__ r,
-                                                 const double* __restrict__ h, int s) {
-    const int l = s >> 3, j = s & 7;
-    const bool act = l < pl.nl;
-    const int lb = act ? pl.b[l] : 0, ln = act ? pl.n[l] : 0;
-    auto f = [&](int e) {
-        const double d = __dsub_rn((double)(float)r[e], h[e]);
-        double p = __dmul_rn(d, d);
-        asm volatile("" : "+v"(p));
-        return p;
-    };
-    double acc = 0.0;
-    const int full = ln - ln % 8;
-    if (ln >= 8) {
-        acc = f(lb + j);
-        for (int i = 8; i < full; i += 8) acc = __dadd_rn(acc, f(lb + i + j));
-    }
-    // butterfly over j (the 8 lanes of the leaf)
-    acc = __dadd_rn(acc, __shfl_xor(acc, 1, WAVE));
-    acc = __dadd_rn(acc, __shfl_xor(acc, 2, WAVE));
-    acc = __dadd_rn(acc, __shfl_xor(acc, 4, WAVE));
-    if (j == 0 && act) {
-        if (ln < 8) {
-            acc = 0.0;
-            for (int i = 0; i < ln; ++i) acc = __dadd_rn(acc, f(lb + i));
-        } else {
-            for (int i = full; i < ln; ++i) acc = __dadd_rn(acc, f(lb + i));
-        }
-    }
-    const int base = threadIdx.x & 32;  // this half-wave's lane 0
-    const double v0 = __shfl(acc, base, WAVE), v1 = __shfl(acc, base + 8, WAVE);
-    const double v2 = __shfl(acc, base + 16, WAVE), v3 = __shfl(acc, base + 24, WAVE);
-    switch (pl.shape) {
-        case 0: return v0;
-        case 1: return __dadd_rn(v0, v1);
-        case 2: return __dadd_rn(__dadd_rn(v0, v1), v2);
-        case 3: return __dadd_rn(v0, __dadd_rn(v1, v2));
-        default: return __dadd_rn(__dadd_rn(v0, v1), __dadd_rn(v2, v3));
-    }
 }
 
 // xor-1 / xor-2 / xor-4 partner of a double within 8 lanes (DPP quad swaps
@@ -143,22 +103,30 @@ __device__ __forceinline__ double dpp_f64(double v, int ctrl) {
     return __longlong_as_double((long long)((uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32)));
 }
 
-// coop_word_diff for all N history items of one recalled row at once: the
-// item row's elements are read once and feed the N accumulators (the same
-// operations, per item, as coop_word_diff: bit-identical results)
+// word_diff of one recalled row against all N history items on a half-wave
+// (32 lanes): lane (leaf l, j) keeps numpy's j-th leaf accumulator (elements
+// b + j, b + j + 8, ...: 8 lanes read 64 consecutive bytes of the item row)
+// for every history item, a xor-1/2/4 butterfly is the leaf's
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), lane j = 0 adds the leaf's tail in
+// order, and the leaves combine by the plan's shape -- the same operations in
+// the same order as numpy's pairwise sum (bit-identical)
 __device__ __forceinline__ void coop_word_diff_n(const PwPlan& pl, const double* __restrict__ r,
-                                                 const double (*__restrict__ h)[CTX_DC_MAX], int N, int s,
+                                                 const double* __restrict__ hb, int hs, int N, int s,
                                                  double (&out)[CTX_NMAX]) {
+    auto h = [&](int i, int e) { return hb[i * hs + e]; };  // history row i, element e (LDS)
     const int l = s >> 3, j = s & 7;
     const bool act = l < pl.nl;
-    const int lb = act ? pl.b[l] : 0, ln = act ? pl.n[l] : 0;
+    // the lane's leaf by selects (a run-time index into pl.b / pl.n would put
+    // the plan in scratch)
+    const int lb = !act ? 0 : l == 0 ? pl.b[0] : l == 1 ? pl.b[1] : l == 2 ? pl.b[2] : pl.b[3];
+    const int ln = !act ? 0 : l == 0 ? pl.n[0] : l == 1 ? pl.n[1] : l == 2 ? pl.n[2] : pl.n[3];
     double acc[CTX_NMAX] = {0.0, 0.0, 0.0, 0.0};
     auto fa = [&](int e, bool first) {
         const double re = (double)(float)r[e];
 #pragma unroll
         for (int i = 0; i < CTX_NMAX; ++i) {
             if (i >= N) break;
-            const double d = __dsub_rn(re, h[i][e]);
+            const double d = __dsub_rn(re, h(i, e));
             double p = __dmul_rn(d, d);
             asm volatile("" : "+v"(p));
             acc[i] = first ? p : __dadd_rn(acc[i], p);
@@ -185,7 +153,7 @@ __device__ __forceinline__ void coop_word_diff_n(const PwPlan& pl, const double*
 #pragma unroll
             for (int i = 0; i < CTX_NMAX; ++i) {
                 if (i >= N) break;
-                const double d = __dsub_rn(re, h[i][lb + e]);
+                const double d = __dsub_rn(re, h(i, lb + e));
                 double p = __dmul_rn(d, d);
                 asm volatile("" : "+v"(p));
                 acc[i] = (ln < 8 && e == 0) ? p : __dadd_rn(acc[i], p);
@@ -228,31 +196,48 @@ __device__ __forceinline__ int32_t ctx_code(const nrk_ctx_spec& sp, double v) {
 __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, const nrk_ctx_spec* __restrict__ spec,
                                                            double* __restrict__ out_raw,
                                                            int32_t* __restrict__ out_codes) {
-    __shared__ double s_cont[4][CTX_NMAX][CTX_DC_MAX];
+    // the history content rows: N x dc doubles per wave (dynamic, sized by
+    // the host: 24 KB at N = 3, dc = 250 instead of a 32-KB worst case, so 4
+    // workgroups fit a CU instead of 3)
+    extern __shared__ double s_dyn[];
     __shared__ __attribute__((aligned(16))) float s_w2v[4][CTX_NMAX][CTX_DW_MAX];
     __shared__ double s_wd[4][64][CTX_NMAX];  // word_diff of this chunk's rows
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t g = (int64_t)blockIdx.x * 4 + wv;
     if (g >= tb.n_groups) return;
     const int N = tb.last_n, F = 1 + 3 * N + 6;
+    double* const s_cont = s_dyn + (size_t)wv * N * tb.dc;  // [N][dc]
     const int32_t u = tb.group_user[g];
     const int hn = u >= 0 ? tb.hist_n[u] : -1;  // -1: the user has no history entry
     int32_t hrow[CTX_NMAX];
     double hcre[CTX_NMAX];
     bool hw2v[CTX_NMAX], hcont[CTX_NMAX];
-    for (int i = 0; i < N; ++i) {
+#pragma unroll
+    for (int i = 0; i < CTX_NMAX; ++i) {
+        if (i >= N) {
+            hrow[i] = -1;
+            hw2v[i] = hcont[i] = false;
+            hcre[i] = (double)NAN;
+            continue;
+        }
         const int32_t r = i < hn ? tb.hist_last[(int64_t)u * N + i] : -1;
         hrow[i] = r;
         hw2v[i] = r >= 0 && tb.w2v_ok[r];
         hcont[i] = r >= 0 && (tb.content_flags[r] & 1);
         hcre[i] = r >= 0 ? tb.created[r] : (double)NAN;
-        for (int e = lane; e < tb.dc; e += 64) s_cont[wv][i][e] = hcont[i] ? tb.content[(int64_t)r * tb.dc + e] : 0.0;
+        for (int e = lane; e < tb.dc; e += 64) s_cont[i * tb.dc + e] = hcont[i] ? tb.content[(int64_t)r * tb.dc + e] : 0.0;
         for (int e = lane; e < tb.dw; e += 64) s_w2v[wv][i][e] = hw2v[i] ? tb.w2v[(int64_t)r * tb.dw + e] : 0.0f;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const bool uyt = tb.user_yt != nullptr && u >= 0 && tb.user_yt_ok[u];
+    // the user's history categories: up to 64 held one per lane (loaded with
+    // every lane active, read back by v_readlane per category); more take the
+    // per-row loop below
+    const int64_t uk0 = u >= 0 ? tb.ucat_off[u] : 0, uk1 = u >= 0 ? tb.ucat_off[u + 1] : 0;
+    const int ncat = (int)(uk1 - uk0);
+    const int32_t ucv = (ncat <= 64 && lane < ncat) ? tb.ucat[uk0 + lane] : -1;
     const int64_t p0 = tb.group_off[g], p1 = tb.group_off[g + 1];
     const PwPlan plan = pw_plan(tb.dc);
     for (int64_t c0 = p0; c0 < p1; c0 += 64) {
@@ -270,9 +255,12 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
                 const double* rrow = tb.content + (int64_t)(ion ? it : 0) * tb.dc;
                 // every lane runs the (shuffling) sums; rows that do not count take 0
                 double ss[CTX_NMAX];
-                coop_word_diff_n(plan, rrow, s_cont[wv], N, lane & 31, ss);
-                if ((lane & 31) == 0 && qr0 < nr)
-                    for (int i = 0; i < N; ++i) s_wd[wv][qr][i] = (ion && i < hn && hcont[i]) ? sqrt(ss[i]) : 0.0;
+                coop_word_diff_n(plan, rrow, s_cont, tb.dc, N, lane & 31, ss);
+                if ((lane & 31) == 0 && qr0 < nr) {
+#pragma unroll
+                    for (int i = 0; i < CTX_NMAX; ++i)
+                        if (i < N) s_wd[wv][qr][i] = (ion && i < hn && hcont[i]) ? sqrt(ss[i]) : 0.0;
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
@@ -282,16 +270,20 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
         if (q >= p1) continue;
         const int64_t pos = tb.pair_pos ? tb.pair_pos[q] : q;
         const int32_t it = tb.pair_item[pos];
-        double f[1 + 3 * CTX_NMAX + 6];
-        f[0] = tb.pair_score[pos];
-        for (int i = 0; i < N; ++i) {
-            f[1 + 3 * i] = NAN;
-            f[2 + 3 * i] = 0.0;
-            f[3 + 3 * i] = 0.0;
+        // the row's features in registers: every array below is indexed by
+        // compile-time loop indices (a runtime-N index put them in scratch)
+        double fs[CTX_NMAX][3];  // sim_i, time_diff_i, word_diff_i
+        double st[6];            // sim_max, sim_mean, sim_min, sim_std, item_user_sim, recall_in_user_cat
+#pragma unroll
+        for (int i = 0; i < CTX_NMAX; ++i) {
+            fs[i][0] = NAN;
+            fs[i][1] = 0.0;
+            fs[i][2] = 0.0;
         }
-        for (int k = 0; k < 4; ++k) f[1 + 3 * N + k] = NAN;
-        f[1 + 3 * N + 4] = 0.0;
-        f[1 + 3 * N + 5] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st[k] = NAN;
+        st[4] = 0.0;
+        st[5] = 0.0;
         if (hn >= 0) {
             const bool iw2v = it >= 0 && tb.w2v_ok[it];
             const double icre = it >= 0 ? (double)(float)tb.created[it] : (double)NAN;  // f32 array (:588-594)
@@ -313,30 +305,36 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
                         }
                     }
                 } else {
-                    for (int i = 0; i < N; ++i) dots[i] = dot_f32(ir, s_w2v[wv][i], tb.dw);
+#pragma unroll
+                    for (int i = 0; i < CTX_NMAX; ++i) {
+                        if (i >= N) break;
+                        dots[i] = dot_f32(ir, s_w2v[wv][i], tb.dw);
+                    }
                 }
             }
-            for (int i = 0; i < N; ++i) {
+#pragma unroll
+            for (int i = 0; i < CTX_NMAX; ++i) {
                 sims[i] = NAN;
-                if (i >= hn) continue;
+                if (i >= N || i >= hn) continue;
                 const float sv = hw2v[i] && iw2v ? dots[i] : 0.0f;
                 sims[i] = sv;
-                f[1 + 3 * i] = (double)sv;
+                fs[i][0] = (double)sv;
                 // time_diff_i (:617-631)
                 double td = 0.0;
                 if (hcre[i] == hcre[i]) {
                     const double d = fabs(icre - hcre[i]);
                     td = d == d ? d : 0.0;
                 }
-                f[2 + 3 * i] = (double)(float)td;
+                fs[i][1] = (double)(float)td;
                 // word_diff_i (:633-648), computed cooperatively above
-                f[3 + 3 * i] = (double)(float)s_wd[wv][lane][i];
+                fs[i][2] = (double)(float)s_wd[wv][lane][i];
             }
             // nan-statistics of the sims (:660-664), float32
             float mx = -INFINITY, mn = INFINITY, tot = 0.0f;
             int cnt = 0;
-            for (int i = 0; i < N; ++i) {
-                if (sims[i] != sims[i]) continue;
+#pragma unroll
+            for (int i = 0; i < CTX_NMAX; ++i) {
+                if (i >= N || sims[i] != sims[i]) continue;
                 mx = fmaxf(mx, sims[i]);
                 mn = fminf(mn, sims[i]);
                 tot = __fadd_rn(tot, sims[i]);
@@ -345,18 +343,19 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
             if (cnt > 0) {
                 const float mean = (float)((double)tot / (double)cnt);
                 float ss = 0.0f;
-                for (int i = 0; i < N; ++i) {
-                    if (sims[i] != sims[i]) continue;
+#pragma unroll
+                for (int i = 0; i < CTX_NMAX; ++i) {
+                    if (i >= N || sims[i] != sims[i]) continue;
                     const float d = __fsub_rn(sims[i], mean);
                     float sq = __fmul_rn(d, d);
                     asm volatile("" : "+v"(sq));  // no contraction into the running sum
                     ss = __fadd_rn(ss, sq);
                 }
                 const float var = (float)((double)ss / (double)cnt);
-                f[1 + 3 * N + 0] = (double)mx;
-                f[1 + 3 * N + 1] = (double)mean;
-                f[1 + 3 * N + 2] = (double)mn;
-                f[1 + 3 * N + 3] = (double)(float)sqrt((double)var);  // correctly rounded f32 sqrt
+                st[0] = (double)mx;
+                st[1] = (double)mean;
+                st[2] = (double)mn;
+                st[3] = (double)(float)sqrt((double)var);  // correctly rounded f32 sqrt
             }
             // item_user_sim (:538-558), zero vector for a missing item
             if (uyt && it >= 0 && tb.item_yt_ok[it]) {
@@ -372,19 +371,35 @@ __global__ __launch_bounds__(256) void ctx_features_kernel(nrk_ctx_tables tb, co
                 } else {
                     d = dot_f32(a, b, tb.dy);
                 }
-                f[1 + 3 * N + 4] = (double)d;
+                st[4] = (double)d;
             }
             // recall_in_user_cat (:677-690)
             const int32_t c = it >= 0 ? tb.category[it] : -1;
             int inc = 0;
-            if (c >= 0)
-                for (int64_t k = tb.ucat_off[u]; k < tb.ucat_off[u + 1]; ++k) inc |= tb.ucat[k] == c ? 1 : 0;
-            f[1 + 3 * N + 5] = (double)inc;
+            if (c >= 0) {
+                if (ncat <= 64) {
+                    for (int kk = 0; kk < ncat; ++kk) inc |= __builtin_amdgcn_readlane(ucv, kk) == c ? 1 : 0;
+                } else {
+                    for (int64_t k = uk0; k < uk1; ++k) inc |= tb.ucat[k] == c ? 1 : 0;
+                }
+            }
+            st[5] = (double)inc;
         }
-        if (out_raw)
-            for (int k = 0; k < F; ++k) out_raw[pos * F + k] = f[k];
-        if (out_codes)
-            for (int k = 0; k < F; ++k) out_codes[pos * tb.code_stride + k] = ctx_code(spec[k], f[k]);
+        // column order: score, (sim, time_diff, word_diff) per history item,
+        // the six row statistics
+        auto emit = [&](int col, double v) {
+            if (out_raw) out_raw[pos * F + col] = v;
+            if (out_codes) out_codes[pos * tb.code_stride + col] = ctx_code(spec[col], v);
+        };
+        emit(0, tb.pair_score[pos]);
+#pragma unroll
+        for (int i = 0; i < CTX_NMAX; ++i) {
+            if (i >= N) break;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) emit(1 + 3 * i + c, fs[i][c]);
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) emit(1 + 3 * N + k, st[k]);
     }
 }
 
@@ -411,7 +426,8 @@ int nrk_ctx_features(const nrk_ctx_tables* tables, const nrk_ctx_spec* spec, dou
                     t.category,
                 "null table pointer");
     NRK_REQUIRE(!t.user_yt || (t.user_yt_ok && t.item_yt && t.item_yt_ok && t.dy >= 1), "yt tables incomplete");
-    ctx_features_kernel<<<(int)((t.n_groups + 3) / 4), 256, 0, as_stream(stream)>>>(t, spec, out_raw, out_codes);
+    const size_t lds = (size_t)4 * t.last_n * t.dc * sizeof(double);
+    ctx_features_kernel<<<(int)((t.n_groups + 3) / 4), 256, lds, as_stream(stream)>>>(t, spec, out_raw, out_codes);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
