@@ -614,6 +614,12 @@ constexpr int TM_SW = 128;  // samples per workgroup
 #endif
 constexpr int TM_NW = NRK_TM_NW;
 constexpr bool TM_WLDS = TM_NW == 8;
+// W fragments from LDS in a 3-slot ring per (k-step, column tile) group (1)
+// or double-buffered per k-step (0, round 4)
+#ifndef NRK_TM_WRING
+#define NRK_TM_WRING 1
+#endif
+constexpr bool TM_WRING = NRK_TM_WRING;
 constexpr int TM_NT = TM_NW * 64;
 constexpr int TM_TMAX = 64; // positions (T)
 
@@ -962,7 +968,37 @@ __global__ __launch_bounds__(TM_NT, 1) __attribute__((amdgpu_waves_per_eu(TM_NW 
             const int j = 16 * jt + lr < DIN_H ? 16 * jt + lr : DIN_H - 1;
             acc[jt] = *reinterpret_cast<const din_f4*>(ct + j * CTS + 16 * i + 4 * lg);
         }
-        if constexpr (TM_WLDS) {
+        if constexpr (TM_WLDS && TM_WRING) {
+            // the (k-step s, column tile jt) groups' 4 fragments each, read two
+            // groups (10 MFMAs) ahead in a 3-slot ring: 12 fragments live
+            // instead of a whole k-step double-buffered (24: the NI = 4
+            // instantiation spilled 45 VGPRs at 256)
+            din_half8 wq[3][4];
+            auto wread = [&](int q, din_half8 (&w)[4]) {
+                const int s = q / 3, jt = q % 3;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) w[c] = wl[((jt * NI + s) * 4 + c) * 64 + lane];
+            };
+            wread(0, wq[0]);
+            wread(1, wq[1]);
+            din_half8 ph, pl;
+            static_for<3 * NI>([&](auto qc) {
+                constexpr int q = decltype(qc)::value, s = q / 3, jt = q % 3;
+                if constexpr (q + 2 < 3 * NI) wread(q + 2, wq[(q + 2) % 3]);
+                if constexpr (jt == 0) {
+                    const din_half8 qf = *reinterpret_cast<const din_half8*>(ql + pa * QS + (DIN_E * s + 8 * lg) * 2);
+                    __builtin_amdgcn_sched_barrier(0);
+                    ph = kf[s] * qf;
+                    pl = __builtin_elementwise_fma(kf[s], qf, -ph);
+                }
+                const din_half8(&w)[4] = wq[q % 3];
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], w[0], acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], w[1], acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, w[2], acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, w[3], acc[jt], 0, 0, 0);
+                acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl, w[2], acc[jt], 0, 0, 0);
+            });
+        } else if constexpr (TM_WLDS) {
             // k-step s + 1's 12 fragments are read while k-step s's 15 MFMAs
             // run (two register sets; the barrier keeps the reads ahead)
             din_half8 wb[2][3][4];
