@@ -19,14 +19,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
     // weight rows padded by one word: lane o reads row o, so an unpadded
     // power-of-two row stride would put all 64 lanes on one LDS bank
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int S0 = 2 * D + 1, S1 = h0 + 1;
+    // rows padded to a multiple of 4 floats + 4: 16-B aligned for the 4-wide
+    // reads below, and lane o's row starts 4 banks after lane o - 1's
+    const int S0 = 2 * D + 4, h0p = (h0 + 3) & ~3, S1 = h0p + 4, h1p = (h1 + 3) & ~3;
     float* sw0 = lds;               // [h0][S0]
-    float* sb0 = sw0 + h0 * S0;     // [h0]
-    float* sw1 = sb0 + h0;          // [h1][S1]
-    float* sb1 = sw1 + h1 * S1;     // [h1]
+    float* sb0 = sw0 + h0 * S0;     // [h0] (h0p)
+    float* sw1 = sb0 + h0p;         // [h1][S1]
+    float* sb1 = sw1 + h1 * S1;     // [h1] (h1p)
     // per-wave broadcast rows for the two matvecs: [x (2D) | y0 (h0)]; every
     // lane reads the same word (LDS broadcast) instead of a v_readlane per term
-    float* sx = sb1 + h1 + (threadIdx.x >> 6) * (2 * D + 128);
+    float* sx = sb1 + h1p + (threadIdx.x >> 6) * (2 * D + 128);
     for (int i = threadIdx.x; i < h0 * 2 * D; i += blockDim.x) sw0[(i / (2 * D)) * S0 + i % (2 * D)] = w0[i];
     for (int i = threadIdx.x; i < h0; i += blockDim.x) sb0[i] = b0[i];
     for (int i = threadIdx.x; i < h1 * h0; i += blockDim.x) sw1[(i / h0) * S1 + i % h0] = w1[i];
@@ -99,11 +101,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
             float z1 = lane + WAVE < h0 ? sb0[lane + WAVE] : 0.0f;
             const float* wr0 = sw0 + (lane < h0 ? lane : 0) * S0;
             const float* wr1 = sw0 + (lane + WAVE < h0 ? lane + WAVE : 0) * S0;
-#pragma unroll 16
-            for (int q = 0; q < 2 * D; ++q) {
-                const float xq = sx[q];
-                z0 += wr0[q] * xq;
-                z1 += wr1[q] * xq;
+            // 4 inputs (broadcast) and 4 weights per LDS read; the fma
+            // chain still runs q = 0, 1, 2, ... in order
+#pragma unroll 2
+            for (int q = 0; q < 2 * D; q += 4) {
+                const float4 xq = *reinterpret_cast<const float4*>(sx + q);
+                const float4 a = *reinterpret_cast<const float4*>(wr0 + q);
+                const float4 b = *reinterpret_cast<const float4*>(wr1 + q);
+                z0 += a.x * xq.x;
+                z0 += a.y * xq.y;
+                z0 += a.z * xq.z;
+                z0 += a.w * xq.w;
+                z1 += b.x * xq.x;
+                z1 += b.y * xq.y;
+                z1 += b.z * xq.z;
+                z1 += b.w * xq.w;
             }
             y0 = fmaxf(z0, 0.0f);
             y1 = fmaxf(z1, 0.0f);
@@ -117,7 +129,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
         {
             float z = lane < h1 ? sb1[lane] : 0.0f;
             const float* wr = sw1 + (lane < h1 ? lane : 0) * S1;
-            for (int q = 0; q < h0; ++q) z += wr[q] * sy[q];
+            int q = 0;
+            for (; q + 4 <= h0; q += 4) {
+                const float4 yq = *reinterpret_cast<const float4*>(sy + q);
+                const float4 a = *reinterpret_cast<const float4*>(wr + q);
+                z += a.x * yq.x;
+                z += a.y * yq.y;
+                z += a.z * yq.z;
+                z += a.w * yq.w;
+            }
+            for (; q < h0; ++q) z += wr[q] * sy[q];
             v = lane < h1 ? fmaxf(z, 0.0f) : 0.0f;
         }
         __builtin_amdgcn_wave_barrier();  // sx / sy are rewritten for the next user
@@ -253,7 +274,8 @@ int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* i
     if (n == 0) return NRK_OK;
     NRK_REQUIRE(user_table && item_table && uid && hist && hist_len && w0 && b0 && w1 && b1 && out,
                 "null pointer");
-    const size_t lds = sizeof(float) * ((size_t)h0 * (2 * dim + 1) + h0 + (size_t)h1 * (h0 + 1) + h1 +
+    const size_t h0p = (size_t)((h0 + 3) & ~3), h1p = (size_t)((h1 + 3) & ~3);
+    const size_t lds = sizeof(float) * ((size_t)h0 * (2 * dim + 4) + h0p + (size_t)h1 * (h0p + 4) + h1p +
                                         (size_t)4 * (2 * dim + 128));
     hipStream_t s = as_stream(stream);
     const int grid = (int)std::min<int64_t>((n + 3) / 4, 2048);
