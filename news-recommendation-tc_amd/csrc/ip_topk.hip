@@ -2035,8 +2035,17 @@ __device__ __forceinline__ double exact_dot(const float* __restrict__ a, const f
 // then each lane sums its own row sequentially (the oracle's order).
 // DS4 = 0: the generic per-lane gather.  SV = exact survivors held per user
 // (SV / 64 per lane in the final sort).
+// the exact rounds' rows read per lane (dims <= 32) instead of staged
+#ifndef NRK_REFINE_DIRECT
+#define NRK_REFINE_DIRECT 1
+#endif
+constexpr bool REFINE_DIRECT = NRK_REFINE_DIRECT;
+// waves per SIMD the refine's registers are sized for
+#ifndef NRK_REFINE_WPE
+#define NRK_REFINE_WPE 4
+#endif
 template <int DS4, int SV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ip_refine_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRK_REFINE_WPE))) void ip_refine_kernel(
     const float* __restrict__ users, int64_t n_users, const float* __restrict__ items,
     const uint8_t* __restrict__ catalog, int64_t n_items, int dim, int k, int64_t row_offset,
     const uint2* __restrict__ cand, int bandcap, const int32_t* __restrict__ cand_cnt,
@@ -2223,6 +2232,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
             const int32_t rl = lane < m ? krow[wave][(ko + lane) & (IP_KRING - 1)] : -1;
             double sd = 0.0;
             bool keep = false;
+            if constexpr (REFINE_DIRECT && DS4 <= 8) {
+                // every lane reads its own row (one 128-B line at D = 32) and
+                // sums it: no LDS stage and no half-idle passes (config 2:
+                // finish 0.91 -> 0.87 ms).  D = 64 keeps the staged rounds
+                // (its 16 float4 per lane spilled)
+                if (rl >= 0) {
+                    const float4* a4 = reinterpret_cast<const float4*>(uv);
+                    const float4* b4 = reinterpret_cast<const float4*>(items + (int64_t)rl * dim);
+                    float4 y[DS4];
+#pragma unroll
+                    for (int t = 0; t < DS4; ++t) y[t] = b4[t];
+                    double acc = 0.0;
+#pragma unroll
+                    for (int t = 0; t < DS4; ++t) {
+                        const float4 x = a4[t];
+                        acc += (double)x.x * (double)y[t].x;
+                        acc += (double)x.y * (double)y[t].y;
+                        acc += (double)x.z * (double)y[t].z;
+                        acc += (double)x.w * (double)y[t].w;
+                    }
+                    sd = acc + 0.0;
+                    keep = sd >= thr;
+                }
+                push(keep, sd, rl);
+                ko += m;
+                return;
+            }
 #pragma unroll
             for (int hp = 0; hp < 2; ++hp) {
                 float4 v[DS4 / 2];
