@@ -109,6 +109,32 @@ def test_ip_topk_list_prepass_vs_oracle(ops, n_users, n_items, d, k):
     assert np.array_equal(e[ro >= 0], eo[ro >= 0])
 
 
+@pytest.mark.parametrize(
+    "n_users,n_items",
+    [
+        (1500, 100),  # one tile: a single, short step
+        (1500, 7 * 128),  # 7 tiles: no insert-period boundary, the pending maxima flushed at the end
+        (1500, 129 * 128),  # 129 tiles + an odd 21-tile pre-pass: 150 tiles in the sequence
+        (1500, 130 * 128 - 5),  # 151 tiles (a short last step) and a masked last block
+        (1100, 131 * 128 + 77),  # 132 tiles, a partial last tile; 76 users past the first 1,024-user block
+    ],
+)
+def test_ip_topk_ws_steps_vs_oracle(ops, n_users, n_items):
+    """The warp-specialized config-2 scan (D = 32, k = 31): two tiles per
+    barrier step, main-pass inserts every 8 tiles, the pre-pass and main pass
+    as one sequence -- odd sequence lengths, odd pre-passes, ranges shorter
+    than the insert period, masked tails and a partial user block, bit-exact
+    against the oracle."""
+    rng = np.random.default_rng(n_users * 7 + n_items)
+    users = _unit(rng.standard_normal((n_users, 32)))
+    items = _unit(rng.standard_normal((n_items, 32)))
+    s, r, e = _run_topk(ops, users, items, 31)
+    so, ro, eo = oracle.ip_topk(users, items, 31, exact=True)
+    assert np.array_equal(r, ro)
+    assert np.array_equal(s, so)
+    assert np.array_equal(e[ro >= 0], eo[ro >= 0])
+
+
 def test_ip_topk_unnormalised_and_offset(ops):
     rng = np.random.default_rng(3)
     users = (rng.standard_normal((150, 32)) * 5).astype(np.float32)
