@@ -153,18 +153,34 @@ __global__ void catalog_pack_hb_kernel(const float* __restrict__ items, int64_t 
     }
 }
 
+// The catalog statistics read the fp32 rows coalesced: L lanes per row (the
+// power of two >= dim, at most 64), 64 / L consecutive rows per wave and
+// step, lane j of a row holding dims j, j + L, ... (a row-per-lane loop read
+// one 4-B word per 128-B line per lane: 1.2 GB fetched per launch for a 47-MB
+// config-2 catalog).  The per-row sums then run in a lane tree instead of
+// dimension order; max_norm and max_dnorm only enter the screen's error
+// bound eps, whose 1.0001 / (1 + 1e-6) margins cover that rounding.
+__device__ __forceinline__ int cat_lanes(int dim) { return dim <= 16 ? 16 : dim <= 32 ? 32 : 64; }
+
 __global__ void catalog_norm_kernel(const float* __restrict__ items, int64_t n_items, int dim,
                                     CatalogHdr* hdr) {
+    const int lane = threadIdx.x & 63, L = cat_lanes(dim), R = WAVE / L, j = lane & (L - 1);
+    const int64_t wid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     float m = 0.0f, a = 0.0f;
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_items;
-         r += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t r0 = wid * R; r0 < n_items; r0 += nw * R) {
+        const int64_t r = r0 + lane / L;
         float s = 0.0f;
-        for (int d = 0; d < dim; ++d) {
-            const float x = items[r * dim + d];
-            s += x * x;
-            a = fmaxf(a, fabsf(x));
+        if (r < n_items) {
+            const float* row = items + r * dim;
+            for (int d = j; d < dim; d += L) {
+                const float x = row[d];
+                s += x * x;
+                a = fmaxf(a, fabsf(x));
+            }
         }
-        m = fmaxf(m, sqrtf(s));
+        for (int o = L >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, WAVE);
+        if (r < n_items) m = fmaxf(m, sqrtf(s));
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -182,17 +198,24 @@ __global__ void catalog_norm_kernel(const float* __restrict__ items, int64_t n_i
 __global__ void catalog_dnorm_kernel(const float* __restrict__ items, int64_t n_items, int dim,
                                      CatalogHdr* hdr) {
     const float scale = hdr->scale;
+    const int lane = threadIdx.x & 63, L = cat_lanes(dim), R = WAVE / L, j = lane & (L - 1);
+    const int64_t wid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     double m = 0.0;
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_items;
-         r += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t r0 = wid * R; r0 < n_items; r0 += nw * R) {
+        const int64_t r = r0 + lane / L;
         double s = 0.0;
-        for (int d = 0; d < dim; ++d) {
-            const float f = items[r * dim + d];
-            const float x = (float)(_Float16)(f * scale);  // catalog_pack's rounding
-            const double e = (double)x / (double)scale - (double)f;
-            s += e * e;
+        if (r < n_items) {
+            const float* row = items + r * dim;
+            for (int d = j; d < dim; d += L) {
+                const float f = row[d];
+                const float x = (float)(_Float16)(f * scale);  // catalog_pack's rounding
+                const double e = (double)x / (double)scale - (double)f;
+                s += e * e;
+            }
         }
-        m = fmax(m, sqrt(s));
+        for (int o = L >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, WAVE);
+        if (r < n_items) m = fmax(m, sqrt(s));
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, WAVE));
@@ -260,79 +283,10 @@ __device__ __forceinline__ void top_insert(float (&t)[MT], float v) {
 #ifndef NRK_SCAN_STAMP
 #define NRK_SCAN_STAMP 0
 #endif
-// dev A/B switches (make dev DEVFLAGS=...): the half-tile stagger of the
-// scan's two waves per SIMD (default on) and a static priority for the late half
-#ifndef NRK_SCAN_STAGGER
-#define NRK_SCAN_STAGGER 1
-#endif
-#ifndef NRK_SCAN_FLOOR
-#define NRK_SCAN_FLOOR 0
-#endif
-#ifndef NRK_SCAN_PRIO
-#define NRK_SCAN_PRIO 0
-#endif
-constexpr bool STAG = NRK_SCAN_STAGGER;
-// dev A/B: appends through the compiler's branch per half-block (0) instead
-// of the masked store; inserts without the ballot branch per group (0).
-// Config 2, one box: masked stores 5.93 vs 5.99 ms; straight-line inserts
-// 6.31 vs 5.93 (a quarter more VALU, and the four groups' chains did not
-// overlap better than the branches they replaced)
-#ifndef NRK_SCAN_APP_ASM
-#define NRK_SCAN_APP_ASM 1
-#endif
-#ifndef NRK_SCAN_INS_BR
-#define NRK_SCAN_INS_BR 1
-#endif
-#ifndef NRK_SCAN_APP_GRP
-#define NRK_SCAN_APP_GRP 1
-#endif
-constexpr bool SCAN_APP_ASM = NRK_SCAN_APP_ASM, SCAN_INS_BR = NRK_SCAN_INS_BR, SCAN_APP_GRP = NRK_SCAN_APP_GRP;
-// round 5 A/B switches (make dev DEVFLAGS=...):
-//   LAZY   -- round-robin list inserts: every tile folds the lane's tile max
-//             into a pending max per user group, and only group (tt mod UG)
-//             inserts its pending max (one insert check per tile instead of UG)
-//   BSEL   -- the appended half-block picked by v_cndmask on the compare's
-//             lane masks with inline-constant block numbers (no re-compare)
-//   LDSAPP -- appends staged per lane in LDS and flushed to the HBM lists in
-//             runs when some lane's stage fills (one store per flushed entry
-//             slot instead of one per (tile, group); the DMA ring's vmcnt gate
-//             then waits on ring pieces only)
-#ifndef NRK_SCAN_LAZY
-#define NRK_SCAN_LAZY 0
-#endif
-#ifndef NRK_SCAN_BSEL
-#define NRK_SCAN_BSEL 1
-#endif
-#ifndef NRK_SCAN_LDSAPP
-#define NRK_SCAN_LDSAPP 0
-#endif
-// SWP -- the tile's MFMAs software-pipelined against the half-block max
-// reductions (see tile()); the value is the lag in (block, group) steps
-#ifndef NRK_SCAN_SWP
-#define NRK_SCAN_SWP 2
-#endif
-constexpr bool SCAN_LAZY = NRK_SCAN_LAZY, SCAN_BSEL = NRK_SCAN_BSEL, SCAN_LDSAPP = NRK_SCAN_LDSAPP;
-constexpr int SCAN_SWP = NRK_SCAN_SWP;
-// the one-GPU scan fills every CU (FLAT ip_scan_kernel)
-#ifndef NRK_SCAN_FLAT
-#define NRK_SCAN_FLAT 0
-#endif
-constexpr bool SCAN_FLAT = NRK_SCAN_FLAT;
 
 // list pre-pass of the one-pass scan: n_pre = min(SCAN_PRE_MAX, n / 6) tiles
-// of an n-tile range, none below SCAN_PRE_MIN tiles (dev: -DNRK_SCAN_PRE_MAX=0
-// turns it off)
-#ifndef NRK_SCAN_PRE_MAX
-#define NRK_SCAN_PRE_MAX 64
-#endif
-#ifndef NRK_SCAN_PRE_DIV
-#define NRK_SCAN_PRE_DIV 6
-#endif
-#ifndef NRK_SCAN_SHARD_PRE_DIV
-#define NRK_SCAN_SHARD_PRE_DIV 6
-#endif
-constexpr int SCAN_PRE_MAX = NRK_SCAN_PRE_MAX, SCAN_PRE_MIN = 128, SCAN_PRE_DIV = NRK_SCAN_PRE_DIV,
-              SCAN_SHARD_PRE_DIV = NRK_SCAN_SHARD_PRE_DIV;
+// of an n-tile range, none below SCAN_PRE_MIN tiles
+constexpr int SCAN_PRE_MAX = 64, SCAN_PRE_MIN = 128, SCAN_PRE_DIV = 6, SCAN_SHARD_PRE_DIV = 6;
 // (lane bit of m) ? T : F, one v_cndmask_b32 on the compare's SGPR lane mask
 // with inline constants (0..64); sel_mask_v: (lane bit of m) ? T : f
 template <int F, int T>
@@ -376,17 +330,6 @@ __device__ unsigned long long scan_stamps[1024 * 16];
     } while (0)
 #endif
 
-// Per-user screen record (uinfo): theta_lb (scaled), eps (scaled), the
-// exact power-of-two scale scl = su * catalog scale, eps (unscaled).
-//
-// Scan: NW waves x UG x 32 users per workgroup share one NSL-slot LDS ring of
-// catalog tiles (8 KB, or one 16-KB block at dim 256).  Per tile every wave
-// reads the tile's A fragments once and runs TB x DS x UG MFMAs.
-// One segment: user block ub over the tiles [tile_lo, tile_hi).  FLAT (see
-// ip_scan_kernel): seg 1 is the second part of a user block split between
-// two workgroups -- its appends fill the lists from their last slot down, its
-// counts go to acnt1 and its list bound to lb1; a workgroup that scans a
-// whole block (whole) clears the block's seg-1 outputs.
 // Config-4 shard list bound of one user (lane pair (q, h)): the bnd_m largest
 // values of its two lanes' final lists (t: descending, +inf placeholders in
 // front, jk + 1 real values) as exact lower bounds v / scl - eps (rounded down
@@ -436,47 +379,81 @@ __device__ __forceinline__ void list_bound_out(const float (&t)[MT], bool live, 
     }
 }
 
-// the scan's LDS: the NSL-tile ring and the LDS append stage (LDSAPP): per
-// (wave, group) STG_C entry slots x 64 lanes x 8 B, entry-major (slot e of
-// lane l at e * 512 + l * 8: any mix of per-lane slots is bank-conflict
-// free), sized to what the ring leaves of the CU's LDS share
-template <int DP, int NW, int NSL, int UG, int WPE, bool TAPP>
-struct ScanLds {
-    static constexpr int BLOCK_BYTES = 64 * DP;
-    static constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
-    static constexpr int TILE_BYTES = TB * BLOCK_BYTES;
-    static constexpr int WG_PER_CU = (WPE * 4) / NW > 0 ? (WPE * 4) / NW : 1;
-    static constexpr int STG_RAW = (163840 / WG_PER_CU - NSL * TILE_BYTES) / (NW * UG * 512);
-    static constexpr bool LDSAPP = SCAN_LDSAPP && !TAPP && SCAN_APP_GRP && TB > 1 && STG_RAW >= TB + 1;
-    static constexpr int STG_C = LDSAPP ? (STG_RAW < 8 ? STG_RAW : 8) : 1;
-    static constexpr int RING = NSL * TILE_BYTES;
-    static constexpr int STG = LDSAPP ? NW * UG * STG_C * 512 : 16;
-};
+// One user's scan setup (lane pair (q, h) of a 32-user group): the fp16 B
+// operand (scaled by a power of two su), and the screen's error bound eps;
+// returns the user's scaled record.
+//   |fp16 score - exact| = |du.v + u.dv + du.dv + accumulation| with du, dv
+//   the actual fp16 rounding errors of this user and of the items:
+//     <= ||du|| max||v|| + ||u|| max||dv|| + ||du|| max||dv||
+//        + (2^-15 + D 2^-23) ||u|| max||v||  (fp32 accumulation of the exact
+//          fp16 products in any order);
+//   ||du|| is measured here, max||dv|| by catalog_dnorm_kernel.
+template <int DS>
+__device__ __forceinline__ void scan_user_setup(const float* __restrict__ users, int n_users, int dim, int user,
+                                                int h, float vmax, float dvmax, float sv_scale, f16x8 (&uf)[DS],
+                                                float& eps, float& scl, bool& live) {
+    constexpr int DP = DS * 16;
+    const bool active = user < n_users;
+    float uval[DS][8];
+    float nrm2 = 0.0f, uabs = 0.0f;
+    const float* urow = users + (size_t)(active ? user : 0) * dim;
+#pragma unroll
+    for (int s = 0; s < DS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int d = 16 * s + 8 * h + e;
+            const float f = (active && d < dim) ? urow[d] : 0.0f;
+            uval[s][e] = f;
+            nrm2 += f * f;
+            uabs = fmaxf(uabs, fabsf(f));
+        }
+    nrm2 += __shfl_xor(nrm2, 32, WAVE);
+    uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
+    const float su = pow2_scale(uabs);
+    float du2 = 0.0f;  // ||fp16(u su) - u su||^2 (scaled units; each difference exact)
+#pragma unroll
+    for (int s = 0; s < DS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float a = uval[s][e] * su;
+            uf[s][e] = (_Float16)a;
+            const float d = (float)uf[s][e] - a;
+            du2 += d * d;
+        }
+    du2 += __shfl_xor(du2, 32, WAVE);
+    const float nu = sqrtf(nrm2), ndu = sqrtf(du2) / su;
+    const float ceps = 3.0517578e-5f + (float)DP * 1.1920929e-7f;
+    eps = (nrm2 == 0.0f) ? 0.0f : (ndu * vmax + nu * dvmax + ndu * dvmax + ceps * nu * vmax) * 1.0001f + 1e-30f;
+    scl = su * sv_scale;  // scores are scaled by scl (an exact power of 2)
+    // zero users (all scores exactly 0) are answered by the refine directly
+    live = active && nrm2 > 0.0f;
+}
 
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD, int IE, bool TAPP, bool FLAT,
-          bool DOWN = false>
-__device__ __forceinline__ void ip_scan_seg(
-    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
-    int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
-    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int n_pre, int pstride,
-    float* __restrict__ bnd, int bnd_m, int ub, int seg, bool whole, int32_t* __restrict__ acnt1,
-    float* __restrict__ lb1, uint8_t* smem, uint8_t* stg) {
-    constexpr bool APP = true;  // (the two-pass screen's append-free pass 1 is gone)
+// Per-user screen record (uinfo): theta_lb (scaled), eps (scaled), the
+// exact power-of-two scale scl = su * catalog scale, eps (unscaled).
+//
+// The scan (every shape but the warp-specialized one below): workgroup ub
+// takes user block ub -- NW waves x UG x 32 users -- over the tiles
+// [tile_lo, tile_hi); the waves share one NSL-slot LDS ring of catalog tiles
+// (8 KB, or one 16-KB block at dim 256).  Per tile every wave reads the tile's
+// A fragments and runs TB x DS x UG MFMAs.
+template <int DP, int NW, int NSL, int UG, int MT, int WPE>
+__global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
+    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items, int dim, int k,
+    int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt, float4* __restrict__ uinfo, int tile_lo,
+    int tile_hi, int n_pre, int pstride, float* __restrict__ bnd, int bnd_m) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
     constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
     constexpr int TILE_BYTES = TB * BLOCK_BYTES;
     constexpr int LPT = TILE_BYTES / (NW * 1024);  // 1-KB LDS-DMA pieces per wave per tile
     static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
-    static_assert(!FULLREAD || (TB * DS) % 8 == 0, "fragment groups of 8");
     static_assert(NSL >= 2, "ring");
-    // smem: the ring (NSL tiles); stg: the LDS append stage (LDSAPP) -- both
-    // declared by ip_scan_kernel (scan_lds)
-    constexpr bool LDSAPP = ScanLds<DP, NW, NSL, UG, WPE, TAPP>::LDSAPP;
-    constexpr int STG_C = ScanLds<DP, NW, NSL, UG, WPE, TAPP>::STG_C;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NSL * TILE_BYTES];
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, q = lane & 31;
+    const int ub = blockIdx.x;
     const int ubase = ub * (NW * 32 * UG) + wave * (32 * UG);
 #if NRK_SCAN_STAMP
     uint64_t sstp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -500,51 +477,12 @@ __device__ __forceinline__ void ip_scan_seg(
 #pragma unroll
     for (int g = 0; g < UG; ++g) {
         const int user = ubase + g * 32 + q;
-        const bool active = user < n_users;
-        float uval[DS][8];
-        float nrm2 = 0.0f, uabs = 0.0f;
-        const float* urow = users + (size_t)(active ? user : 0) * dim;
-#pragma unroll
-        for (int s = 0; s < DS; ++s)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int d = 16 * s + 8 * h + e;
-                const float f = (active && d < dim) ? urow[d] : 0.0f;
-                uval[s][e] = f;
-                nrm2 += f * f;
-                uabs = fmaxf(uabs, fabsf(f));
-            }
-        nrm2 += __shfl_xor(nrm2, 32, WAVE);
-        uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
-        const float su = pow2_scale(uabs);
-        float du2 = 0.0f;  // ||fp16(u su) - u su||^2 (scaled units; each difference exact)
-#pragma unroll
-        for (int s = 0; s < DS; ++s)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float a = uval[s][e] * su;
-                ufrag[g][s][e] = (_Float16)a;
-                const float d = (float)ufrag[g][s][e] - a;
-                du2 += d * d;
-            }
-        du2 += __shfl_xor(du2, 32, WAVE);
-        // |fp16 score - exact| = |du.v + u.dv + du.dv + accumulation| with du, dv
-        // the actual fp16 rounding errors of this user and of the items:
-        //   <= ||du|| max||v|| + ||u|| max||dv|| + ||du|| max||dv||
-        //      + (2^-15 + D 2^-23) ||u|| max||v||  (fp32 accumulation of the exact
-        //        fp16 products in any order);
-        // ||du|| is measured here, max||dv|| by catalog_dnorm_kernel.
-        const float nu = sqrtf(nrm2), ndu = sqrtf(du2) / su;
-        const float ceps = 3.0517578e-5f + (float)DP * 1.1920929e-7f;
-        const float eps = (nrm2 == 0.0f) ? 0.0f
-                                         : (ndu * vmax + nu * dvmax + ndu * dvmax + ceps * nu * vmax) * 1.0001f + 1e-30f;
-        const float scl = su * sv_scale;  // scores below are scaled by scl (exact power of 2)
+        float eps, scl;
+        scan_user_setup<DS>(users, n_users, dim, user, h, vmax, dvmax, sv_scale, ufrag[g], eps, scl, live[g]);
         eps_s[g] = eps * scl;
-        // the user's record now (its list bound .x at the end; a tail part
-        // writes none): scl and eps are not held through the scan
-        if (!DOWN && h == 0 && active) uinfo[user] = make_float4(-INFINITY, eps_s[g], scl, eps);
-        // zero users (all scores exactly 0) are answered by the refine directly
-        live[g] = active && nrm2 > 0.0f;
+        // the user's record now (its list bound .x at the end): scl and eps
+        // are not held through the scan
+        if (h == 0 && user < n_users) uinfo[user] = make_float4(-INFINITY, eps_s[g], scl, eps);
         tau[g] = live[g] ? -FLT_MAX : INFINITY;
 #pragma unroll
         for (int i = 0; i < MT; ++i) t[g][i] = (live[g] && i >= MT - 1 - jk) ? -INFINITY : INFINITY;
@@ -563,18 +501,8 @@ __device__ __forceinline__ void ip_scan_seg(
         pos[g] = (uint32_t)((g * 32 + q) * 2 + h) * (uint32_t)m2;
         lim[g] = pos[g] + (uint32_t)m2 - 1u;
     }
-    // the list slot of position x (seg 1 of a FLAT launch: from the last slot down)
-    constexpr bool down = FLAT && DOWN;
-    (void)seg;
-    auto slot = [&](uint32_t x, int g) -> uint32_t {
-        const uint32_t m = min(x, lim[g]);
-        if constexpr (down) return lim[g] + (lim[g] + 1u - (uint32_t)m2) - m;
-        return m;
-    };
-    auto app_store = [&](uint32_t e, uint2 v) {
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(wapp) + (e << 3)) = v;
-    };
-    // the same store from the lanes with a set only, without a branch: the
+    auto slot = [&](uint32_t x, int g) -> uint32_t { return min(x, lim[g]); };
+    // the store from the lanes with a set only, without a branch: the
     // compiler's form (s_and_saveexec, s_cbranch_execz, store, s_or exec per
     // half-block) cost ~55 cycles per (group, block) in the phase stamps,
     // mostly the branch; a store with no lane left is a no-op
@@ -589,46 +517,6 @@ __device__ __forceinline__ void ip_scan_seg(
             : "=&s"(sv)
             : "s"(m), "v"(off), "v"(d), "s"(wapp)
             : "memory", "scc");  // s_and_saveexec writes SCC
-    };
-    // LDS stage (LDSAPP): nb = the lane's staged entries per group, pos = the
-    // list position of its first staged entry.  Slot e of group g of this
-    // lane at stg_lane + (g * STG_C + e) * 512.
-    uint32_t nb[UG];
-#pragma unroll
-    for (int g = 0; g < UG; ++g) nb[g] = 0u;
-    const uint32_t stg_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(stg) +
-                              (uint32_t)__builtin_amdgcn_readfirstlane(wave) * (UG * STG_C * 512) + lane * 8;
-    // (score, id) into slot n of group G, from the lanes of m only
-    auto stg_store_if = [&](auto gc, uint64_t m, uint32_t n, uint32_t score, uint32_t id) {
-        constexpr int G = decltype(gc)::value;
-        const uint32_t a = (n << 9) + stg_lane;
-        const uint64_t d = ((uint64_t)id << 32) | score;
-        uint64_t sv;
-        asm volatile(
-            "s_and_saveexec_b64 %0, %1\n\t"
-            "ds_write_b64 %2, %3 offset:%4\n\t"
-            "s_mov_b64 exec, %0"
-            : "=&s"(sv)
-            : "s"(m), "v"(a), "v"(d), "n"(G * STG_C * 512)
-            : "memory", "scc");
-    };
-    // group G's staged entries -> its HBM list (slot e of every lane with
-    // more than e entries -> list position pos + e, clamped like the direct
-    // appends); rare (a lane's stage nearly full), so a run-time loop
-    auto stg_flush = [&](auto gc) {
-        constexpr int G = decltype(gc)::value;
-        for (uint32_t e = 0; e < (uint32_t)STG_C; ++e) {
-            const uint64_t m = __builtin_amdgcn_ballot_w64(nb[G] > e);
-            if (!m) break;
-            uint64_t d;
-            asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
-                         : "=v"(d)
-                         : "v"(stg_lane + e * 512u), "n"(G * STG_C * 512)
-                         : "memory");
-            app_store_if(m, slot(pos[G] + e, G), make_uint2((uint32_t)d, (uint32_t)(d >> 32)));
-        }
-        pos[G] += nb[G];
-        nb[G] = 0u;
     };
 
     const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)(smem);
@@ -660,26 +548,8 @@ __device__ __forceinline__ void ip_scan_seg(
     // all fragment reads and their wait in inline asm: hipcc's waitcnt pass
     // would otherwise drain the in-flight LDS-DMA (the ring prefetch) in
     // front of a compiler-visible LDS access, and a separate wait statement
-    // would let the compiler copy an output before the data landed
-    auto read_frags = [&](int sl, u32x4 (&afr)[TB * DS]) {
-        const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES);
-#pragma unroll
-        for (int g = 0; g < TB * DS; g += 8) {
-            u32x4* f = &afr[g];
-            asm volatile(
-                "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:1024\n\t"
-                "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
-                "ds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:5120\n\t"
-                "ds_read_b128 %6, %8 offset:6144\n\tds_read_b128 %7, %8 offset:7168\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]),
-                  "=&v"(f[6]), "=&v"(f[7])
-                : "v"(base + 1024u * g)
-                : "memory");
-        }
-    };
-    // one block's DS fragments (FULLREAD = false: fewer live registers,
-    // one LDS round trip per block)
+    // would let the compiler copy an output before the data landed.
+    // One block's DS fragments, one LDS round trip per block:
     auto read_block = [&](int sl, int b, u32x4 (&af)[DS]) {
         const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
         if constexpr (DS == 1) {
@@ -697,7 +567,7 @@ __device__ __forceinline__ void ip_scan_seg(
     // the wait for block b's data and the issue of block b + 1's reads are one
     // asm statement whose operands tie both register sets, so nothing reads
     // (or copies) a fragment before its wait
-    constexpr bool PF = !FULLREAD && DS == 2;
+    constexpr bool PF = DS == 2;
     auto pf_issue = [&](int sl, int b, u32x4 (&af)[DS]) {
         const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
         asm volatile("ds_read_b128 %0, %2 offset:0\n\tds_read_b128 %1, %2 offset:1024"
@@ -716,133 +586,82 @@ __device__ __forceinline__ void ip_scan_seg(
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1])::"memory");
     };
     const int full_tiles = tail_blk / TB;  // tiles whose blocks are all full
-    float pend[UG];  // IE = 2: the lane's largest max since its group's last insert
-#pragma unroll
-    for (int g = 0; g < UG; ++g) pend[g] = -INFINITY;
     // the tile's MFMAs and half-block maxima (mx); the bookkeeping on them
-    // (appends, inserts) is book() below
-    auto tile = [&](int tt, int sl, const u32x4 (&afr)[FULLREAD ? TB * DS : 1], auto mask_c,
-                    float (&mx)[UG][TB]) __attribute__((always_inline)) {
+    // (appends, inserts) is book() below.  Software pipeline over the TB x UG
+    // (block, group) steps: step j's DS MFMAs issue while step j - LAG's 16
+    // accumulators reduce, so the reduction VALU fills the MFMA shadows
+    // instead of waiting on the wave's own MFMA results; LAG + 1 accumulator
+    // sets instead of UG (LAG = 2 gives the reduced step's last MFMA a whole
+    // step to land before its first reduction VALU reads it).  The reduction
+    // is a depth-3 tree of v_max3 (max is order-free: the same maxima as a
+    // sequential chain).
+    auto tile = [&](int tt, int sl, auto mask_c, float (&mx)[UG][TB]) __attribute__((always_inline)) {
         constexpr bool MASK = decltype(mask_c)::value;
         u32x4 afp[DS];
         if constexpr (PF) pf_issue(sl, 0, afp);
-        if constexpr (SCAN_SWP && !FULLREAD) {
-            // Software pipeline over the TB x UG (block, group) steps: step j's
-            // DS MFMAs issue while step j - 1's 16 accumulators reduce, so the
-            // reduction VALU fills the MFMA shadows instead of waiting on the
-            // wave's own MFMA results; two accumulator sets instead of UG.
-            // The reduction is a depth-3 tree of v_max3 (max is order-free:
-            // the same maxima as a sequential chain).
-            auto red = [&](const f32x16& a, int bb, int gg) __attribute__((always_inline)) {
-                float x[16];
+        auto red = [&](const f32x16& a, int bb, int gg) __attribute__((always_inline)) {
+            float x[16];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    x[r] = a[r];
-                    if constexpr (MASK) {
-                        const int row = (tt * TB + bb) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        if (row >= n_items) x[r] = -INFINITY;
-                    }
+            for (int r = 0; r < 16; ++r) {
+                x[r] = a[r];
+                if constexpr (MASK) {
+                    const int row = (tt * TB + bb) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row >= n_items) x[r] = -INFINITY;
                 }
-                auto m3 = [](float p, float q, float s) { return fmaxf(fmaxf(p, q), s); };
-                const float m0 = m3(x[0], x[1], x[2]), m1 = m3(x[3], x[4], x[5]), m2 = m3(x[6], x[7], x[8]);
-                const float m4 = m3(x[9], x[10], x[11]), m5 = m3(x[12], x[13], x[14]);
-                mx[gg][bb] = fmaxf(m3(m0, m1, m2), m3(m4, m5, x[15]));
-            };
-            // LAG = SCAN_SWP: step j reduces step j - LAG (LAG + 1 accumulator
-            // sets; LAG = 2 gives the reduced step's last MFMA a whole step to
-            // land before its first reduction VALU reads it)
-            constexpr int LAG = SCAN_SWP, NACC = LAG + 1, NSTEP = TB * UG;
-            f32x16 acc[NACC];
-            u32x4 afb[DS];
-            static_for<TB>([&](auto bc) {
-                constexpr int b = decltype(bc)::value;
-                if constexpr (PF) {
-                    u32x4 afn[DS];
-                    if constexpr (b + 1 < TB) pf_wait_issue(afp, sl, b + 1, afn);
-                    else pf_wait(afp);
-#pragma unroll
-                    for (int s = 0; s < DS; ++s) afb[s] = afp[s];
-                    if constexpr (b + 1 < TB) {
-#pragma unroll
-                        for (int s = 0; s < DS; ++s) afp[s] = afn[s];
-                    }
-                } else {
-                    read_block(sl, b, afb);
-                }
-                static_for<UG>([&](auto gc) {
-                    constexpr int g = decltype(gc)::value, j = b * UG + g;
-                    f32x16& A = acc[j % NACC];
-                    A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[0]), ufrag[g][0],
-                                                               f32x16{}, 0, 0, 0);
-#pragma unroll
-                    for (int s = 1; s < DS; ++s)
-                        A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[s]), ufrag[g][s], A,
-                                                                   0, 0, 0);
-                    if constexpr (j >= LAG) red(acc[(j - LAG) % NACC], (j - LAG) / UG, (j - LAG) % UG);
-                    // the order the scheduler must keep: each MFMA of step j
-                    // followed by its share of step j - LAG's 8 reduction VALU
-                    if constexpr (!MASK) {
-#pragma unroll
-                        for (int s = 0; s < DS; ++s) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                            if (j >= LAG) __builtin_amdgcn_sched_group_barrier(0x002, (8 + DS - 1) / DS, 0);
-                        }
-                        // a fence per step: step j - LAG's reduction stays beside step j's MFMAs
-                        if constexpr (LAG > 1) __builtin_amdgcn_sched_barrier(0);
-                    }
-                });
-            });
-            static_for<LAG>([&](auto lc) {
-                constexpr int j = NSTEP - LAG + decltype(lc)::value;
-                red(acc[j % NACC], j / UG, j % UG);
-            });
-            return;
-        }
-#pragma unroll
-        for (int b = 0; b < TB; ++b) {
-            u32x4 afb[DS];
+            }
+            auto m3 = [](float p, float q, float s) { return fmaxf(fmaxf(p, q), s); };
+            const float m0 = m3(x[0], x[1], x[2]), m1 = m3(x[3], x[4], x[5]), m2 = m3(x[6], x[7], x[8]);
+            const float m4 = m3(x[9], x[10], x[11]), m5 = m3(x[12], x[13], x[14]);
+            mx[gg][bb] = fmaxf(m3(m0, m1, m2), m3(m4, m5, x[15]));
+        };
+        constexpr int LAG = 2, NACC = LAG + 1, NSTEP = TB * UG;
+        f32x16 acc[NACC];
+        u32x4 afb[DS];
+        static_for<TB>([&](auto bc) {
+            constexpr int b = decltype(bc)::value;
             if constexpr (PF) {
                 u32x4 afn[DS];
-                if (b + 1 < TB) pf_wait_issue(afp, sl, b + 1, afn);
+                if constexpr (b + 1 < TB) pf_wait_issue(afp, sl, b + 1, afn);
                 else pf_wait(afp);
 #pragma unroll
                 for (int s = 0; s < DS; ++s) afb[s] = afp[s];
-                if (b + 1 < TB) {
+                if constexpr (b + 1 < TB) {
 #pragma unroll
                     for (int s = 0; s < DS; ++s) afp[s] = afn[s];
                 }
-            } else if constexpr (FULLREAD) {
-#pragma unroll
-                for (int s = 0; s < DS; ++s) afb[s] = afr[b * DS + s];
             } else {
                 read_block(sl, b, afb);
             }
-            // the UG independent accumulation chains interleaved, so one
-            // group's reduction overlaps the other's MFMAs
-            f32x16 acc[UG];
+            static_for<UG>([&](auto gc) {
+                constexpr int g = decltype(gc)::value, j = b * UG + g;
+                f32x16& A = acc[j % NACC];
+                A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[0]), ufrag[g][0], f32x16{},
+                                                           0, 0, 0);
 #pragma unroll
-            for (int g = 0; g < UG; ++g) acc[g] = f32x16{};
+                for (int s = 1; s < DS; ++s)
+                    A = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[s]), ufrag[g][s], A, 0,
+                                                               0, 0);
+                if constexpr (j >= LAG) red(acc[(j - LAG) % NACC], (j - LAG) / UG, (j - LAG) % UG);
+                // the order the scheduler must keep: each MFMA of step j
+                // followed by its share of step j - LAG's 8 reduction VALU
+                if constexpr (!MASK) {
 #pragma unroll
-            for (int s = 0; s < DS; ++s)
-#pragma unroll
-                for (int g = 0; g < UG; ++g)
-                    acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, afb[s]), ufrag[g][s],
-                                                                    acc[g], 0, 0, 0);
-#pragma unroll
-            for (int g = 0; g < UG; ++g) {
-                if constexpr (MASK) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int row = (tt * TB + b) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        if (row >= n_items) acc[g][r] = -INFINITY;
+                    for (int s = 0; s < DS; ++s) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        if (j >= LAG) __builtin_amdgcn_sched_group_barrier(0x002, (8 + DS - 1) / DS, 0);
                     }
+                    // a fence per step: step j - LAG's reduction stays beside step j's MFMAs
+                    __builtin_amdgcn_sched_barrier(0);
                 }
-                float v = fmaxf(fmaxf(acc[g][0], acc[g][1]), acc[g][2]);
-#pragma unroll
-                for (int r = 3; r < 15; r += 2) v = fmaxf(fmaxf(v, acc[g][r]), acc[g][r + 1]);
-                mx[g][b] = fmaxf(v, acc[g][15]);
-            }
-        }
+            });
+        });
+        // the last LAG steps' reductions (all NSTEP of them when NSTEP < LAG:
+        // one block of one group at dim 256)
+        constexpr int NTAIL = NSTEP < LAG ? NSTEP : LAG;
+        static_for<NTAIL>([&](auto lc) {
+            constexpr int j = NSTEP - NTAIL + decltype(lc)::value;
+            red(acc[j % NACC], j / UG, j % UG);
+        });
     };
     // tau below the exact lb - 2 eps: c = RN(lb - 2 eps) is within half an ulp
     // of it, |c| 2^-22 >= 2 ulp(c) covers that and the fma's own rounding,
@@ -854,20 +673,7 @@ __device__ __forceinline__ void ip_scan_seg(
         const float tv = fmaxf(__builtin_fmaf(fabsf(c), -0x1p-22f, c) - 0x1p-120f, -FLT_MAX);
         tau[g] = live[g] ? tv : INFINITY;
     };
-    auto lazy_insert = [&](int g) __attribute__((always_inline)) {
-        const float v = pend[g];
-        pend[g] = -INFINITY;
-        const bool in = v > t[g][MT - 1];
-        if (__builtin_amdgcn_ballot_w64(in)) {
-            top_insert<MT>(t[g], in ? v : -INFINITY);
-            retau(g);
-        }
-    };
     auto book = [&](int tt, const float (&mx)[UG][TB], bool ins_ok) __attribute__((always_inline)) {
-#if NRK_SCAN_FLOOR  // dev floor builds (tools/scan_only.py): 1 = no bookkeeping, 2 = no appends, 3 = no inserts
-        if constexpr (NRK_SCAN_FLOOR == 1) return;
-        if constexpr (NRK_SCAN_FLOOR == 3) ins_ok = false;
-#endif
         // the lane's largest max of the tile, per user group
         float vt[UG];
 #pragma unroll
@@ -879,95 +685,29 @@ __device__ __forceinline__ void ip_scan_seg(
         // appends: every half-block max >= tau reaches the user's HBM list
         // (the count runs past the capacity -- the select then sends the user
         // to the exact fallback -- and extra entries land on the last slots).
-        // TAPP: a lane whose tile max passes stores ALL TB maxima of its
-        // tile (one or two 16-B stores, one branch per group instead of one
-        // per block); the others are true half-block maxima below the tau of
-        // their tile, so the select's thresholds (>= theta_lb, >= cut, both
-        // above every tau) never take them.
-        // the lane masks of every half-block max >= tau (compare -> SGPR pair)
-        uint64_t am[APP && !TAPP ? UG : 1][APP && !TAPP ? TB : 1];
+        // The lane masks of every half-block max >= tau (compare -> SGPR pair):
+        uint64_t am[UG][TB];
         uint64_t any_app = 0;
-        if constexpr (!APP) {
-        } else if constexpr (TAPP) {
 #pragma unroll
-            for (int g = 0; g < UG; ++g) any_app |= __builtin_amdgcn_ballot_w64(vt[g] >= tau[g]);
-        } else {
+        for (int g = 0; g < UG; ++g)
 #pragma unroll
-            for (int g = 0; g < UG; ++g)
-#pragma unroll
-                for (int b = 0; b < TB; ++b) {
-                    am[g][b] = __builtin_amdgcn_ballot_w64(mx[g][b] >= tau[g]);
-                    any_app |= am[g][b];
-                }
-        }
-        SC_STAMP(2);
-#if NRK_SCAN_FLOOR == 2
-        any_app = 0;
-#endif
-        if constexpr (APP && !TAPP && SCAN_APP_GRP && TB > 1 && (SCAN_BSEL || LDSAPP)) {
-            // round 5 form of the grouped appends (BSEL / LDSAPP, see above)
-            if (any_app) {
-                const uint32_t hb0 = (uint32_t)(tt * TB * 2) + (uint32_t)h;  // id of block 0's half-block
-                static_for<UG>([&](auto gc) {
-                    constexpr int g = decltype(gc)::value;
-                    uint64_t gm = 0, multi = 0;
-#pragma unroll
-                    for (int b = 0; b < TB; ++b) {
-                        multi |= gm & am[g][b];
-                        gm |= am[g][b];
-                    }
-                    if (gm) {
-                        // a lone append is the tile max's half-block (see below)
-                        const uint32_t fid = (first_set_block<TB>(am[g]) << 1) + hb0;
-                        const uint32_t p0 = LDSAPP ? nb[g] : pos[g];
-                        if constexpr (LDSAPP) stg_store_if(gc, gm, p0, __float_as_uint(vt[g]), fid);
-                        else app_store_if(gm, slot(p0, g), make_uint2(__float_as_uint(vt[g]), fid));
-                        uint32_t p = add_if(p0, gm);
-                        if (multi) {
-                            p = p0;
-#pragma unroll
-                            for (int b = 0; b < TB; ++b) {
-                                const uint32_t idb = hb0 + 2u * b;
-                                if constexpr (LDSAPP) stg_store_if(gc, am[g][b] & multi, p, __float_as_uint(mx[g][b]), idb);
-                                else app_store_if(am[g][b] & multi, slot(p, g), make_uint2(__float_as_uint(mx[g][b]), idb));
-                                p = add_if(p, am[g][b]);
-                            }
-                        }
-                        if constexpr (LDSAPP) {
-                            nb[g] = p;
-                            // room for the next tile's (up to TB) appends
-                            if (__builtin_amdgcn_ballot_w64(p > (uint32_t)(STG_C - TB))) stg_flush(gc);
-                        } else {
-                            pos[g] = p;
-                        }
-                    }
-                });
+            for (int b = 0; b < TB; ++b) {
+                am[g][b] = __builtin_amdgcn_ballot_w64(mx[g][b] >= tau[g]);
+                any_app |= am[g][b];
             }
-        } else if (any_app) {
-#pragma unroll
-            for (int g = 0; g < UG; ++g) {
-                if constexpr (TAPP) {
-                    if (vt[g] >= tau[g]) {
-                        const uint32_t e = min(pos[g], lim[g] + 1u - (uint32_t)TB);
-                        const uint32_t id0 = (uint32_t)(tt * TB * 2 + h);
-                        if constexpr (TB == 1) {
-                            app_store(e, make_uint2(__float_as_uint(mx[g][0]), id0));
-                        } else {
-#pragma unroll
-                            for (int b = 0; b < TB; b += 2)
-                                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(wapp) + ((e + b) << 3)) =
-                                    make_uint4(__float_as_uint(mx[g][b]), id0 + 2u * b, __float_as_uint(mx[g][b + 1]),
-                                               id0 + 2u * (b + 1));
-                        }
-                        pos[g] += TB;
-                    }
-                } else if constexpr (SCAN_APP_GRP && TB > 1) {
+        SC_STAMP(2);
+        if (any_app) {
+            const uint32_t hb0 = (uint32_t)(tt * TB * 2) + (uint32_t)h;  // id of block 0's half-block
+            static_for<UG>([&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                if constexpr (TB > 1) {
                     // one store per group: a lane appends 0 or 1 of its TB
                     // half-blocks per tile nearly always, and when it appends
                     // any, its largest (the tile max vt) is among them -- so a
-                    // single append IS the tile max's half-block; lanes with
-                    // two or more redo theirs in block order from the same slot
-                    // behind a rare scalar branch
+                    // single append IS the tile max's half-block (picked by
+                    // v_cndmask on the compare masks); lanes with two or more
+                    // redo theirs in block order from the same slot behind a
+                    // rare scalar branch
                     uint64_t gm = 0, multi = 0;
 #pragma unroll
                     for (int b = 0; b < TB; ++b) {
@@ -975,89 +715,46 @@ __device__ __forceinline__ void ip_scan_seg(
                         gm |= am[g][b];
                     }
                     if (gm) {
-                        uint32_t fid = (uint32_t)((tt * TB + TB - 1) * 2 + h);
-#pragma unroll
-                        for (int b = TB - 2; b >= 0; --b)
-                            fid = mx[g][b] >= tau[g] ? (uint32_t)((tt * TB + b) * 2 + h) : fid;
+                        const uint32_t fid = (first_set_block<TB>(am[g]) << 1) + hb0;
                         const uint32_t p0 = pos[g];
                         app_store_if(gm, slot(p0, g), make_uint2(__float_as_uint(vt[g]), fid));
-                        pos[g] = add_if(p0, gm);  // one append per lane, unless multi
+                        uint32_t p = add_if(p0, gm);
                         if (multi) {
                             // p ends at p0 + the lane's append count: the same
-                            // as pos for the lanes with one or none
-                            uint32_t p = p0;
+                            // as above for the lanes with one or none
+                            p = p0;
 #pragma unroll
                             for (int b = 0; b < TB; ++b) {
                                 app_store_if(am[g][b] & multi, slot(p, g),
-                                             make_uint2(__float_as_uint(mx[g][b]), (uint32_t)((tt * TB + b) * 2 + h)));
+                                             make_uint2(__float_as_uint(mx[g][b]), hb0 + 2u * b));
                                 p = add_if(p, am[g][b]);
                             }
-                            pos[g] = p;
                         }
+                        pos[g] = p;
                     }
                 } else {
-#pragma unroll
-                    for (int b = 0; b < TB; ++b) {
-                        const uint2 ev = make_uint2(__float_as_uint(mx[g][b]), (uint32_t)((tt * TB + b) * 2 + h));
-                        if constexpr (SCAN_APP_ASM) {
-                            app_store_if(am[g][b], slot(pos[g], g), ev);
-                        } else {
-                            if (mx[g][b] >= tau[g]) app_store(slot(pos[g], g), ev);
-                        }
-                        pos[g] = add_if(pos[g], am[g][b]);
-                    }
+                    app_store_if(am[g][0], slot(pos[g], g), make_uint2(__float_as_uint(mx[g][0]), hb0));
+                    pos[g] = add_if(pos[g], am[g][0]);
                 }
-            }
+            });
         }
         // threshold: maxima enter the lane's top list (a subset of the
         // half-block maxima: the (jk + 1)-th largest stays a lower bound),
         // then tau = (min over the user's two lanes) - 2 eps.  Every inserted
         // value exceeded the lane's list minimum, >= the tau of its tile, so
-        // it was appended.
-        //   IE = 1: every tile, per group, the lane's tile max when some lane
-        //           of the wave has one that enters (branchy);
-        //   IE = 2: no branch: group IG (alternating by tile, from the tile
-        //           loop) inserts the lane's largest max since its last
-        //           insert (pend), -inf (a no-op) when it does not enter.
+        // it was appended.  Every tile, per group, the lane's tile max, when
+        // some lane of the wave has one that enters (skipped when none does,
+        // ~1/4 of the (tile, group)s; -inf inserts nothing).  A pre-pass tile
+        // (!ins_ok): its maxima are in the lists already.
         SC_STAMP(3);
-        if constexpr (SCAN_LAZY && IE == 1) {
-            // LAZY: pend = the lane's largest tile max since its group's last
-            // insert (a pre-pass tile's maxima are in the lists already); group
-            // (tt mod UG) inserts it.  The list stays a set of distinct
-            // half-block maxima (one value per insert), and an inserted value
-            // beat the list minimum at its insert, which bounds every tau since
-            // its tile from above: it was appended at its tile.
-            if (ins_ok) {
-#pragma unroll
-                for (int g = 0; g < UG; ++g) pend[g] = fmaxf(pend[g], vt[g]);
-            }
-#pragma unroll
-            for (int g = 0; g < UG; ++g)
-                if ((tt & (UG - 1)) == g) lazy_insert(g);
-        } else if (!ins_ok) {  // a pre-pass tile: its maxima are in the lists already
-        } else if constexpr (IE == 1) {
+        if (ins_ok) {
 #pragma unroll
             for (int g = 0; g < UG; ++g) {
-                // skipped when no lane of the wave has a record (~1/4 of the
-                // (tile, group)s); -inf inserts nothing
                 const float v = vt[g];
                 const bool in = v > t[g][MT - 1];
-                if (SCAN_INS_BR && !__builtin_amdgcn_ballot_w64(in)) continue;
+                if (!__builtin_amdgcn_ballot_w64(in)) continue;
                 top_insert<MT>(t[g], in ? v : -INFINITY);
                 retau(g);
-            }
-        } else {
-#pragma unroll
-            for (int g = 0; g < UG; ++g) pend[g] = fmaxf(pend[g], vt[g]);
-            // group (tt & 1) (UG = 2) / every other tile (UG = 1): a uniform branch
-#pragma unroll
-            for (int g = 0; g < UG; ++g) {
-                if ((tt & 1) == g) {
-                    const float v = pend[g];
-                    pend[g] = -INFINITY;
-                    top_insert<MT>(t[g], v > t[g][MT - 1] ? v : -INFINITY);
-                    retau(g);
-                }
             }
         }
     };
@@ -1071,7 +768,7 @@ __device__ __forceinline__ void ip_scan_seg(
     // MFMAs.  The book order per wave is unchanged (tile t's appends use the
     // tau left by tile t - 1's inserts), so the lists are identical.
     // (WPE = 4: two workgroups per CU already interleave on every SIMD)
-    const bool late = STAG && WPE == 2 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
+    const bool late = WPE == 2 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
     float mx[UG][TB];  // the LATE half keeps a tile's maxima across the barrier
     int ptt = -1;
     bool pins = true;
@@ -1107,10 +804,8 @@ __device__ __forceinline__ void ip_scan_seg(
         issue_tile(tt + NSL - 1, (it + NSL - 1) % NSL);
         if (late && ptt >= 0) book(ptt, mx, pins);
         const int sl = it % NSL;
-        u32x4 afr[FULLREAD ? TB * DS : 1];
-        if constexpr (FULLREAD) read_frags(sl, afr);
-        if (tt < full_tiles) tile(tt, sl, afr, std::false_type{}, mx);
-        else tile(tt, sl, afr, std::true_type{}, mx);
+        if (tt < full_tiles) tile(tt, sl, std::false_type{}, mx);
+        else tile(tt, sl, std::true_type{}, mx);
         const bool ins_ok = !sampled(tt);
         if (late) {
             ptt = tt;
@@ -1122,53 +817,41 @@ __device__ __forceinline__ void ip_scan_seg(
 #if NRK_SCAN_STAMP
     t_prev = __builtin_readcyclecounter();
 #endif
-    if constexpr (APP && IE == 1) {
-        if (n_pre > 0) {
-            // the pre-pass over the same ring (its own prologue; the trailing
-            // prefetches past the sample are dummies), every wave inserting
-            // right after its tile; the MASK body serves every sampled tile
+    if (n_pre > 0) {
+        // the pre-pass over the same ring (its own prologue; the trailing
+        // prefetches past the sample are dummies), every wave inserting
+        // right after its tile; the MASK body serves every sampled tile
 #pragma unroll
-            for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p * pstride, p);
-            for (int i = 0; i < n_pre; ++i) {
-                const int tt = tile_lo + i * pstride;
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * (NSL - 2)) : "memory");
-                __builtin_amdgcn_s_barrier();
-                issue_tile(tt + (NSL - 1) * pstride, (i + NSL - 1) % NSL);
-                u32x4 afr[FULLREAD ? TB * DS : 1];
-                if constexpr (FULLREAD) read_frags(i % NSL, afr);
-                if (tt < full_tiles) tile(tt, i % NSL, afr, std::false_type{}, mx);
-                else tile(tt, i % NSL, afr, std::true_type{}, mx);
-#pragma unroll
-                for (int g = 0; g < UG; ++g) {
-                    float v = mx[g][0];
-#pragma unroll
-                    for (int b = 1; b < TB; ++b) v = fmaxf(v, mx[g][b]);
-                    const bool in = v > t[g][MT - 1];
-                    if (__builtin_amdgcn_ballot_w64(in)) top_insert<MT>(t[g], in ? v : -INFINITY);
-                }
-            }
-#pragma unroll
-            for (int g = 0; g < UG; ++g) retau(g);
-            // every piece landed and every wave is done with the ring
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p * pstride, p);
+        for (int i = 0; i < n_pre; ++i) {
+            const int tt = tile_lo + i * pstride;
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * (NSL - 2)) : "memory");
             __builtin_amdgcn_s_barrier();
+            issue_tile(tt + (NSL - 1) * pstride, (i + NSL - 1) % NSL);
+            if (tt < full_tiles) tile(tt, i % NSL, std::false_type{}, mx);
+            else tile(tt, i % NSL, std::true_type{}, mx);
+#pragma unroll
+            for (int g = 0; g < UG; ++g) {
+                float v = mx[g][0];
+#pragma unroll
+                for (int b = 1; b < TB; ++b) v = fmaxf(v, mx[g][b]);
+                const bool in = v > t[g][MT - 1];
+                if (__builtin_amdgcn_ballot_w64(in)) top_insert<MT>(t[g], in ? v : -INFINITY);
+            }
         }
+#pragma unroll
+        for (int g = 0; g < UG; ++g) retau(g);
+        // every piece landed and every wave is done with the ring
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
 #pragma unroll
     for (int p = 0; p < NSL - 1; ++p) issue_tile(tile_lo + p, p);
-#if NRK_SCAN_PRIO
-    if (late) __builtin_amdgcn_s_setprio(1);
-#endif
     for (int tt = tile_lo, it = 0; tt < ntile; ++tt, ++it) step(tt, it);
     if (late && ptt >= 0) book(ptt, mx, pins);
-    if constexpr (SCAN_LAZY && IE == 1 && APP) {
-#pragma unroll
-        for (int g = 0; g < UG; ++g) lazy_insert(g);  // the final lists hold every pending max
-    }
-    if constexpr (LDSAPP) static_for<UG>([&](auto gc) { stg_flush(gc); });
 #if NRK_SCAN_STAMP
     SC_STAMP(4);
-    if ((threadIdx.x == 0 || threadIdx.x == NW / 2 * 64) && blockIdx.x < 1024 && APP)
+    if ((threadIdx.x == 0 || threadIdx.x == NW / 2 * 64) && blockIdx.x < 1024)
         for (int k = 0; k < 8; ++k) scan_stamps[blockIdx.x * 16 + (threadIdx.x ? 8 : 0) + k] = sstp[k];
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing dummy pieces
@@ -1178,128 +861,21 @@ __device__ __forceinline__ void ip_scan_seg(
         const float lb = pair_min32(t[g][MT - 1]);
         const int user = ubase + g * 32 + q;
         if (user < n_users) {
-            const int cnt_g = (int)(pos[g] - (lim[g] + 1u - (uint32_t)m2));
-            if (FLAT && down) {
-                acnt1[(size_t)user * 2 + h] = cnt_g;
-                if (h == 0) lb1[user] = live[g] ? lb : -INFINITY;
-            } else {
-                acnt[(size_t)user * 2 + h] = cnt_g;
-                if (h == 0) reinterpret_cast<float*>(uinfo + user)[0] = live[g] ? lb : -INFINITY;
-                if (FLAT && whole) {  // no second part
-                    acnt1[(size_t)user * 2 + h] = 0;
-                    if (h == 0) lb1[user] = -INFINITY;
-                }
-            }
+            acnt[(size_t)user * 2 + h] = (int)(pos[g] - (lim[g] + 1u - (uint32_t)m2));
+            if (h == 0) reinterpret_cast<float*>(uinfo + user)[0] = live[g] ? lb : -INFINITY;
         }
     }
-    // Config-4 shard (bnd != nullptr): per user the bnd_m largest values of
-    // its two lanes' final lists as exact lower bounds v / scl - eps (rounded
-    // down to fp32, descending, -inf padded) -- each list value is a distinct
-    // half-block's fp16 maximum of this range, so each bounds a distinct
-    // item's exact score from below.  The pair's lists (descending, +inf
-    // placeholders in front) are merged in registers: A . reverse(B) is
-    // bitonic, log2(2 MT) half-cleaner stages sort it.  Replaces a pass over
-    // the appended maxima (ip_shard_bound_kernel).  Lists of up to 32 (k <=
-    // 64; longer ones would spill the merge -- those shards keep the pass).
-    if constexpr (MT > 32) {
-    } else if (bnd != nullptr) {
+    // Config-4 shard (bnd != nullptr): per user the bnd_m largest list values
+    // as exact lower bounds (list_bound_out).  Replaces a pass over the
+    // appended maxima (ip_shard_bound_kernel).  Lists of up to 32 (k <= 64;
+    // longer ones would spill the merge -- those shards keep the pass).
+    if constexpr (MT <= 32) {
+        if (bnd != nullptr) {
 #pragma unroll
-        for (int g = 0; g < UG; ++g)
-            list_bound_out<MT>(t[g], live[g], h, ubase + g * 32 + q, n_users, jk, bnd, bnd_m, uinfo);
-    }
-}
-
-// The scan launch.  Not FLAT: workgroup b scans user block b over the whole
-// range.  FLAT (head > 0): the grid fills every workgroup slot of the chip
-// although the user blocks do not divide among them (config 2: 245 blocks,
-// 256 CUs, so 11 CUs sat idle): workgroup b < n_blocks scans the head of
-// block b (tiles [0, head)), workgroup n_blocks + b its tail ([head, T)),
-// with head = c T / (c + 1) rounded up, c = ceil(n_blocks / E), E = the
-// slots the heads leave free: the E free CUs run c tails each while the
-// heads run, so every CU runs about the same number of tiles.  A block has two parts; the tail's appends share the
-// lists with the head's (filling them from the last slot down), its counts
-// go to acnt1 and its list bound to lb1, and the select merges both (each
-// part is a complete one-pass scan of its own tiles with its own list
-// pre-pass, so each part's bound is valid for the user, and the larger is
-// the user's).
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FULLREAD = true, int IE = 1, bool TAPP = false,
-          bool FLAT = false>
-__global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
-    const float* __restrict__ users, int n_users, const uint8_t* __restrict__ catalog, int n_items,
-    int dim, int k, int m2, uint2* __restrict__ app, int32_t* __restrict__ acnt,
-    float4* __restrict__ uinfo, int tile_lo, int tile_hi, int n_pre = 0, int pstride = 1,
-    float* __restrict__ bnd = nullptr, int bnd_m = 0, int head = 0, int32_t* __restrict__ acnt1 = nullptr,
-    float* __restrict__ lb1 = nullptr) {
-    using L = ScanLds<DP, NW, NSL, UG, WPE, TAPP>;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[L::RING];
-    __shared__ __attribute__((aligned(16))) uint8_t stg[L::STG];
-    if constexpr (!FLAT) {
-        ip_scan_seg<DP, NW, NSL, UG, MT, WPE, FULLREAD, IE, TAPP, false>(
-            users, n_users, catalog, n_items, dim, k, m2, app, acnt, uinfo, tile_lo, tile_hi, n_pre, pstride, bnd,
-            bnd_m, blockIdx.x, 0, true, nullptr, nullptr, smem, stg);
-    } else {
-        // workgroup w < n_blocks: the head of block w; the others: the tail of
-        // block w - n_blocks (dispatched after the heads, onto the CUs the
-        // heads leave free, then onto each CU a tail frees)
-        const int T = tile_hi - tile_lo;
-        const int nub = (n_users + NW * 32 * UG - 1) / (NW * 32 * UG);
-        const bool tail = (int)blockIdx.x >= nub;
-        const int b = tail ? (int)blockIdx.x - nub : (int)blockIdx.x;
-        const int t0 = tail ? head : 0, t1 = tail ? T : head, n = t1 - t0;
-        const int np = IE == 1 && n >= (tail ? 32 : SCAN_PRE_MIN) ? min(SCAN_PRE_MAX, n / SCAN_PRE_DIV) : 0;
-        // two copies (the tail's list slots run down): compile-time, no extra registers
-        if (tail)
-            ip_scan_seg<DP, NW, NSL, UG, MT, WPE, FULLREAD, IE, TAPP, true, true>(
-                users, n_users, catalog, n_items, dim, k, m2, app, acnt, uinfo, tile_lo + t0, tile_lo + t1, np,
-                np > 0 ? n / np : 1, nullptr, 0, b, 1, false, acnt1, lb1, smem, stg);
-        else
-            ip_scan_seg<DP, NW, NSL, UG, MT, WPE, FULLREAD, IE, TAPP, true, false>(
-                users, n_users, catalog, n_items, dim, k, m2, app, acnt, uinfo, tile_lo + t0, tile_lo + t1, np,
-                np > 0 ? n / np : 1, nullptr, 0, b, 0, head >= T, acnt1, lb1, smem, stg);
-    }
-}
-
-// One user's scan setup (lane pair (q, h) of a 32-user group): the fp16 B
-// operand (scaled by a power of two su), and the screen's error bound eps
-// (see ip_scan_seg); returns the user's scaled record.
-template <int DS>
-__device__ __forceinline__ void scan_user_setup(const float* __restrict__ users, int n_users, int dim, int user,
-                                                int h, float vmax, float dvmax, float sv_scale, f16x8 (&uf)[DS],
-                                                float& eps, float& scl, bool& live) {
-    constexpr int DP = DS * 16;
-    const bool active = user < n_users;
-    float uval[DS][8];
-    float nrm2 = 0.0f, uabs = 0.0f;
-    const float* urow = users + (size_t)(active ? user : 0) * dim;
-#pragma unroll
-    for (int s = 0; s < DS; ++s)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int d = 16 * s + 8 * h + e;
-            const float f = (active && d < dim) ? urow[d] : 0.0f;
-            uval[s][e] = f;
-            nrm2 += f * f;
-            uabs = fmaxf(uabs, fabsf(f));
+            for (int g = 0; g < UG; ++g)
+                list_bound_out<MT>(t[g], live[g], h, ubase + g * 32 + q, n_users, jk, bnd, bnd_m, uinfo);
         }
-    nrm2 += __shfl_xor(nrm2, 32, WAVE);
-    uabs = fmaxf(uabs, __shfl_xor(uabs, 32, WAVE));
-    const float su = pow2_scale(uabs);
-    float du2 = 0.0f;
-#pragma unroll
-    for (int s = 0; s < DS; ++s)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float a = uval[s][e] * su;
-            uf[s][e] = (_Float16)a;
-            const float d = (float)uf[s][e] - a;
-            du2 += d * d;
-        }
-    du2 += __shfl_xor(du2, 32, WAVE);
-    const float nu = sqrtf(nrm2), ndu = sqrtf(du2) / su;
-    const float ceps = 3.0517578e-5f + (float)DP * 1.1920929e-7f;
-    eps = (nrm2 == 0.0f) ? 0.0f : (ndu * vmax + nu * dvmax + ndu * dvmax + ceps * nu * vmax) * 1.0001f + 1e-30f;
-    scl = su * sv_scale;
-    live = active && nrm2 > 0.0f;
+    }
 }
 
 // Warp-specialized scan (WS, round 5; D = 32, k <= 32: config 2 and every
@@ -1890,58 +1466,41 @@ __device__ __forceinline__ void sh_load(const uint2* s0, const uint2* s1, int a0
 // band = every appended entry >= cut = theta - 2 eps (rounded down); an
 // item with exact score >= cut + eps has an fp16 score >= cut, so its
 // half-block max was >= every tau of the scan and was appended.
-template <bool FLAT>
 __global__ __launch_bounds__(256) void ip_select_kernel(
     int64_t n_users, int k, int m2, int bandcap, const uint2* __restrict__ app,
     const int32_t* __restrict__ acnt, const float4* __restrict__ uinfo, uint2* __restrict__ cand,
     int32_t* __restrict__ cand_cnt, float2* __restrict__ ucut, int32_t* __restrict__ ovf_flag,
-    int32_t* __restrict__ ovf_list, int32_t* __restrict__ ovf_count, const int32_t* __restrict__ acnt1,
-    const float* __restrict__ lb1) {
+    int32_t* __restrict__ ovf_list, int32_t* __restrict__ ovf_count) {
     __shared__ __attribute__((aligned(16))) uint32_t sel[4][IP_SEL + 4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * 4;
     const unsigned long long lt = (1ull << lane) - 1ull;
     // persistent waves (see the shard kernels): the next user's counts and
-    // record load during this one; entries load SH_ENT x 64 at a time.  A
-    // FLAT scan's tail part (acnt1, lb1; zeros / -inf otherwise) fills each
-    // list from its last slot down: the user's entries are list 0 [0, a0),
-    // list 1 [0, a1), then the tails, and the list bound is the larger one.
+    // record load during this one; entries load SH_ENT x 64 at a time (the
+    // user's entries: list 0 [0, a0), then list 1 [0, a1))
     int64_t u = (int64_t)blockIdx.x * 4 + wave;
-    int2 ac_n = make_int2(0, 0), ad_n = make_int2(0, 0);
+    int2 ac_n = make_int2(0, 0);
     float4 inf_n = make_float4(0.f, 0.f, 0.f, 0.f);
-    float lb1_n = -INFINITY;
     if (u < n_users) {
         ac_n = reinterpret_cast<const int2*>(acnt)[u];
-        if (FLAT) ad_n = reinterpret_cast<const int2*>(acnt1)[u];
         inf_n = uinfo[u];
-        if (FLAT) lb1_n = lb1[u];
     }
     for (; u < n_users; u += nw) {
-        const int a0 = ac_n.x, a1 = ac_n.y, d0 = ad_n.x, d1 = ad_n.y;
-        float4 inf = inf_n;
-        if (FLAT) inf.x = fmaxf(inf.x, lb1_n);
+        const int a0 = ac_n.x, a1 = ac_n.y;
+        const float4 inf = inf_n;
         if (u + nw < n_users) {
             ac_n = reinterpret_cast<const int2*>(acnt)[u + nw];
-            if (FLAT) ad_n = reinterpret_cast<const int2*>(acnt1)[u + nw];
             inf_n = uinfo[u + nw];
-            if (FLAT) lb1_n = lb1[u + nw];
         }
-        bool ovf = a0 + d0 > m2 || a1 + d1 > m2;
-        const int n = ovf ? 0 : a0 + a1 + d0 + d1;
+        bool ovf = a0 > m2 || a1 > m2;
+        const int n = ovf ? 0 : a0 + a1;
         const uint2* s0 = app + (size_t)(2 * u) * m2;
         const uint2* s1 = s0 + m2;
         auto sh_load = [&](int n_, int b0, int lane_, uint2 (&ent)[SH_ENT]) {
 #pragma unroll
             for (int j = 0; j < SH_ENT; ++j) {
                 const int e = b0 + j * WAVE + lane_;
-                const uint2* src;
-                if constexpr (FLAT)
-                    src = e < a0 ? s0 + e
-                          : e < a0 + a1 ? s1 + (e - a0)
-                          : e < a0 + a1 + d0 ? s0 + (m2 - 1 - (e - a0 - a1))
-                                             : s1 + (m2 - 1 - (e - a0 - a1 - d0));
-                else
-                    src = e < a0 ? s0 + e : s1 + (e - a0);
+                const uint2* src = e < a0 ? s0 + e : s1 + (e - a0);
                 ent[j] = e < n_ ? *src : make_uint2(0u, 0u);
             }
         };
@@ -2421,241 +1980,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRK_REFINE_
     }
     wave_bitonic_sort<SE>(x);
     emit(x, SE);
-}
-
-// ----------------------------------------------- refine by half-block --
-// The one-GPU finish for dims 16 / 32 / 64 (the half-block-major copy), as
-// five light launches instead of ip_refine_kernel's wave per user.  The
-// per-user refine gathers every band half-block (1 KB of fp16 at D = 32) for
-// each of the ~32 band entries of each user: 8 GB of L2 / Infinity-Cache
-// gathers per config-2 launch, although the catalog has only 23 MB of them.
-// Inverted, each half-block is read once per bucket of the users whose band
-// holds it (about 350 at config 2), and the per-pair traffic is the user's
-// fp32 row (128 B):
-//   hb_count   -- li = atomicAdd(cnt[hb]) per band entry (its place in the
-//                 half-block's bucket);
-//   hb_scan    -- bucket offsets (exclusive scan of cnt);
-//   hb_scatter -- bucket[off[hb] + li] = (user, hb): users grouped by half-block;
-//   hb_score   -- one wave per 64 bucket entries: per half-block segment, the
-//                 16 items' fp16 A fragment once and the users in groups of 16
-//                 as the B operand of v_mfma_f32_16x16x32_f16 (16 items x 16
-//                 users per MFMA; the same fp16 values and scale as the screen,
-//                 fp32 accumulation in any order stays within eps); an item
-//                 reaching the user's cut gets the exact fp64 score (the
-//                 oracle's sequential sum), kept at >= cut + eps, appended to
-//                 the user's survivor list (atomic count, SVB slots);
-//   hb_final   -- per user: the survivors sorted (score desc, row asc), the
-//                 top k written; zero users answered directly; more than SVB
-//                 survivors -> the exact path, as in ip_refine_kernel.
-// Rows and scores are the refine's bit for bit: the same candidate set (every
-// band item with fp16 score >= cut and exact score >= cut + eps), the same
-// exact sums and order.
-struct Surv {
-    double s;
-    int32_t row;
-    int32_t pad;
-};
-
-// thread per user: each band slot j < cand_cnt[u] takes a place in its
-// half-block's bucket
-__global__ __launch_bounds__(256) void ip_hb_count_kernel(int64_t n_users, int bandcap, const uint2* __restrict__ cand,
-                                                          const int32_t* __restrict__ cand_cnt,
-                                                          int32_t* __restrict__ hb_cnt, int32_t* __restrict__ li) {
-    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_users;
-         u += (int64_t)gridDim.x * blockDim.x) {
-        const int n = cand_cnt[u];
-        const size_t f0 = (size_t)u * bandcap;
-        for (int j = 0; j < n; ++j) li[f0 + j] = atomicAdd(&hb_cnt[cand[f0 + j].y], 1);
-    }
-}
-
-// exclusive scan of n counts -> off[0..n] (one 1024-thread workgroup: each
-// thread sums a contiguous chunk, the chunk sums are scanned in LDS)
-__global__ __launch_bounds__(1024) void ip_hb_scan_kernel(const int32_t* __restrict__ cnt, int64_t n,
-                                                          int32_t* __restrict__ off) {
-    __shared__ int32_t part[1024];
-    const int t = threadIdx.x;
-    const int64_t per = (n + 1023) / 1024, lo = t * per, hi = lo + per < n ? lo + per : n;
-    int32_t sum = 0;
-    for (int64_t i = lo; i < hi; ++i) sum += cnt[i];
-    part[t] = sum;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int32_t v = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    int32_t run = part[t] - sum;  // exclusive prefix of this chunk
-    for (int64_t i = lo; i < hi; ++i) {
-        off[i] = run;
-        run += cnt[i];
-    }
-    if (t == 1023) off[n] = part[1023];
-}
-
-__global__ __launch_bounds__(256) void ip_hb_scatter_kernel(int64_t n_users, int bandcap,
-                                                            const uint2* __restrict__ cand,
-                                                            const int32_t* __restrict__ cand_cnt,
-                                                            const int32_t* __restrict__ hb_off,
-                                                            const int32_t* __restrict__ li,
-                                                            uint2* __restrict__ bucket) {
-    for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n_users;
-         u += (int64_t)gridDim.x * blockDim.x) {
-        const int n = cand_cnt[u];
-        const size_t f0 = (size_t)u * bandcap;
-        for (int j = 0; j < n; ++j) {
-            const uint32_t hb = cand[f0 + j].y;
-            bucket[hb_off[hb] + li[f0 + j]] = make_uint2((uint32_t)u, hb);
-        }
-    }
-}
-
-// DP = 16, 32 or 64 (dim == DP): KS k-steps of 32 dims
-template <int DP>
-__global__ __launch_bounds__(256) void ip_hb_score_kernel(
-    const float* __restrict__ users, const float* __restrict__ items, const uint8_t* __restrict__ catalog,
-    int64_t n_items, const uint2* __restrict__ bucket, const int32_t* __restrict__ hb_total,
-    const float2* __restrict__ ucut, const float4* __restrict__ uinfo, int32_t* __restrict__ scnt,
-    Surv* __restrict__ surv, int svb) {
-    constexpr int KS = DP <= 32 ? 1 : DP / 32;
-    const int lane = threadIdx.x & 63;
-    const int64_t nwin = ((int64_t)*hb_total + 63) / 64, nw = (int64_t)gridDim.x * 4;
-    const int64_t nblk = (n_items + 31) >> 5;
-    const CatalogHdr* hdr = reinterpret_cast<const CatalogHdr*>(catalog + (size_t)nblk * 64 * DP);
-    const float inv_cs = 1.0f / hdr->scale;  // exact: a power of two
-    const uint8_t* hbc = catalog + catalog_hb_offset(n_items, DP);
-    const int64_t tot = *hb_total;
-    const int col = lane & 15, kq = lane >> 4;
-    for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < nwin; w += nw) {
-        const int64_t e = w * 64 + lane;
-        const uint2 be = e < tot ? bucket[e] : make_uint2(0u, 0xFFFFFFFFu);
-        uint64_t todo = __ballot(e < tot);
-        while (todo) {
-            // one half-block segment (the bucket is grouped by half-block)
-            const int s0 = __ffsll((long long)todo) - 1;
-            const uint32_t hb = (uint32_t)__shfl((int)be.y, s0, WAVE);
-            const uint64_t seg = __ballot(be.y == hb) & todo;
-            todo &= ~seg;
-            const int nseg = __popcll(seg);
-            // A: item (lane & 15) of the half-block, dims 32 ks + 8 kq + [0, 8)
-            f16x8 afr[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const int d0 = 32 * ks + 8 * kq;
-                if (d0 < DP)
-                    afr[ks] = __builtin_bit_cast(
-                        f16x8, *reinterpret_cast<const uint4*>(hbc + ((size_t)hb * 16 + col) * (2 * DP) + 2 * d0));
-                else
-                    afr[ks] = f16x8{};
-            }
-            // the lane's 4 items: rows 4 kq + i of the half-block
-            int32_t irow[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                irow[i] = (int32_t)((int64_t)(hb >> 1) * 32 + i + 8 * kq + 4 * (hb & 1));
-            for (int g0 = 0; g0 < nseg; g0 += 16) {
-                const int m = g0 + col;  // this lane's user: the segment's m-th entry
-                const bool vu = m < nseg;
-                const int src = vu ? s0 + m : s0;
-                const uint32_t u = (uint32_t)__shfl((int)be.x, src, WAVE);
-                const float* ur = users + (size_t)u * DP;
-                const float4 inf = uinfo[u];
-                const float2 cu = ucut[u];
-                const float su = inf.z * inv_cs;  // the screen's user scale (exact)
-                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    const int d0 = 32 * ks + 8 * kq;
-                    f16x8 bfr = f16x8{};
-                    if (d0 < DP) {
-                        const float4 x0 = *reinterpret_cast<const float4*>(ur + d0);
-                        const float4 x1 = *reinterpret_cast<const float4*>(ur + d0 + 4);
-                        bfr[0] = (_Float16)(x0.x * su); bfr[1] = (_Float16)(x0.y * su);
-                        bfr[2] = (_Float16)(x0.z * su); bfr[3] = (_Float16)(x0.w * su);
-                        bfr[4] = (_Float16)(x1.x * su); bfr[5] = (_Float16)(x1.y * su);
-                        bfr[6] = (_Float16)(x1.z * su); bfr[7] = (_Float16)(x1.w * su);
-                    }
-                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(afr[ks], bfr, acc, 0, 0, 0);
-                }
-                const float pcut = cu.x * inf.z;  // the cut in the screen's scaled units (exact)
-                double thr = -INFINITY;
-                if (cu.x != -INFINITY) {
-                    thr = (double)cu.x + (double)cu.y;
-                    thr = thr - fabs(thr) * 1e-15 - 1e-300;  // round down (ip_refine_kernel's cut + eps)
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (vu && irow[i] < n_items && acc[i] >= pcut) {
-                        const double sd = exact_dot(ur, items + (int64_t)irow[i] * DP, DP);
-                        if (sd >= thr) {
-                            const int p = atomicAdd(&scnt[u], 1);
-                            if (p < svb) surv[(size_t)u * svb + p] = Surv{sd, irow[i], 0};
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-// per user (persistent waves): sort the survivors, write the top k
-template <int SE>
-__global__ __launch_bounds__(256) void ip_hb_final_kernel(
-    const float* __restrict__ users, int64_t n_users, int64_t n_items, int dim, int k, int64_t row_offset,
-    const int32_t* __restrict__ ovf_flag, const int32_t* __restrict__ scnt, const Surv* __restrict__ surv,
-    int32_t* __restrict__ ovf_list, int32_t* __restrict__ ovf_count, float* __restrict__ out_s,
-    int32_t* __restrict__ out_r, double* __restrict__ out_e) {
-    constexpr int SV = SE * WAVE;
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    for (int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < n_users; u += nw) {
-        const int ov = ovf_flag[u];
-        const int cnt = scnt[u];
-        const float* uv = users + u * dim;
-        const float ul = lane < dim ? uv[lane] : 0.0f;
-        if (ov) continue;  // in ovf_list already: the exact path
-        float nz = fabsf(ul);
-        for (int d = lane + WAVE; d < dim; d += WAVE) nz += fabsf(uv[d]);
-        nz = wave_sum_f32(nz);
-        if (nz == 0.0f) {  // zero user: every score is exactly 0 -> the lowest rows
-            for (int i = lane; i < k; i += WAVE) {
-                const bool ok = i < n_items;
-                out_s[u * k + i] = ok ? 0.0f : -FLT_MAX;
-                out_r[u * k + i] = ok ? (int32_t)(i + row_offset) : -1;
-                if (out_e) out_e[u * k + i] = ok ? 0.0 : -INFINITY;
-            }
-            continue;
-        }
-        if (cnt > SV) {  // dense exact ties: the exact fallback
-            if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
-            continue;
-        }
-        Cand x[SE];
-#pragma unroll
-        for (int e = 0; e < SE; ++e) {
-            const int idx = e * 64 + lane;
-            if (idx < cnt) {
-                const Surv sv = surv[(size_t)u * SV + idx];
-                x[e].s = sv.s;
-                x[e].row = sv.row;
-            } else {
-                x[e].s = -INFINITY;
-                x[e].row = INT32_MAX;
-            }
-        }
-        wave_bitonic_sort<SE>(x);
-#pragma unroll
-        for (int e = 0; e < SE; ++e) {
-            const int idx = e * 64 + lane;
-            if (idx < k) {
-                const bool ok = x[e].row != INT32_MAX;
-                out_s[u * k + idx] = ok ? (float)x[e].s : -FLT_MAX;
-                out_r[u * k + idx] = ok ? (int32_t)(x[e].row + row_offset) : -1;
-                if (out_e) out_e[u * k + idx] = ok ? x[e].s : -INFINITY;
-            }
-        }
-    }
 }
 
 // -------------------------------------------------------------- fallback --
@@ -3254,24 +2578,6 @@ struct IpWs {
     int blk_lo, blk_hi;  // block range screened (config-4 shards), set by the caller
     float* bnd = nullptr;  // config-4 shard: the scan's per-user bounds (ip_scan_kernel's bnd)
     int bnd_m = 0;
-    // refine by half-block (screen path, k <= IP_KFAST): bucket counts /
-    // offsets per half-block, each band slot's place in its bucket, the
-    // buckets, and per user the survivor count and list (svb slots)
-    int32_t* hb_cnt = nullptr;
-    int32_t* hb_off = nullptr;
-    int32_t* hb_li = nullptr;
-    uint2* hb_bucket = nullptr;
-    int32_t* scnt = nullptr;
-    Surv* surv = nullptr;
-    int64_t n_hb = 0;
-    int svb = 0;
-    // FLAT scan (ip_scan_kernel): the tail parts' counts and list bounds;
-    // flat_ok = the caller's select reads them (the one-GPU screen), flat_used
-    // = the scan launch split blocks (set by launch_scan_v)
-    int32_t* acnt1 = nullptr;
-    float* lb1 = nullptr;
-    bool flat_ok = false;
-    mutable bool flat_used = false;
     size_t bytes;
 };
 
@@ -3328,10 +2634,6 @@ static IpWs ip_ws_layout(void* base, int64_t n_users, int64_t n_items, int k, in
     off += align256((size_t)n_users * sizeof(float4));
     w.acnt = reinterpret_cast<int32_t*>(p + off);
     off += align256((size_t)n_users * 2 * sizeof(int32_t));
-    w.acnt1 = reinterpret_cast<int32_t*>(p + off);
-    off += align256((size_t)n_users * 2 * sizeof(int32_t));
-    w.lb1 = reinterpret_cast<float*>(p + off);
-    off += align256((size_t)n_users * sizeof(float));
     w.cand = reinterpret_cast<uint2*>(p + off);
     off += align256((size_t)n_users * w.bandcap * sizeof(uint2));
     w.app = reinterpret_cast<uint2*>(p + off);
@@ -3340,22 +2642,6 @@ static IpWs ip_ws_layout(void* base, int64_t n_users, int64_t n_items, int k, in
     off += align256((size_t)std::min<int64_t>(n_users, FB_GRID) * (size_t)n_items * sizeof(uint32_t));
     w.slow_list = reinterpret_cast<int32_t*>(p + off);
     off += align256((size_t)n_users * sizeof(int32_t));
-    if (k <= IP_KFAST && (dim == 16 || dim == 32 || dim == 64)) {  // nrk_ip_topk_finish's by_hb dims
-        w.n_hb = 2 * n_blocks_of(n_items);
-        w.svb = k <= 64 ? 128 : 256;  // ip_refine_kernel's SV
-        w.hb_cnt = reinterpret_cast<int32_t*>(p + off);
-        off += align256((size_t)(w.n_hb + 1) * sizeof(int32_t));
-        w.hb_off = reinterpret_cast<int32_t*>(p + off);
-        off += align256((size_t)(w.n_hb + 1) * sizeof(int32_t));
-        w.hb_li = reinterpret_cast<int32_t*>(p + off);
-        off += align256((size_t)n_users * w.bandcap * sizeof(int32_t));
-        w.hb_bucket = reinterpret_cast<uint2*>(p + off);
-        off += align256((size_t)n_users * w.bandcap * sizeof(uint2));
-        w.scnt = reinterpret_cast<int32_t*>(p + off);
-        off += align256((size_t)n_users * sizeof(int32_t));
-        w.surv = reinterpret_cast<Surv*>(p + off);
-        off += align256((size_t)n_users * w.svb * sizeof(Surv));
-    }
     w.bytes = off;
     return w;
 }
@@ -3381,11 +2667,8 @@ static int n_cus() {
 // ring slots of the UG = 4 scan (config 2): 4 (one more tile in flight
 // than round 3's 3) since the bookkeeping got cheaper -- bench context, one
 // box, three pairs: scan 5.77 vs 5.80-5.86 ms
-#ifndef NRK_SCAN_NSL4
-#define NRK_SCAN_NSL4 4
-#endif
-constexpr int SCAN_NSL4 = NRK_SCAN_NSL4;
-template <int DP, int NW, int NSL, int UG, int MT, int WPE, bool FR, int IE = 1, bool TAPP = false>
+constexpr int SCAN_NSL4 = 4;
+template <int DP, int NW, int NSL, int UG, int MT, int WPE>
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
     const int per_wg = NW * 32 * UG;
@@ -3397,12 +2680,8 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
     // config 2, +17% on a config-4 shard, whose appends it cuts by 2/3)
     const int n = t_hi - t_lo;
     const int pre_div = w.bnd != nullptr ? SCAN_SHARD_PRE_DIV : SCAN_PRE_DIV;  // a catalog shard's own
-    const int n_pre = (IE == 1 && n >= SCAN_PRE_MIN) ? std::min(SCAN_PRE_MAX, n / pre_div) : 0;
+    const int n_pre = n >= SCAN_PRE_MIN ? std::min(SCAN_PRE_MAX, n / pre_div) : 0;
     const int pstride = n_pre > 0 ? n / n_pre : 1;
-    // FLAT: every workgroup slot of the chip busy (see ip_scan_kernel)
-    constexpr int WG_CU = (WPE * 4) / NW > 0 ? (WPE * 4) / NW : 1;
-    const int slots = n_cus() * WG_CU, nub = (int)grid;
-    w.flat_used = false;
     if constexpr (SCAN_WS && DP == 32 && MT == 16 && NW == 8 && UG == 4) {
         // the warp-specialized form of this variant (same users per workgroup)
         // a catalog shard (list bounds) inserts more often: its appended
@@ -3413,18 +2692,7 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
             w.bnd_m, insp);
         return;
     }
-    if (SCAN_FLAT && w.flat_ok && w.bnd == nullptr && nub < slots && n >= 64) {
-        const int E = slots - nub, c = (nub + E - 1) / E;
-        const int head = (int)(((int64_t)c * n + c) / (c + 1));  // ceil(c n / (c + 1))
-        if (head < n) {
-            ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP, true><<<2 * nub, NW * 64, 0, s>>>(
-                users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, 0, 1, nullptr, 0,
-                head, w.acnt1, w.lb1);
-            w.flat_used = true;
-            return;
-        }
-    }
-    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE, FR, IE, TAPP><<<grid, NW * 64, 0, s>>>(
+    ip_scan_kernel<DP, NW, NSL, UG, MT, WPE><<<grid, NW * 64, 0, s>>>(
         users, n_users, cat, n_items, dim, k, w.m2, w.app, w.acnt, w.uinfo, t_lo, t_hi, n_pre, pstride, w.bnd,
         w.bnd_m);
 }
@@ -3439,19 +2707,17 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
         // (UG = 4) per workgroup at 2 waves / SIMD -- every LDS fragment read
         // and tile barrier serves twice the MFMAs of the 64-user waves
         // (round 3): config-2 screen 6.8-7.0 vs 7.0-7.2 ms
-        launch_scan_v<DP, 8, SCAN_NSL4, 4, MT, 2, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s);
+        launch_scan_v<DP, 8, SCAN_NSL4, 4, MT, 2>(users, n_users, cat, n_items, dim, k, w, s);
         return;
     }
     // 8 waves share a 3-slot ring, 2 workgroups (4 waves / SIMD) per CU; every
-    // tile inserts (IE = 1), appends per half-block max >= tau.  Config 2
-    // (tools/scan_ab.sh / ab2.sh, screen = scan + select): 7.1 ms with 343
-    // appended maxima per user; whole-tile appends (TAPP, variant 4) 7.4-7.5
-    // with 885 (the select reads 2.6x more); 4-wave workgroups 7.9-8.2, 4 / 6
-    // / 8 ring slots 7.3-7.4, alternating inserts (IE = 2) 8.1 (the lagging
-    // cut doubles the appends); a round-3 measurement build without any
-    // append / insert work ran 4.9-6.4 ms
+    // tile inserts, appends per half-block max >= tau.  Config 2 (round 3,
+    // screen = scan + select): 7.1 ms with 343 appended maxima per user;
+    // whole-tile appends 7.4-7.5 with 885 (the select reads 2.6x more);
+    // 4-wave workgroups 7.9-8.2, 4 / 6 / 8 ring slots 7.3-7.4, alternating
+    // inserts 8.1 (the lagging cut doubles the appends)
     constexpr int NW = (UG == 2) ? 8 : 4, NSL = (UG == 2) ? 3 : 4;
-    launch_scan_v<DP, NW, NSL, UG, MT, WPE, false, 1, false>(users, n_users, cat, n_items, dim, k, w, s);
+    launch_scan_v<DP, NW, NSL, UG, MT, WPE>(users, n_users, cat, n_items, dim, k, w, s);
 }
 
 template <int DP>
@@ -3487,17 +2753,8 @@ static int ip_range(IpWs& w, int64_t n_items, int dim, int64_t blk_lo, int64_t b
 
 // config-4 shard bounds from the scan's register lists (ip_scan_kernel's
 // epilogue) instead of a pass over the appended maxima (ip_shard_bound_kernel)
-#ifndef NRK_SHARD_LISTBOUND
-#define NRK_SHARD_LISTBOUND 1
-#endif
-constexpr bool SHARD_LISTBOUND = NRK_SHARD_LISTBOUND;
 // the scan's epilogue merges lists of up to 32 per lane (k <= 64)
-static inline bool shard_listbound(int k) { return SHARD_LISTBOUND && (k + 1) / 2 <= 32; }
-// the one-GPU finish by half-block buckets (ip_hb_*) instead of ip_refine_kernel
-#ifndef NRK_HB_REFINE
-#define NRK_HB_REFINE 0
-#endif
-constexpr bool HB_REFINE = NRK_HB_REFINE;
+static inline bool shard_listbound(int k) { return (k + 1) / 2 <= 32; }
 
 // persistent grid of the shard kernels: SH_WG_PER_CU 4-wave workgroups per CU
 static int sh_grid(int64_t n_users) {
@@ -3565,12 +2822,12 @@ int nrk_ip_catalog_build(const float* items, int64_t n_items, int dim, void* cat
     }
     const int64_t total = n_blocks_of(n_items) * (dp / 16) * 64;
     if (total > 0) {
-        const int g2 = (int)std::min<int64_t>((n_items + 255) / 256, 2048);
+        const int g2 = (int)std::min<int64_t>((n_items + 15) / 16, 2048);  // >= one row group per wave
         catalog_norm_kernel<<<g2, 256, 0, s>>>(items, n_items, dim, hdr);
     }
     catalog_hdr_kernel<<<1, 1, 0, s>>>(hdr, dim, dp);
     if (total > 0) {
-        const int g2 = (int)std::min<int64_t>((n_items + 255) / 256, 2048);
+        const int g2 = (int)std::min<int64_t>((n_items + 15) / 16, 2048);
         catalog_dnorm_kernel<<<g2, 256, 0, s>>>(items, n_items, dim, hdr);
         const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
         catalog_pack_kernel<<<grid, 256, 0, s>>>(items, n_items, dim, dp, hdr,
@@ -3622,15 +2879,7 @@ static int screen_phases(const float* users, int64_t n_users, const void* catalo
     hipStream_t s = as_stream(stream);
     const uint8_t* cat = reinterpret_cast<const uint8_t*>(catalog);
     if ((phases & 1) && n_items > 0 && k <= IP_KFAST) {
-        w.flat_ok = true;  // this select reads the tail parts' counts and bounds
         scan_dispatch(users, (int)n_users, cat, (int)n_items, dim, k, w, s);
-        if (SCAN_FLAT && !w.flat_used &&
-            (hipMemsetAsync(w.acnt1, 0, (size_t)n_users * 2 * sizeof(int32_t), s) != hipSuccess ||
-             hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.lb1), 0xFF800000u /* -inf */, (size_t)n_users, s) !=
-                 hipSuccess)) {
-            set_error("nrk_ip_topk_scan: hipMemsetAsync failed");
-            return NRK_EHIP;
-        }
     }
     if (phases & 2) {
         if (hipMemsetAsync(w.ovf_count, 0, 256, s) != hipSuccess) {
@@ -3646,15 +2895,9 @@ static int screen_phases(const float* users, int64_t n_users, const void* catalo
             const int grid = (int)std::min<int64_t>((n_users + 255) / 256, 4096);
             ip_all_exact_kernel<<<grid, 256, 0, s>>>(n_users, w.cnt, w.ovf_flag, w.ovf_list, w.ovf_count);
         } else {
-            // FLAT builds read the tail parts (zeros / -inf when the scan did not split)
-            if (SCAN_FLAT)
-                ip_select_kernel<true><<<sh_grid(n_users), 256, 0, s>>>(
-                    n_users, k, w.m2, w.bandcap, w.app, w.acnt, w.uinfo, w.cand, w.cnt, w.ucut, w.ovf_flag,
-                    w.ovf_list, w.ovf_count, w.acnt1, w.lb1);
-            else
-                ip_select_kernel<false><<<sh_grid(n_users), 256, 0, s>>>(
-                    n_users, k, w.m2, w.bandcap, w.app, w.acnt, w.uinfo, w.cand, w.cnt, w.ucut, w.ovf_flag,
-                    w.ovf_list, w.ovf_count, nullptr, nullptr);
+            ip_select_kernel<<<sh_grid(n_users), 256, 0, s>>>(n_users, k, w.m2, w.bandcap, w.app, w.acnt, w.uinfo,
+                                                              w.cand, w.cnt, w.ucut, w.ovf_flag, w.ovf_list,
+                                                              w.ovf_count);
         }
     }
     NRK_CHECK_LAUNCH();
@@ -3705,34 +2948,7 @@ int nrk_ip_topk_finish(const float* users, int64_t n_users, const float* items,
         if (k <= 64) NRK_REFINE(DS4, 128);          \
         else NRK_REFINE(DS4, 256);                  \
     } while (0)
-    const bool by_hb = HB_REFINE && k <= IP_KFAST && n_items > 0 && catalog != nullptr &&
-                       (dim == 16 || dim == 32 || dim == 64);
-    if (by_hb) {
-        if (hipMemsetAsync(w.hb_cnt, 0, (size_t)(w.n_hb + 1) * sizeof(int32_t), s) != hipSuccess ||
-            hipMemsetAsync(w.scnt, 0, (size_t)n_users * sizeof(int32_t), s) != hipSuccess) {
-            set_error("nrk_ip_topk_finish: hipMemsetAsync failed");
-            return NRK_EHIP;
-        }
-        const int gs = (int)std::min<int64_t>((n_users + 255) / 256, 16384);
-        ip_hb_count_kernel<<<gs, 256, 0, s>>>(n_users, w.bandcap, w.cand, w.cnt, w.hb_cnt, w.hb_li);
-        ip_hb_scan_kernel<<<1, 1024, 0, s>>>(w.hb_cnt, w.n_hb, w.hb_off);
-        ip_hb_scatter_kernel<<<gs, 256, 0, s>>>(n_users, w.bandcap, w.cand, w.cnt, w.hb_off, w.hb_li, w.hb_bucket);
-        const int gsc = sh_grid(n_users * 8);  // persistent 4-wave workgroups over the 64-entry windows
-#define NRK_HB_SCORE(DP)                                                                                      \
-    ip_hb_score_kernel<DP><<<gsc, 256, 0, s>>>(users, items, cat, n_items, w.hb_bucket, w.hb_off + w.n_hb, w.ucut, \
-                                               w.uinfo, w.scnt, w.surv, w.svb)
-        if (dim == 32) NRK_HB_SCORE(32);
-        else if (dim == 16) NRK_HB_SCORE(16);
-        else NRK_HB_SCORE(64);
-#undef NRK_HB_SCORE
-        const int gf = sh_grid(n_users);
-        if (w.svb == 128)
-            ip_hb_final_kernel<2><<<gf, 256, 0, s>>>(users, n_users, n_items, dim, k, row_offset, w.ovf_flag, w.scnt,
-                                                    w.surv, w.ovf_list, w.ovf_count, out_scores, out_rows, out_exact);
-        else
-            ip_hb_final_kernel<4><<<gf, 256, 0, s>>>(users, n_users, n_items, dim, k, row_offset, w.ovf_flag, w.scnt,
-                                                    w.surv, w.ovf_list, w.ovf_count, out_scores, out_rows, out_exact);
-    } else if (k <= IP_KFAST || n_items == 0) {
+    if (k <= IP_KFAST || n_items == 0) {
         if (dim == 32) NRK_REFINE_SV(8);
         else if (dim == 16) NRK_REFINE_SV(4);
         else if (dim == 64) NRK_REFINE_SV(16);

@@ -16,11 +16,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
     const int32_t* __restrict__ hist_len, int64_t n, int T, const float* __restrict__ w0,
     const float* __restrict__ b0, int h0, const float* __restrict__ w1,
     const float* __restrict__ b1, int h1, float* __restrict__ out) {
-    // weight rows padded by one word: lane o reads row o, so an unpadded
-    // power-of-two row stride would put all 64 lanes on one LDS bank
+    // the 4-wide reads of sx / the weight rows below stay 16-B aligned and
+    // inside their own row only while 2D is a multiple of 4 (the host allows
+    // D = 16, 32, 64 only)
+    static_assert(D % 2 == 0 && D >= 16 && D <= 64 && (D & (D - 1)) == 0, "tt_user_kernel: D in {16, 32, 64}");
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    // rows padded to a multiple of 4 floats + 4: 16-B aligned for the 4-wide
-    // reads below, and lane o's row starts 4 banks after lane o - 1's
+    // weight rows padded to a multiple of 4 floats + 4: lane o reads row o, so
+    // an unpadded power-of-two row stride would put all 64 lanes on one LDS
+    // bank; with the padding the rows are 16-B aligned for the 4-wide reads
+    // and lane o's row starts 4 banks after lane o - 1's
     const int S0 = 2 * D + 4, h0p = (h0 + 3) & ~3, S1 = h0p + 4, h1p = (h1 + 3) & ~3;
     float* sw0 = lds;               // [h0][S0]
     float* sb0 = sw0 + h0 * S0;     // [h0] (h0p)

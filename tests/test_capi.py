@@ -105,10 +105,9 @@ def test_argument_errors_raise_valueerror():
     assert rc == _lib.NRK_EINVAL and b"2 GiB" in L.nrk_last_error()
     rc = L.nrk_ip_topk(None, 10, None, None, 20_000_000, 256, 129, 0, None, None, None, None, 0, None)
     assert rc == _lib.NRK_EINVAL and b"null pointer" in L.nrk_last_error()
-    # the append lists (3.6 GB) and the by-half-block refine's buckets and survivor lists (0.8 GB) live
-    # in the workspace: bounded at config 2 (250k users), none of them on the exact path
+    # the append lists (3.6 GB) live in the workspace: bounded at config 2 (250k users), none on the exact path
     ws31 = L.nrk_ip_topk_workspace_bytes(250000, 364047, 32, 31)
-    assert 0 < ws31 < 5 << 30
+    assert 0 < ws31 < 4 << 30
     assert L.nrk_ip_topk_workspace_bytes(1000, 364047, 32, 129) < L.nrk_ip_topk_workspace_bytes(1000, 364047, 32, 101)
 
 

@@ -462,25 +462,29 @@ def test_catalog_shards_bound_full_size(ops):
     assert np.array_equal(s[sample].cpu().numpy(), so)
 
 
-@pytest.mark.parametrize("n_shards,k", [(2, 31), (3, 31), (8, 31), (8, 61), (4, 10)])
-def test_catalog_owner_refine_equals_single(ops, n_shards, k):
+@pytest.mark.parametrize("n_shards,k,d", [(2, 31, 32), (3, 31, 32), (8, 31, 32), (8, 61, 32), (4, 10, 32),
+                                          (3, 31, 16), (4, 21, 64), (3, 100, 32), (2, 31, 128)])
+def test_catalog_owner_refine_equals_single(ops, n_shards, k, d):
     """Config 4, owner refine (nrk.dist.owner_replay: the two exchanges
     in-process): every rank screens its tile range of the shared catalog,
     bands above the global bound go to each user block's owner, which
     refines its users -- rows and scores identical to one GPU, incl. a
-    cross-shard exact tie, a zero user and the tie-stress overflow path."""
+    cross-shard exact tie, a zero user and the tie-stress overflow path.
+    d = 32 with k <= 31 is the warp-specialized shard scan; the other dims
+    run ip_scan_kernel's variants, k = 100 the shard bound pass
+    (ip_shard_bound_kernel) instead of the scan's list epilogue."""
     from nrk.dist import HipRangeShard, owner_replay, shard_blocks
 
-    rng = np.random.default_rng(n_shards * 100 + k)
-    users = _unit(rng.standard_normal((300, 32)))
+    rng = np.random.default_rng(n_shards * 100 + k + d)
+    users = _unit(rng.standard_normal((300, d)))
     users[7] = 0.0
-    items = _unit(rng.standard_normal((20000, 32)))
+    items = _unit(rng.standard_normal((20000, d)))
     items[19990] = items[10]
     items[5000:5600] = items[100]  # dense exact duplicates -> overflowed users take the exact path
     users[9] = items[100]
     so, ro = oracle.ip_topk(users, items, k)
     cat = ops.Catalog(_dev(items))
-    tb = ops.ip_topk_tile_blocks(32)
+    tb = ops.ip_topk_tile_blocks(d)
     shards = [HipRangeShard(cat, *shard_blocks(len(items), n_shards, r, tb), k, len(users)) for r in range(n_shards)]
     s, r, e = owner_replay(_dev(users), shards, k)
     assert np.array_equal(r.cpu().numpy(), ro)
