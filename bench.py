@@ -12,15 +12,19 @@ value = recalled user-item pairs / s = users x 30 / step time (rank 0 of the
 31 is dropped by recall(), youtubednn_recaller.py:524).
 
 With --gpus N > 1 (torch.distributed.run, one process per GPU, RCCL) the
-layouts are BASELINE's (layout_plan):
-  * recall = config 4 (default --shard catalog): the same 250k users, the
-    catalog's 32-item blocks split N-way in whole screen tiles; each rank
-    runs the user tower for its user block (all_gather -> every user),
-    screens its item range for every user, the ranks exchange the shard
-    bounds (all_gather) and the band candidates (all_to_all to the user's
-    owner), and each rank refines its own user block exactly (strong
-    scaling: value = 250k x 30 / the slowest rank's step).  --shard users
-    runs N independent 250k-user problems instead (weak scaling).
+layouts are (layout_plan):
+  * recall, headline value (default --shard users): the users are
+    independent units, so every rank runs its own 250k-user problem against
+    the whole (replicated, 70 MB) catalog with no data-path collective --
+    weak scaling, value = N x 250k x 30 / the slowest rank's step.
+  * recall, "config4" beside it (BASELINE config 4; --shard catalog makes it
+    the headline): the same 250k users, the catalog's 32-item blocks split
+    N-way in whole screen tiles; each rank runs the user tower for its user
+    block (all_gather -> every user), screens its item range for every user,
+    the ranks exchange the shard bounds (all_gather) and the band candidates
+    (all_to_all to the user's owner), and each rank refines its own user
+    block exactly (strong scaling: value = 250k x 30 / the slowest rank's
+    step).
   * DIN = config 3: the 165 Dice batches of 4096 (last 3,909) split
     round-robin, batch b on rank b mod N (value = 675,653 / the slowest
     rank's pass).
@@ -752,30 +756,37 @@ def launch_ranks(n, argv):
 def layout_plan(args, world):
     """Per-rank work of the N-rank run (the dry run prints it, the workload
     follows it):
-      recall: "catalog" (BASELINE config 4, default at N > 1): rank r screens
-              the 32-item blocks shard_blocks(I, N, r, tile) (whole screen
-              tiles) for every user, runs the tower for and refines the user
-              block shard_range(U, N, r); "users": every rank its own U users
+      recall: "catalog" (BASELINE config 4, default at N > 1): the ranks
+              form an R x C grid (nrk.dist.layout_2d: R = 2 user groups at
+              N = 8, else 1); rank r = g C + c screens the 32-item blocks
+              shard_blocks(I, C, c, tile) (whole screen tiles) for group g's
+              users, runs the tower for and refines its 1 / C of them
+              (nrk.dist.grid_ranges); "users": every rank its own U users
               against the whole catalog; N = 1: "single".
       din:    the Dice batches of 4096 round-robin (din_batches)."""
-    from nrk.dist import shard_blocks, shard_range
+    from nrk.dist import grid_ranges, layout_2d
     from nrk.ops import ip_topk_tile_blocks
 
     U, I, D = args.users, args.items, args.dim
     layout = "single" if world == 1 else args.shard
     tb = ip_topk_tile_blocks(D)
+    owner = getattr(args, "topk", 30) + 1 <= 128
+    # the R x C grid of the owner protocol (the merge protocol: one row)
+    R, C = layout_2d(world, getattr(args, "user_groups", None) or (None if owner else 1)) if layout == "catalog" \
+        else (1, world)
     per = []
     for r in range(world):
         if layout == "catalog":
-            blo, bhi = shard_blocks(I, world, r, tb)
+            (glo, ghi), (ulo, uhi), (blo, bhi) = grid_ranges(U, I, world, R, r, tb)
             per.append({"rank": r, "blocks": [blo, bhi], "items": [min(I, 32 * blo), min(I, 32 * bhi)],
-                        "users": list(shard_range(U, world, r))})
+                        "users": [ulo, uhi], "group_users": [glo, ghi]})
         else:
             per.append({"rank": r, "blocks": [0, -(-I // 32)], "items": [0, I], "users": [0, U]})
-    rec = {"layout": layout, "tile_blocks": tb, "per_rank": per,
+    grid = f"{R} user groups x {C} catalog shards" if R > 1 else f"{C} catalog shards"
+    rec = {"layout": layout, "tile_blocks": tb, "per_rank": per, "user_groups": R,
            "parallelism": {"single": "single",
-                           "catalog": (f"catalog-sharded x{world} (BASELINE config 4: shard screen, bound "
-                                       f"all_gather, band all_to_all, owner refine)" if getattr(args, "topk", 30) + 1 <= 128 else
+                           "catalog": (f"catalog-sharded x{world} as {grid} (BASELINE config 4: shard screen, bound "
+                                       f"all_gather, band all_to_all, owner refine)" if owner else
                                        f"catalog-sharded x{world} (BASELINE config 4, k + 1 > 128: per-shard exact "
                                        f"top-k, all_to_all to the owner, merge)"),
                            "users": f"users-sharded x{world} (independent replicas)"}[layout]}
@@ -808,8 +819,8 @@ def dry_run(args, world, rank, local):
         dist.all_reduce(mine)
     tot = [int(x) for x in mine]
     assert tot[0] == world, (tot, world)
-    if plan["recall"]["layout"] == "catalog":
-        assert tot[1] == -(-args.items // 32) and tot[2] == args.users, tot
+    if plan["recall"]["layout"] == "catalog":  # every block once per user group
+        assert tot[1] == plan["recall"]["user_groups"] * -(-args.items // 32) and tot[2] == args.users, tot
     assert tot[3] == args.din_samples and tot[4] == plan["din"]["batches"], tot
     log(f"[rank {rank}/{world}] local_rank {local} pid {os.getpid()} backend {args.backend or 'gloo'} (dry run) "
         f"blocks {rec['blocks']} users {rec['users']} din batches {din['batches']} samples {din['samples']}")
@@ -850,10 +861,16 @@ def main(argv=None):
                          "rank side 359 / 366 / 372 ms per 1.25M-user step at 131072 / 65536 / 32768)")
     ap.add_argument("--fused-hash-ctx", action="store_true",
                     help="config 5 with the synthetic hash-bin context instead of the real context features")
-    ap.add_argument("--shard", choices=["users", "catalog"], default="catalog",
-                    help="N>1 recall layout: catalog-sharded (BASELINE config 4, the default: shard "
-                         "screens, bound all_gather, band all_to_all, owner refine; strong scaling) or "
-                         "users-sharded (N independent 250k-user problems, weak scaling)")
+    ap.add_argument("--shard", choices=["users", "catalog"], default="users",
+                    help="N>1 recall layout of the headline value: users-sharded (the default: every "
+                         "rank its own 250k-user problem against the whole catalog, no data-path "
+                         "collective, weak scaling) or catalog-sharded (BASELINE config 4: shard screens, "
+                         "bound all_gather, band all_to_all, owner refine; strong scaling)")
+    ap.add_argument("--no-config4", action="store_true",
+                    help="N>1, --shard users: skip the BASELINE config-4 measurement (catalog-sharded, "
+                         "strong scaling) reported beside the headline as \"config4\"")
+    ap.add_argument("--user-groups", type=int, default=None,
+                    help="config 4: R user groups x N/R catalog shards (nrk.dist.layout_2d; default 1)")
     ap.add_argument("--din-samples", type=int, default=DIN_SAMPLES)
     ap.add_argument("--din-steps", type=int, default=10)
     ap.add_argument("--din-warmup", type=int, default=2)
@@ -900,137 +917,175 @@ def main(argv=None):
             dist.destroy_process_group()
         return
 
-    U, I, D, K = args.users, args.items, args.dim, args.topk + 1
-    plan = layout_plan(args, world)
-    catalog_mode = plan["recall"]["layout"] == "catalog"
-    t0 = time.time()
-    # users-sharded: every rank its own users (seed 23 + rank); catalog-sharded:
-    # one shared workload, rank r screens item blocks [blk_lo, blk_hi)
-    wl = recall_workload(23 if catalog_mode else 23 + rank, U, I, D, device)
-    item_vec = ops.tt_item_fwd(wl["item_table"], torch.arange(I, dtype=torch.int32, device=device))
-    cat = ops.Catalog(item_vec)
-    owner = K <= ops.IP_KFAST  # the owner protocol's shard screen; larger k: the merge protocol
-    if catalog_mode:
-        from nrk.dist import HipRangeShard, HipShard, catalog_sharded_owner, catalog_sharded_topk, gather_users
-
-        me = plan["recall"]["per_rank"][rank]
-        (blo, bhi), (ulo, uhi) = me["blocks"], me["users"]
-        if owner:
-            shard = HipRangeShard(cat, blo, bhi, K, U)
-        else:
-            i0, i1 = me["items"]
-            shard = HipShard(ops.Catalog(item_vec[i0:i1].contiguous()), i0, K, U)
-    else:
-        ws = ops.ip_topk_workspace(U, cat, K, device)
-        out_s = torch.empty((U, K), dtype=torch.float32, device=device)
-        out_r = torch.empty((U, K), dtype=torch.int32, device=device)
-    torch.cuda.synchronize()
-    log(f"[rank {rank}] setup {time.time() - t0:.1f}s: U={U} I={I} D={D} K={K} clicks={wl['n_clicks']}")
-
-    def step_catalog(ev=None):
-        # tower for this rank's user block, all_gather -> every user on every
-        # rank; screen this rank's item blocks for every user, all_gather the
-        # shard bounds, band pack + all_to_all to each user's owner, exact
-        # refine of the own user block (nrk.dist.catalog_sharded_owner)
-        if ev is not None:
-            ev[0].record()
-        u_loc = ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"][ulo:uhi], wl["hist"][ulo:uhi],
-                                wl["hist_len"][ulo:uhi], wl["w0"], wl["b0"], wl["w1"], wl["b1"], validate=False)
-        u = gather_users(u_loc, U)
-        if ev is not None:
-            ev[1].record()
-        mark = None if ev is None else (lambda ph: ev[2 if ph == "screen" else 3].record())
-        if owner:
-            res = catalog_sharded_owner(u, shard, K, mark=mark)
-        else:
-            res = catalog_sharded_topk(u, shard, K)
-            if mark is not None:
-                mark("screen")
-                mark("exchange")
-        if ev is not None:
-            ev[4].record()
-        return res
-
-    def step(ev=None):
+    def run_recall(shard_mode):
+        """One recall measurement: BASELINE config 2 at N = 1, at N > 1 the
+        layout ``shard_mode`` ("users": weak-scaled replicas, "catalog":
+        config 4).  Returns the step function, outputs and the line fields."""
+        rargs = argparse.Namespace(**vars(args))
+        rargs.shard = shard_mode
+        U, I, D, K = args.users, args.items, args.dim, args.topk + 1
+        plan = layout_plan(rargs, world)
+        catalog_mode = plan["recall"]["layout"] == "catalog"
+        t0 = time.time()
+        # users-sharded: every rank its own users (seed 23 + rank); catalog-sharded:
+        # one shared workload, rank r screens item blocks [blk_lo, blk_hi)
+        wl = recall_workload(23 if catalog_mode else 23 + rank, U, I, D, device)
+        item_vec = ops.tt_item_fwd(wl["item_table"], torch.arange(I, dtype=torch.int32, device=device))
+        cat = ops.Catalog(item_vec)
+        owner = K <= ops.IP_KFAST  # the owner protocol's shard screen; larger k: the merge protocol
         if catalog_mode:
-            return step_catalog(ev)
-        if ev is not None:
-            ev[0].record()
-        u = ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"], wl["hist"],
-                            wl["hist_len"], wl["w0"], wl["b0"], wl["w1"], wl["b1"], validate=False)
-        if ev is not None:
-            ev[1].record()
-        # the screen as its two launches, so the roofline times the MFMA scan alone
-        ops.ip_topk_scan(u, cat, K, ws)
-        if ev is not None:
-            ev[5].record()
-        ops.ip_topk_select(u, cat, K, ws)
-        if ev is not None:
-            ev[2].record()
-        ops.ip_topk_finish(u, cat, K, ws, out_s, out_r)
-        if ev is not None:
-            ev[3].record()
-            ev[4].record()
-        return u
+            from nrk.dist import HipRangeShard, HipShard, catalog_sharded_owner, catalog_sharded_topk, gather_users
+            from nrk.dist import grid_groups
 
-    # the tower's inputs are validated once here (hist_len in [0, T]: two
-    # device syncs); the timed steps run it with validate=False
-    ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"], wl["hist"], wl["hist_len"], wl["w0"],
-                    wl["b0"], wl["w1"], wl["b1"])
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if dist is not None:
-        elapsed = max_over_ranks(elapsed, device)
-    ms_step = elapsed / args.steps * 1e3
-    tower_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    screen_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    finish_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
-    refine_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
-    scan_ms = None if catalog_mode else float(np.mean([e[1].elapsed_time(e[5]) for e in evs]))
-    select_ms = None if catalog_mode else float(np.mean([e[5].elapsed_time(e[2]) for e in evs]))
-    pairs = U * args.topk * (1 if catalog_mode else world)
-    value = pairs / (elapsed / args.steps)
+            me = plan["recall"]["per_rank"][rank]
+            (blo, bhi), (ulo, uhi) = me["blocks"], me["users"]
+            glo, ghi = me["group_users"]  # this rank's user group (all users when R = 1)
+            grp, _, _ = grid_groups(world, plan["recall"]["user_groups"], rank)
+            if owner:
+                shard = HipRangeShard(cat, blo, bhi, K, ghi - glo)
+            else:
+                i0, i1 = me["items"]
+                shard = HipShard(ops.Catalog(item_vec[i0:i1].contiguous()), i0, K, U)
+        else:
+            ws = ops.ip_topk_workspace(U, cat, K, device)
+            out_s = torch.empty((U, K), dtype=torch.float32, device=device)
+            out_r = torch.empty((U, K), dtype=torch.int32, device=device)
+        torch.cuda.synchronize()
+        log(f"[rank {rank}] setup {time.time() - t0:.1f}s: U={U} I={I} D={D} K={K} clicks={wl['n_clicks']}")
 
-    # catalog mode: this rank's screen covers its own item blocks
-    n_scr = (min(I, bhi * 32) - blo * 32) if catalog_mode else cat.n
-    flops = 2.0 * U * n_scr * D
-    kernel_ms = screen_ms if catalog_mode else scan_ms
-    achieved = flops / (kernel_ms * 1e-3) / 1e12
-    default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and world == 1
-    # the config-2 scan runs the warp-specialized kernel (ip_scan_ws_kernel)
-    # unless built with -DNRK_SCAN_WS=0
-    traffic = pmc_traffic(["nrk::ip_scan_ws_kernel<"], default_cfg) or pmc_traffic(["nrk::ip_scan_kernel<"], default_cfg)
-    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                "traffic": round(traffic) if traffic else None,
-                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/" + PROFILE_ROUND + "_traffic.json; "
-                                "null when absent or measured on other kernel sources)",
-                "kernel": ("ip_scan_ws_kernel (warp-specialized fp16 MFMA 32x32x16 screen) + bound all_gather, "
-                           "this rank's item blocks" if catalog_mode else
-                           "ip_scan_ws_kernel (warp-specialized fp16 MFMA 32x32x16 screen), HIP events around its launch"),
-                "kernel_ms": round(kernel_ms, 4),
-                "algorithmic_flop_per_launch": flops,
-                # the same flops over the whole timed step (tower + scan + select + finish on
-                # one GPU; this rank's screen share over the slowest rank's step at N > 1):
-                # the roofline fraction ``value`` itself achieves
-                "step_frac": round(flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-                "busy": pmc_busy(["nrk::ip_scan_ws_kernel", "nrk::ip_select_kernel", "nrk::ip_refine_kernel",
-                                  "nrk::tt_user_kernel"], default_cfg),
-                "busy_source": "profiles/" + PROFILE_ROUND + "_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
-                               "SQ_WAIT_ANY, GRBM_GUI_ACTIVE passes; tools/pmc_busy.py, calibrated by "
-                               "tools/calib)"}
+        def step_catalog(ev=None):
+            # tower for this rank's user block, all_gather -> every user of the
+            # rank's user group on every rank of it; screen this rank's item
+            # blocks for those users, all_gather the shard bounds, band pack +
+            # all_to_all to each user's owner, exact refine of the own user block
+            # (nrk.dist.catalog_sharded_owner; all inside the group)
+            if ev is not None:
+                ev[0].record()
+            u_loc = ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"][ulo:uhi], wl["hist"][ulo:uhi],
+                                    wl["hist_len"][ulo:uhi], wl["w0"], wl["b0"], wl["w1"], wl["b1"], validate=False)
+            u = gather_users(u_loc, ghi - glo, group=grp)
+            if ev is not None:
+                ev[1].record()
+            mark = None if ev is None else (lambda ph: ev[2 if ph == "screen" else 3].record())
+            if owner:
+                res = catalog_sharded_owner(u, shard, K, group=grp, mark=mark)
+            else:
+                res = catalog_sharded_topk(u, shard, K)
+                if mark is not None:
+                    mark("screen")
+                    mark("exchange")
+            if ev is not None:
+                ev[4].record()
+            return res
+
+        def step(ev=None):
+            if catalog_mode:
+                return step_catalog(ev)
+            if ev is not None:
+                ev[0].record()
+            u = ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"], wl["hist"],
+                                wl["hist_len"], wl["w0"], wl["b0"], wl["w1"], wl["b1"], validate=False)
+            if ev is not None:
+                ev[1].record()
+            # the screen as its two launches, so the roofline times the MFMA scan alone
+            ops.ip_topk_scan(u, cat, K, ws)
+            if ev is not None:
+                ev[5].record()
+            ops.ip_topk_select(u, cat, K, ws)
+            if ev is not None:
+                ev[2].record()
+            ops.ip_topk_finish(u, cat, K, ws, out_s, out_r)
+            if ev is not None:
+                ev[3].record()
+                ev[4].record()
+            return u
+
+        # the tower's inputs are validated once here (hist_len in [0, T]: two
+        # device syncs); the timed steps run it with validate=False
+        ops.tt_user_fwd(wl["user_table"], wl["item_table"], wl["uid"], wl["hist"], wl["hist_len"], wl["w0"],
+                        wl["b0"], wl["w1"], wl["b1"])
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        for i in range(args.steps):
+            step(evs[i])
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
+        if dist is not None:
+            elapsed = max_over_ranks(elapsed, device)
+        ms_step = elapsed / args.steps * 1e3
+        tower_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+        screen_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+        finish_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+        refine_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
+        scan_ms = None if catalog_mode else float(np.mean([e[1].elapsed_time(e[5]) for e in evs]))
+        select_ms = None if catalog_mode else float(np.mean([e[5].elapsed_time(e[2]) for e in evs]))
+        pairs = U * args.topk * (1 if catalog_mode else world)
+        value = pairs / (elapsed / args.steps)
+
+        # catalog mode: this rank's screen covers its own item blocks
+        n_scr = (min(I, bhi * 32) - blo * 32) if catalog_mode else cat.n
+        flops = 2.0 * ((ghi - glo) if catalog_mode else U) * n_scr * D
+        kernel_ms = screen_ms if catalog_mode else scan_ms
+        achieved = flops / (kernel_ms * 1e-3) / 1e12
+        default_cfg = (U, I, D, args.topk) == (250_000, 364_047, 32, 30) and world == 1
+        # the config-2 scan runs the warp-specialized kernel (ip_scan_ws_kernel)
+        # unless built with -DNRK_SCAN_WS=0
+        traffic = pmc_traffic(["nrk::ip_scan_ws_kernel<"], default_cfg) or pmc_traffic(["nrk::ip_scan_kernel<"], default_cfg)
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                    "traffic": round(traffic) if traffic else None,
+                    "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/" + PROFILE_ROUND + "_traffic.json; "
+                                    "null when absent or measured on other kernel sources)",
+                    "kernel": ("ip_scan_ws_kernel (warp-specialized fp16 MFMA 32x32x16 screen) + bound all_gather, "
+                               "this rank's item blocks" if catalog_mode else
+                               "ip_scan_ws_kernel (warp-specialized fp16 MFMA 32x32x16 screen), HIP events around its launch"),
+                    "kernel_ms": round(kernel_ms, 4),
+                    "algorithmic_flop_per_launch": flops,
+                    # the same flops over the whole timed step (tower + scan + select + finish on
+                    # one GPU; this rank's screen share over the slowest rank's step at N > 1):
+                    # the roofline fraction ``value`` itself achieves
+                    "step_frac": round(flops / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                    "busy": pmc_busy(["nrk::ip_scan_ws_kernel", "nrk::ip_select_kernel", "nrk::ip_refine_kernel",
+                                      "nrk::tt_user_kernel"], default_cfg),
+                    "busy_source": "profiles/" + PROFILE_ROUND + "_busy.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, "
+                                   "SQ_WAIT_ANY, GRBM_GUI_ACTIVE passes; tools/pmc_busy.py, calibrated by "
+                                   "tools/calib)"}
+        return {"step": step, "plan": plan, "catalog": catalog_mode, "value": value, "ms_step": ms_step,
+                "tower_ms": tower_ms, "screen_ms": screen_ms, "finish_ms": finish_ms, "refine_ms": refine_ms,
+                "scan_ms": scan_ms, "select_ms": select_ms, "roofline": roofline,
+                "item_vec": item_vec, "out_r": None if catalog_mode else out_r, "U": U, "I": I, "D": D, "K": K}
+
+    U, I, D, K = args.users, args.items, args.dim, args.topk + 1
+    rec = run_recall("single" if world == 1 else args.shard)
+    step, plan, catalog_mode, value, ms_step = rec["step"], rec["plan"], rec["catalog"], rec["value"], rec["ms_step"]
+    tower_ms, screen_ms, finish_ms, refine_ms = rec["tower_ms"], rec["screen_ms"], rec["finish_ms"], rec["refine_ms"]
+    scan_ms, select_ms, roofline, item_vec, out_r = (rec["scan_ms"], rec["select_ms"], rec["roofline"],
+                                                      rec["item_vec"], rec["out_r"])
+    # N > 1 with the users-sharded headline: BASELINE config 4 (the catalog
+    # sharded over the same N ranks, strong scaling of one 250k-user problem,
+    # the two RCCL exchanges) measured beside it
+    config4 = None
+    if world > 1 and args.shard == "users" and not args.no_config4:
+        del rec
+        c4 = run_recall("catalog")
+        config4 = {"value": round(c4["value"], 1), "unit": "recalled pairs/s", "ms_per_step": round(c4["ms_step"], 4),
+                   "scaling": "strong", "workload": f"BASELINE config 4: the same {U} users x {I} items, D={D}, "
+                                                    f"catalog sharded {world}-way (one problem over all ranks)",
+                   "parallelism": c4["plan"]["recall"]["parallelism"],
+                   "phase_ms": {"tower_and_gather": round(c4["tower_ms"], 4),
+                                "screen_and_bound_exchange": round(c4["screen_ms"], 4),
+                                "band_pack_and_all_to_all": round(c4["finish_ms"], 4),
+                                "owner_refine": round(c4["refine_ms"], 4)},
+                   "roofline": c4["roofline"]}
+        del c4
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1088,7 +1143,9 @@ def main(argv=None):
                                     f"search), {U} users x {I} items, D={D}, catalog sharded {world}-way"
                                     if catalog_mode else
                                     "BASELINE config 2: YouTubeDNN recall (user tower + exact top-31 "
-                                    "IP search), 250k users x 364,047 items, D=32"),
+                                    "IP search), 250k users x 364,047 items, D=32"
+                                    + (f", one such problem per rank ({world} ranks, users-sharded)"
+                                       if world > 1 else "")),
                        "users": U, "items": I, "dim": D, "topk": args.topk,
                        "parallelism": plan["recall"]["parallelism"],
                        "din_parallelism": plan["din"]["parallelism"]},
@@ -1098,7 +1155,7 @@ def main(argv=None):
                          {"tower": round(tower_ms, 4), "screen": round(screen_ms, 4), "scan": round(scan_ms, 4),
                           "select": round(select_ms, 4), "finish": round(finish_ms, 4)}),
             "roofline": roofline, "cpu_baseline": cpu, "din": din, "itemcf": itemcf, "plugins": plugins,
-            "host": host_info(),
+            "config4": config4, "host": host_info(),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

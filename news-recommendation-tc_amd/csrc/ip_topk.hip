@@ -54,6 +54,15 @@ constexpr int IP_KMAX = 2048;   // largest k at all (exact path above IP_KFAST)
 #define NRK_SCAN_TILE 8192
 #endif
 constexpr int SCAN_TILE = NRK_SCAN_TILE;
+// dim 128 (BASELINE config 5): blocks per tile (a 32-item block is already
+// 8 KB there; dev A/B -DNRK_SCAN_TB128=2: 16-KB tiles, one barrier per two blocks)
+#ifndef NRK_SCAN_TB128
+#define NRK_SCAN_TB128 1
+#endif
+// 32-item blocks per screen tile (one LDS ring slot, one barrier) at padded dim dp
+__host__ __device__ constexpr int scan_tb(int dp) {
+    return dp == 128 ? NRK_SCAN_TB128 : (64 * dp >= SCAN_TILE ? 1 : SCAN_TILE / (64 * dp));
+}
 constexpr int IP_SEL = 512;     // appended maxima >= theta_lb held by the select
 constexpr int IP_BQ = 288;      // largest band (k = 128); the refine holds SV + 32 entries
 constexpr int IP_KRING = 256;   // prefilter-kept rows awaiting an exact round (ring, power of two)
@@ -444,7 +453,7 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     int tile_hi, int n_pre, int pstride, float* __restrict__ bnd, int bnd_m) {
     constexpr int DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
-    constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
+    constexpr int TB = scan_tb(DP);
     constexpr int TILE_BYTES = TB * BLOCK_BYTES;
     constexpr int LPT = TILE_BYTES / (NW * 1024);  // 1-KB LDS-DMA pieces per wave per tile
     static_assert(LPT >= 1 && LPT * NW * 1024 == TILE_BYTES, "tile split");
@@ -934,7 +943,7 @@ __global__ __launch_bounds__(64 * 4 * (1 + NB), NB == 1 ? 2 : 1) void ip_scan_ws
     int tile_hi, int n_pre, int pstride, float* __restrict__ bnd, int bnd_m, int insp) {
     constexpr int NPW = 4, UG = 8, UGB = UG / NB, DS = DP / 16;
     constexpr int BLOCK_BYTES = 64 * DP;
-    constexpr int TB = BLOCK_BYTES >= SCAN_TILE ? 1 : SCAN_TILE / BLOCK_BYTES;
+    constexpr int TB = scan_tb(DP);
     constexpr int TILE_BYTES = TB * BLOCK_BYTES;
     constexpr int NPC = TILE_BYTES / 1024;  // 1-KB pieces per tile: waves 0 .. NPC - 1 load one each
     static_assert(TB == 4 && DS == 2 && NPC == 8 && (NB == 1 || NB == 2), "WS scan: 8-KB tiles of four blocks at DP = 32");
@@ -2602,7 +2611,7 @@ static inline int ip_m2(int64_t n_items, int k, int dim) {
     m2 = std::min<int64_t>(m2, ((nblk + 63) / 64) * 64);
     if (mt <= 16) {
         const int dp = pad_dim(dim);
-        const int64_t tb = 64 * dp >= SCAN_TILE ? 1 : SCAN_TILE / (64 * dp);
+        const int64_t tb = scan_tb(dp);
         const int64_t ntile = (nblk + tb - 1) / tb;
         const double et = mt * (1.0 + log(std::max(1.0, (double)ntile / mt)));
         int64_t mt2 = ((tb * ((int64_t)(2.0 * et) + 16) + 63) / 64) * 64;
@@ -2672,7 +2681,7 @@ template <int DP, int NW, int NSL, int UG, int MT, int WPE>
 static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                           const IpWs& w, hipStream_t s) {
     const int per_wg = NW * 32 * UG;
-    constexpr int TB = 64 * DP >= SCAN_TILE ? 1 : SCAN_TILE / (64 * DP);
+    constexpr int TB = scan_tb(DP);
     const int nblk = (n_items + 31) / 32;
     const int t_lo = w.blk_lo / TB, t_hi = (std::min(w.blk_hi, nblk) + TB - 1) / TB;
     const unsigned grid = (unsigned)((n_users + per_wg - 1) / per_wg);
@@ -2742,7 +2751,7 @@ static void scan_dispatch(const float* users, int nu, const uint8_t* cat, int ni
 
 // a tile-aligned block range of a shard (config 4), checked
 static int ip_range(IpWs& w, int64_t n_items, int dim, int64_t blk_lo, int64_t blk_hi) {
-    const int tb = 64 * pad_dim(dim) >= SCAN_TILE ? 1 : SCAN_TILE / (64 * pad_dim(dim));
+    const int tb = scan_tb(pad_dim(dim));
     NRK_REQUIRE(blk_lo >= 0 && blk_lo <= blk_hi && blk_hi <= n_blocks_of(n_items), "block range out of bounds");
     NRK_REQUIRE(blk_lo == blk_hi || (blk_lo % tb == 0 && (blk_hi % tb == 0 || blk_hi == n_blocks_of(n_items))),
                 "block range must start (and end, unless at the catalog end) on a 8-KB tile");

@@ -9,6 +9,10 @@
 
 namespace nrk {
 
+#ifndef NRK_TT_CH
+#define NRK_TT_CH 16
+#endif
+
 template <int D>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void tt_user_kernel(
     const float* __restrict__ user_table, const float* __restrict__ item_table,
@@ -40,7 +44,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
     __syncthreads();  // the only block barrier: the user loop below is per wave
 
     constexpr int P = WAVE / D;  // history phases per lane group
-    constexpr int CH = 8;        // history rows in flight per lane
+    // history rows in flight per lane: every row of a config-2 user (T = 30,
+    // D = 32: 15 per lane) in one round trip (dev A/B: -DNRK_TT_CH=8)
+    constexpr int CH = NRK_TT_CH;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int d = lane % D, ph = lane / D;
     const int64_t wstride = (int64_t)gridDim.x * 4;

@@ -17,6 +17,9 @@ torch.distributed over RCCL ("nccl" on ROCm), 127.0.0.1 rendezvous.
   owner of each user block, which runs the exact refine of its users only
   from every shard's slots (nrk_ip_topk_refine_x): the refine shrinks 1/N
   with the screen and no merge is needed.  Same rows and scores as one GPU.
+  The ranks may form an R x C grid (layout_2d, bench --user-groups R): R user
+  groups, each running this protocol over C catalog shards inside its own
+  process group, so the per-user passes cover U / R users (default R = 1).
 * catalog-sharded, merge (catalog_sharded_topk) -- each shard holds its own
   rows and refines every user against them (k <= 128: after the bound
   exchange; larger k: the exact path, no exchange) and an all_to_all of the
@@ -317,6 +320,49 @@ def catalog_sharded_owner(users, shard, k: int, group=None, exchange_bound: bool
     lo, hi = shard_range(U, world, rank)
     ovf = (rc[:, :hi - lo] < 0).any(0).to(torch.int32)
     return shard.refine(users[lo:hi].contiguous(), rc, re, shard.ucut(lo, hi), ovf)
+
+
+def layout_2d(world: int, R: int | None = None):
+    """The config-4 rank grid: R user groups x C catalog shards, R C = world.
+    Rank r = g C + c screens group g's users (shard_range(U, R, g)) over
+    catalog shard c (shard_blocks(I, C, c, tile)) and refines its 1 / C of
+    group g's users; the two exchanges stay inside the group's C ranks.
+    Every per-user pass of a rank (the shard screen's list pre-pass share,
+    the bound and band passes) covers U / R users instead of U, and each shard's
+    tile range is R times longer, which shrinks the sampled pre-pass relative
+    to it.  Default R = 1: measured on the one-GPU replay (tools/catalog_replay.py,
+    DESIGN 4.6), 2 x 4 runs 1.67 ms per rank against 1.52 for 1 x 8 -- a
+    group's 125k users fill only 123 of the 256 CUs at the warp-specialized
+    scan's 1,024 users per workgroup -- and 4 x 2 overflows the band
+    exchange's 32 slots per user and shard (exact path)."""
+    if R is None:
+        R = 1
+    if R < 1 or world % R:
+        raise ValueError(f"{R} user groups do not divide {world} ranks")
+    return R, world // R
+
+
+def grid_groups(world: int, R: int, rank: int):
+    """The R process groups of layout_2d (every rank creates all of them, in
+    the same order, as torch.distributed requires); returns (this rank's
+    group, its group index g, its shard index c).  R = 1: the default group."""
+    C = world // R
+    if R == 1:
+        return None, 0, rank
+    groups = [dist.new_group(list(range(g * C, (g + 1) * C))) for g in range(R)]
+    return groups[rank // C], rank // C, rank % C
+
+
+def grid_ranges(n_users: int, n_items: int, world: int, R: int, rank: int, tile_blocks: int):
+    """Rank r's share in layout_2d: (group users [glo, ghi), own users
+    [lo, hi) (global rows: the users it runs the tower for and refines),
+    block range [blo, bhi) of its catalog shard)."""
+    C = world // R
+    g, c = rank // C, rank % C
+    glo, ghi = shard_range(n_users, R, g)
+    lo, hi = shard_range(ghi - glo, C, c)
+    blo, bhi = shard_blocks(n_items, C, c, tile_blocks)
+    return (glo, ghi), (glo + lo, glo + hi), (blo, bhi)
 
 
 def owner_replay(users, shards, k: int, timer=None):

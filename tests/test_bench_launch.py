@@ -42,10 +42,10 @@ def test_bench_launcher_propagates_rank_failure():
 
 
 def test_bench_layout_plan_config4_and_din_batches():
-    """--gpus N lays the work out as BASELINE's configs: recall catalog-sharded
-    (config 4, whole screen tiles, every item block and user once) and the
-    165 DIN Dice batches round-robin (batch b on rank b mod N)."""
-    p = _run(["--gpus", "3", "--dry-run", "--backend", "gloo"])
+    """--gpus N --shard catalog lays the work out as BASELINE's configs: recall
+    catalog-sharded (config 4, whole screen tiles, every item block and user
+    once) and the 165 DIN Dice batches round-robin (batch b on rank b mod N)."""
+    p = _run(["--gpus", "3", "--shard", "catalog", "--dry-run", "--backend", "gloo"])
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     plan = line["layout"]
@@ -64,6 +64,16 @@ def test_bench_layout_plan_config4_and_din_batches():
     assert line["covered"] == {"item_blocks": nblk, "users": 250_000, "din_samples": 675_653, "din_batches": 165}
 
 
+def test_bench_default_layout_is_users_sharded():
+    """The N > 1 headline is users-sharded (weak scaling, no data-path
+    collective); config 4 is measured beside it."""
+    p = _run(["--gpus", "2", "--dry-run", "--backend", "gloo"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    rec = line["layout"]["recall"]
+    assert rec["layout"] == "users" and all(r["users"] == [0, 250_000] for r in rec["per_rank"])
+
+
 def test_bench_layout_plan_users_and_single():
     from importlib import import_module
     import argparse
@@ -79,3 +89,32 @@ def test_bench_layout_plan_users_and_single():
     assert one["recall"]["parallelism"] == "single" and one["din"]["per_rank"][0]["samples"] == 675_653
     mine, rows = bench.din_batches(675_653, 4096, 8, 4)
     assert mine == list(range(4, 165, 8)) and rows[-1] == 675_652  # batch 164 = 4 mod 8: the short one, last
+
+
+def test_bench_layout_plan_grid():
+    """Config 4 as a rank grid: --gpus 4 --user-groups 2 (nrk.dist.layout_2d;
+    the default is one group) -- each user group's ranks split the
+    catalog in whole tiles, every user once, every item block once per group."""
+    p = _run(["--gpus", "4", "--shard", "catalog", "--user-groups", "2", "--dry-run", "--backend", "gloo"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    rec = line["layout"]["recall"]
+    assert rec["user_groups"] == 2 and "2 user groups x 2 catalog shards" in rec["parallelism"]
+    nblk = -(-364_047 // 32)
+    per = rec["per_rank"]
+    assert [r["group_users"] for r in per] == [[0, 125_000], [0, 125_000], [125_000, 250_000], [125_000, 250_000]]
+    assert [r["blocks"][0] for r in per] == [0, per[0]["blocks"][1], 0, per[2]["blocks"][1]]
+    assert per[1]["blocks"][1] == nblk and per[3]["blocks"][1] == nblk
+    users = [r["users"] for r in per]
+    assert users[0][0] == 0 and users[-1][1] == 250_000 and all(a[1] == b[0] for a, b in zip(users, users[1:]))
+    assert line["covered"]["item_blocks"] == 2 * nblk and line["covered"]["users"] == 250_000
+    from importlib import import_module
+    import argparse
+
+    sys.path[:0] = [REPO, os.path.join(REPO, "news-recommendation-tc_amd")]
+    bench = import_module("bench")
+    a = argparse.Namespace(users=250_000, items=364_047, dim=32, din_samples=675_653, shard="catalog", topk=30,
+                           user_groups=None)
+    assert bench.layout_plan(a, 8)["recall"]["user_groups"] == 1
+    a.user_groups = 2
+    assert bench.layout_plan(a, 8)["recall"]["user_groups"] == 2

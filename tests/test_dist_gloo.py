@@ -230,6 +230,75 @@ def test_catalog_sharded_owner_refine_matches_single(world, U, I, k, x_cap):
         assert np.array_equal(s, so[ulo:uhi]), rank
 
 
+def _grid_worker(rank, world, port, R, U, I, D, k, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nrk.dist import catalog_sharded_owner, grid_groups, grid_ranges, shard_range
+
+        rng = np.random.default_rng(11)
+        users = rng.standard_normal((U, D)).astype(np.float32)
+        items = rng.standard_normal((I, D)).astype(np.float32)
+        items[I // 2 + 1] = items[3]
+        grp, g, c = grid_groups(world, R, rank)
+        C = world // R
+        (glo, ghi), (ulo, uhi), _ = grid_ranges(U, I, world, R, rank, 1)
+        lo, hi = shard_range(I, C, c)  # the stand-in shards by rows
+        shard = _OwnerShard(items, lo, hi, k, force_ovf=1 if c == C - 1 else None)
+        s, r, e = catalog_sharded_owner(torch.from_numpy(users[glo:ghi]), shard, k, group=grp)
+        q.put((rank, ulo, uhi, s.numpy(), r.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,R,U,I,k", [(4, 2, 41, 300, 31), (6, 2, 50, 400, 8), (6, 3, 23, 90, 10)])
+def test_grid_owner_refine_matches_single(world, R, U, I, k):
+    """Config 4 as an R x C rank grid (nrk.dist.layout_2d / grid_groups):
+    each user group runs the owner protocol over its C catalog shards inside
+    its own process group (bound all_gather and band all_to_all among C
+    ranks); every rank's user block equals one GPU's rows and scores."""
+    from oracle import oracle
+
+    D = 16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, port, R, U, I, D, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(11)
+    users = rng.standard_normal((U, D)).astype(np.float32)
+    items = rng.standard_normal((I, D)).astype(np.float32)
+    items[I // 2 + 1] = items[3]
+    so, ro = oracle.ip_topk(users, items, k)
+    covered = np.zeros(U, np.int32)
+    for rank, ulo, uhi, s, r in got:
+        covered[ulo:uhi] += 1
+        assert np.array_equal(r, ro[ulo:uhi]), rank
+        assert np.array_equal(s, so[ulo:uhi]), rank
+    assert (covered == 1).all()
+
+
+def test_layout_2d():
+    from nrk.dist import grid_ranges, layout_2d
+
+    assert layout_2d(8) == (1, 8) and layout_2d(4) == (1, 4) and layout_2d(1) == (1, 1) and layout_2d(8, 2) == (2, 4)
+    with pytest.raises(ValueError):
+        layout_2d(6, 4)
+    U, I, tb = 250_000, 364_047, 4
+    seen_u, seen_b = np.zeros(U, np.int32), np.zeros(-(-I // 32), np.int32)
+    for r in range(8):
+        (glo, ghi), (lo, hi), (blo, bhi) = grid_ranges(U, I, 8, 2, r, tb)
+        assert glo <= lo <= hi <= ghi and blo % tb == 0
+        seen_u[lo:hi] += 1
+        seen_b[blo:bhi] += 1
+    assert (seen_u == 1).all() and (seen_b == 2).all()  # every item block screened once per user group
+
+
 def test_shard_blocks_tile_aligned():
     from nrk.dist import shard_blocks
 
