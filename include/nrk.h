@@ -148,10 +148,16 @@ int nrk_ip_topk_bound(const float* users, int64_t n_users, const void* catalog, 
 int nrk_ip_topk_apply_bound(int64_t n_users, const float* bounds, int n_lists, int m, int k, void* workspace,
                             size_t workspace_bytes, nrk_stream_t stream);
 
+/* 32-item blocks per screen tile at this dim (one LDS ring slot of the MFMA
+ * scan; 8 KB, or 4 blocks = 32 KB at dims 65..128): catalog shard ranges start
+ * on a tile.  0 for dim outside [1, 256].  Host-only, no device work.  New: no
+ * reference counterpart (Faiss shards are whole indexes). */
+int nrk_ip_topk_tile_blocks(int dim);
+
 /* Config 4 (catalog sharded) with owner refine: every rank
  * holds the SAME packed catalog and fp32 rows (nrk_ip_catalog_build over all
  * items) and screens only its block range [blk_lo, blk_hi) (32-item blocks;
- * blk_lo a multiple of 8192 / (64 * pad_dim(dim)), blk_hi too unless it is
+ * blk_lo a multiple of nrk_ip_topk_tile_blocks(dim), blk_hi too unless it is
  * the catalog end) for every user; half-block ids stay global.  No per-shard
  * select:
  *   nrk_ip_topk_shard_screen = the scan of [blk_lo, blk_hi) + per user the m

@@ -54,10 +54,13 @@ constexpr int IP_KMAX = 2048;   // largest k at all (exact path above IP_KFAST)
 #define NRK_SCAN_TILE 8192
 #endif
 constexpr int SCAN_TILE = NRK_SCAN_TILE;
-// dim 128 (BASELINE config 5): blocks per tile (a 32-item block is already
-// 8 KB there; dev A/B -DNRK_SCAN_TB128=2: 16-KB tiles, one barrier per two blocks)
+// dim 128 (BASELINE config 5): blocks per tile -- a 32-item block is already
+// 8 KB there; 4 blocks (32-KB tiles): one barrier / DMA wait per four blocks
+// and the next block's fragments read under the current block's MFMAs (see
+// ip_scan_kernel's PF2).  250k users x 5M items, one box (tools/scan128.py,
+// rows identical): 275.6 ms at 1 block, 254.3 at 2, 245.1 at 4
 #ifndef NRK_SCAN_TB128
-#define NRK_SCAN_TB128 1
+#define NRK_SCAN_TB128 4
 #endif
 // 32-item blocks per screen tile (one LDS ring slot, one barrier) at padded dim dp
 __host__ __device__ constexpr int scan_tb(int dp) {
@@ -594,6 +597,33 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
     auto pf_wait = [&](u32x4 (&cur)[DS]) {
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1])::"memory");
     };
+    // DS >= 4 with several blocks per tile (dims 64, 128): two fragment sets
+    // by block parity -- block b + 1's DS reads are issued right after block
+    // b's have landed, so they fly under block b's UG x DS MFMAs (one LDS
+    // round trip per tile exposed instead of one per block)
+    constexpr bool PF2 = DS >= 4 && TB >= 2;
+    auto blk_issue = [&](int sl, int b, u32x4 (&af)[DS]) {
+        const uint32_t base = lds0 + (uint32_t)(sl * TILE_BYTES + b * DS * 1024);
+#pragma unroll
+        for (int s2 = 0; s2 < DS; s2 += 4)
+            asm volatile(
+                "ds_read_b128 %0, %4 offset:0\n\tds_read_b128 %1, %4 offset:1024\n\t"
+                "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072"
+                : "=&v"(af[s2]), "=&v"(af[s2 + 1]), "=&v"(af[s2 + 2]), "=&v"(af[s2 + 3])
+                : "v"(base + 1024u * s2)
+                : "memory");
+    };
+    auto blk_wait = [&](u32x4 (&af)[DS]) {
+        if constexpr (DS == 4) {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3])::"memory");
+        } else {
+#pragma unroll
+            for (int s2 = 0; s2 < DS; s2 += 8)
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(af[s2]), "+v"(af[s2 + 1]), "+v"(af[s2 + 2]), "+v"(af[s2 + 3]), "+v"(af[s2 + 4]),
+                               "+v"(af[s2 + 5]), "+v"(af[s2 + 6]), "+v"(af[s2 + 7])::"memory");
+        }
+    };
     const int full_tiles = tail_blk / TB;  // tiles whose blocks are all full
     // the tile's MFMAs and half-block maxima (mx); the bookkeeping on them
     // (appends, inserts) is book() below.  Software pipeline over the TB x UG
@@ -626,9 +656,16 @@ __global__ __launch_bounds__(NW * 64, WPE) void ip_scan_kernel(
         constexpr int LAG = 2, NACC = LAG + 1, NSTEP = TB * UG;
         f32x16 acc[NACC];
         u32x4 afb[DS];
+        u32x4 fb2[PF2 ? 2 : 1][PF2 ? DS : 1];
+        if constexpr (PF2) blk_issue(sl, 0, fb2[0]);
         static_for<TB>([&](auto bc) {
             constexpr int b = decltype(bc)::value;
-            if constexpr (PF) {
+            if constexpr (PF2) {
+                blk_wait(fb2[b & 1]);
+                if constexpr (b + 1 < TB) blk_issue(sl, b + 1, fb2[(b + 1) & 1]);
+#pragma unroll
+                for (int s = 0; s < DS; ++s) afb[s] = fb2[b & 1][s];
+            } else if constexpr (PF) {
                 u32x4 afn[DS];
                 if constexpr (b + 1 < TB) pf_wait_issue(afp, sl, b + 1, afn);
                 else pf_wait(afp);
@@ -1608,12 +1645,15 @@ __device__ __forceinline__ double exact_dot(const float* __restrict__ a, const f
 #define NRK_REFINE_DIRECT 1
 #endif
 constexpr bool REFINE_DIRECT = NRK_REFINE_DIRECT;
-// waves per SIMD the refine's registers are sized for
+// waves per SIMD the refine's registers are sized for (dim 64's staged
+// rounds take 2).  Round 6: two prefilter rounds in flight (three register
+// slots rotated by unrolling) at 3 waves per SIMD measured slower than one
+// round ahead at 4: finish 0.961-0.966 vs 0.873-0.884 ms (config 2, one box)
 #ifndef NRK_REFINE_WPE
 #define NRK_REFINE_WPE 4
 #endif
 template <int DS4, int SV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRK_REFINE_WPE))) void ip_refine_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ? 2 : NRK_REFINE_WPE))) void ip_refine_kernel(
     const float* __restrict__ users, int64_t n_users, const float* __restrict__ items,
     const uint8_t* __restrict__ catalog, int64_t n_items, int dim, int k, int64_t row_offset,
     const uint2* __restrict__ cand, int bandcap, const int32_t* __restrict__ cand_cnt,
@@ -2710,7 +2750,9 @@ template <int DP, int MT>
 static void launch_scan(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                         const IpWs& w, hipStream_t s) {
     constexpr int UG = (DP <= 128 && MT <= 32) ? 2 : 1;
-    constexpr int WPE = (DP >= 128 || MT >= 32) ? 2 : 4;
+    // 2 waves per SIMD everywhere: at 4 (128 VGPRs) the dim-16 / dim-64
+    // k <= 32 and the dim-32 k <= 64 variants spilled 42-96 VGPRs to scratch
+    constexpr int WPE = 2;
     if constexpr (DP == 32 && MT == 16) {
         // default at D = 32, k <= 32 (BASELINE config 2): 8 waves x 128 users
         // (UG = 4) per workgroup at 2 waves / SIMD -- every LDS fragment read
@@ -2725,7 +2767,10 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
     // whole-tile appends 7.4-7.5 with 885 (the select reads 2.6x more);
     // 4-wave workgroups 7.9-8.2, 4 / 6 / 8 ring slots 7.3-7.4, alternating
     // inserts 8.1 (the lagging cut doubles the appends)
-    constexpr int NW = (UG == 2) ? 8 : 4, NSL = (UG == 2) ? 3 : 4;
+    // ring slots capped by the CU's 160 KB of LDS (dim 128's 32-KB tiles: 4 -> 3 at UG = 1)
+    constexpr int TILE_B = scan_tb(DP) * 64 * DP, NSL_CAP = 163840 / TILE_B;
+    constexpr int NW = (UG == 2) ? 8 : 4, NSL0 = (UG == 2) ? 3 : 4, NSL = NSL0 < NSL_CAP ? NSL0 : NSL_CAP;
+    static_assert(NSL >= 2, "ring");
     launch_scan_v<DP, NW, NSL, UG, MT, WPE>(users, n_users, cat, n_items, dim, k, w, s);
 }
 
@@ -2807,6 +2852,11 @@ int nrk_dev_scan_stamps(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(scan_stamps), sizeof(scan_stamps)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+int nrk_ip_topk_tile_blocks(int dim) {
+    if (dim <= 0 || dim > 256) return 0;
+    return scan_tb(pad_dim(dim));
+}
 
 size_t nrk_ip_catalog_bytes(int64_t n_items, int dim) {
     if (n_items < 0 || dim <= 0 || dim > 256) return 0;

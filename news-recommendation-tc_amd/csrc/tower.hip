@@ -10,7 +10,7 @@
 namespace nrk {
 
 #ifndef NRK_TT_CH
-#define NRK_TT_CH 16
+#define NRK_TT_CH 8
 #endif
 
 template <int D>
@@ -44,8 +44,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
     __syncthreads();  // the only block barrier: the user loop below is per wave
 
     constexpr int P = WAVE / D;  // history phases per lane group
-    // history rows in flight per lane: every row of a config-2 user (T = 30,
-    // D = 32: 15 per lane) in one round trip (dev A/B: -DNRK_TT_CH=8)
+    // history rows in flight per lane (a config-2 user, T = 30 at D = 32, has
+    // up to 15 per lane: two rounds).  All 16 at once measured slower in the
+    // bench (tower 0.330-0.334 vs 0.294-0.295 ms, one box, two pairs): a
+    // round issues CH unconditional loads per lane, and most histories are
+    // short (dev A/B: -DNRK_TT_CH=16)
     constexpr int CH = NRK_TT_CH;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int d = lane % D, ph = lane / D;

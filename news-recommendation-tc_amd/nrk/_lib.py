@@ -32,6 +32,7 @@ SIGNATURES = {
     "nrk_ip_catalog_bytes": (SZ, [I64, INT]),
     "nrk_ip_catalog_build": (INT, [P, I64, INT, P, P]),
     "nrk_ip_topk_workspace_bytes": (SZ, [I64, I64, INT, INT]),
+    "nrk_ip_topk_tile_blocks": (INT, [INT]),
     "nrk_ip_topk": (INT, [P, I64, P, P, I64, INT, INT, I64, P, P, P, P, SZ, P]),
     "nrk_ip_topk_screen": (INT, [P, I64, P, I64, INT, INT, P, SZ, P]),
     "nrk_ip_topk_finish": (INT, [P, I64, P, P, I64, INT, INT, I64, P, P, P, P, SZ, P]),

@@ -249,9 +249,12 @@ def ip_topk_bound(users, catalog: Catalog, k: int, m: int, workspace):
 
 
 def ip_topk_tile_blocks(d: int) -> int:
-    """32-item blocks per screen tile (shard ranges start on a tile)."""
-    dp = 16 if d <= 16 else 32 if d <= 32 else 64 if d <= 64 else 128 if d <= 128 else 256
-    return max(1, 8192 // (64 * dp))
+    """32-item blocks per screen tile (shard ranges start on a tile):
+    nrk_ip_topk_tile_blocks, the scan's own constant (no device work)."""
+    tb = _lib.lib().nrk_ip_topk_tile_blocks(int(d))
+    if tb <= 0:
+        raise ValueError(f"dim must be in [1, 256], got {d}")
+    return tb
 
 
 def ip_topk_shard_screen(users, catalog: Catalog, k: int, blk_lo: int, blk_hi: int, m: int, workspace):
