@@ -1469,9 +1469,33 @@ __device__ __forceinline__ void lds_ranks(const uint32_t* __restrict__ row, int 
     }
 }
 
-// the key of rank r (r < c) of a wave's LDS row of c keys (see lds_ranks),
-// 64 keys at a time (a run-time loop: few registers whatever c is)
+// 64 keys, one per lane, sorted descending by a wave bitonic network (21
+// exchange stages through lane_xor: DPP / ds_swizzle / permlane swaps, one
+// max-or-min each)
+__device__ __forceinline__ uint32_t wave_sort_desc_u32(uint32_t x, int lane) {
+    static_for<6>([&](auto klc) {
+        constexpr int kl = decltype(klc)::value + 1, k = 1 << kl;
+        static_for<kl>([&](auto jc) {
+            constexpr int j = 1 << (kl - 1 - decltype(jc)::value);
+            const uint32_t y = lane_xor<j>(x);
+            const bool up = (lane & k) == 0;  // k = 64: every lane (descending overall)
+            const bool lower = (lane & j) == 0;
+            x = (lower == up) ? max(x, y) : min(x, y);
+        });
+    });
+    return x;
+}
+
+// the key of rank r (r < c) of a wave's LDS row of c keys (see lds_ranks):
+// up to 64 keys by one wave sort (~21 exchange stages; the rank count costs
+// ~5 VALU per key per lane), more 64 at a time (a run-time loop: few
+// registers whatever c is)
 __device__ __forceinline__ uint32_t lds_select(uint32_t* __restrict__ row, int c, int r, int lane) {
+    if (c <= WAVE) {
+        wave_sync_lds();
+        const uint32_t srt = wave_sort_desc_u32(lane < c ? row[lane] : 0u, lane);
+        return (uint32_t)__builtin_amdgcn_readlane((int)srt, r);
+    }
     if (lane < 4) row[c + lane] = 0u;  // zero pad (the row has room: c + 4 <= its size)
     wave_sync_lds();
     uint32_t x = 0u;
