@@ -1516,7 +1516,15 @@ __device__ __forceinline__ uint32_t lds_select(uint32_t* __restrict__ row, int c
 // wid, wid + nw, ...; the next user's counts / record are loaded during this one) and
 // load a user's appended entries 256 at a time, all loads in flight at once:
 // one wave per user was bound by per-wave start-up and dependent round trips.
-constexpr int SH_WG_PER_CU = 8;
+// Workgroups per CU of those persistent grids: every one must be resident,
+// or the queued ones run after the first finish (a second, thinner wave of
+// work).  Their ~106 SGPRs admit 6 4-wave workgroups per CU, not 8
+// (MI355X_MICROARCH.md: floor(800 / (ceil(sgpr / 16) 16 + 16)); the
+// occupancy API says 7).  Dev A/B: -DNRK_SH_WG=8 (the round-5 grid).
+#ifndef NRK_SH_WG
+#define NRK_SH_WG 6
+#endif
+constexpr int SH_WG_PER_CU = NRK_SH_WG;
 constexpr int SH_ENT = 4;  // entries per lane per load batch
 
 __device__ __forceinline__ void sh_load(const uint2* s0, const uint2* s1, int a0, int n, int b0, int lane,

@@ -270,6 +270,19 @@ __global__ __launch_bounds__(256) void tt_item_kernel(const float* __restrict__ 
 
 using namespace nrk;
 
+// workgroups of 256 threads resident at once on the device (occupancy API x
+// CUs), at most one per 4 users; dev A/B: -DNRK_TT_GRID=2048 (the old fixed grid)
+#ifndef NRK_TT_GRID
+#define NRK_TT_GRID 0
+#endif
+static int tt_grid(const void* fn, size_t lds, int64_t n) {
+    int per_cu = 0, dev = 0, cus = 256;
+    if (NRK_TT_GRID > 0) return (int)std::min<int64_t>((n + 3) / 4, NRK_TT_GRID);
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 4;
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n + 3) / 4, (int64_t)per_cu * std::max(cus, 1)));
+}
+
 extern "C" {
 
 int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* item_table,
@@ -291,11 +304,14 @@ int nrk_tt_user_fwd(const float* user_table, int64_t n_user_rows, const float* i
     const size_t lds = sizeof(float) * ((size_t)h0 * (2 * dim + 4) + h0p + (size_t)h1 * (h0p + 4) + h1p +
                                         (size_t)4 * (2 * dim + 128));
     hipStream_t s = as_stream(stream);
-    const int grid = (int)std::min<int64_t>((n + 3) / 4, 2048);
+    // persistent grid of resident workgroups only (the weights' LDS admits ~5
+    // per CU): a grid larger than the resident set left the queued
+    // workgroups to run after the first ones finished, on a thinner machine
 #define NRK_TT_LAUNCH(DD)                                                                      \
     do {                                                                                       \
         (void)hipFuncSetAttribute((const void*)tt_user_kernel<DD>,                                 \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);             \
+        const int grid = tt_grid((const void*)tt_user_kernel<DD>, lds, n);                      \
         tt_user_kernel<DD><<<grid, 256, lds, s>>>(user_table, item_table, uid, hist, hist_len, \
                                                   n, seq_len, w0, b0, h0, w1, b1, h1, out);    \
     } while (0)
