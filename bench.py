@@ -57,7 +57,7 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-PROFILE_ROUND = "r05"
+PROFILE_ROUND = "r06"
 TRAFFIC_FILE = os.path.join(REPO, "profiles", PROFILE_ROUND + "_traffic.json")
 BUSY_FILE = os.path.join(REPO, "profiles", PROFILE_ROUND + "_busy.json")
 CSRC = os.path.join(REPO, "news-recommendation-tc_amd", "csrc")
