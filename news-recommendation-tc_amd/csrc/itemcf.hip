@@ -10,8 +10,9 @@
 // global sequence number ("slot") = pair_off[u] + loc1 * L_u + loc2, and the
 // reference's fp64 sum for (i, j) is the sum of its pair weights in slot
 // order.  The GPU reproduces exactly that order without a hash table:
-//   1. cf_pairs        one wave per user: weight w[slot] and key
-//                      (i << b | j) per slot (i == j -> sentinel), item_cnt.
+//   1. cf_pairs_flat   flat over the slots, CF_CHUNK per wave: weight
+//                      w[slot] and key (i << b | j) per slot (i == j ->
+//                      sentinel); cf_item_count: item_cnt.
 //   2. LSD radix sort  of (key, slot) -- stable, so equal keys keep slot
 //                      order (rs_upsweep / rs_scan_rows / rs_downsweep,
 //                      8 bits per pass, 2b bits total).
@@ -123,6 +124,7 @@ __global__ __launch_bounds__(1024) void scan_exclusive_kernel(F f, int64_t n, in
 struct CfParams {
     double loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha;
     int64_t dt_zero;  // |dt| >= dt_zero -> pow(time_alpha, dt) is +0 (cf_dt_zero)
+    double ln_time, ln_created;  // cf_ln of the two alphas
 };
 
 // Smallest |dt| from which time_alpha^|dt| lies below 2^-1100 for every dt
@@ -131,6 +133,22 @@ struct CfParams {
 // evaluating it.  Click timestamps are milliseconds (0.7^dt underflows from
 // dt ~ 2,100 ms on), so this is nearly every pair.  No shortcut unless
 // 0 < time_alpha < 1.
+// The two time-decay factors are exp(alpha^x) (weights.py time_decay_weight).
+// Round 6 evaluates alpha^x as exp(x ln alpha) with ln alpha formed once on
+// the host: the device pow re-derives log(alpha) in double-double on every
+// call, most of its cost, in the kernel that spends its time on these
+// factors.  The exponent carries an absolute error <= |y| 2^-52 (y = x ln
+// alpha), so alpha^x is off by a relative |y| 2^-52 and exp(alpha^x) by
+// e^y |y| 2^-52 <= 2^-52 / e relative: below half an ulp of the factor (the
+// ItemCF bar is rtol 1e-12; device and host libm already differ by an ulp).
+// ln is NaN (-> the device pow) unless alpha is positive and finite.
+static inline double cf_ln(double alpha) {
+    return alpha > 0.0 && std::isfinite(alpha) ? std::log(alpha) : NAN;
+}
+__device__ __forceinline__ double cf_apow(double alpha, double ln_alpha, double x) {
+    return ln_alpha == ln_alpha ? exp(x * ln_alpha) : pow(alpha, x);
+}
+
 static inline int64_t cf_dt_zero(double time_alpha) {
     if (!(time_alpha > 0.0 && time_alpha < 1.0)) return INT64_MAX;
     const double l2 = -std::log2(time_alpha);  // > 0
@@ -138,28 +156,124 @@ static inline int64_t cf_dt_zero(double time_alpha) {
     return d < 9.0e18 ? (int64_t)d : INT64_MAX;
 }
 
-__global__ __launch_bounds__(256) void cf_pairs_kernel(
+// item_cnt[i] += the occurrences of i in the users' clicks (item_cf.py:43,
+// cnt[i] += 1 per occurrence).  Round 5 counted with one global atomic per
+// click from the pairs kernel: a popular item's counter took tens of
+// thousands of same-address atomics in a row, 1.65 of that kernel's 1.89 ms.
+// Here a workgroup folds 4,096 clicks into an LDS hash table (open
+// addressing, load <= 1/2) and adds each distinct item's count once: a hot
+// item's counter sees one atomic per chunk.
+constexpr int CF_CNT_CHUNK = 4096;
+constexpr int CF_CNT_SLOTS = 8192;
+constexpr int CF_CNT_THREADS = 512;
+
+__global__ __launch_bounds__(CF_CNT_THREADS) void cf_item_count_kernel(const int64_t* __restrict__ offsets,
+                                                                     int64_t n_users,
+                                                                     const int32_t* __restrict__ items,
+                                                                     unsigned long long* __restrict__ cnt) {
+    __shared__ int32_t hk[CF_CNT_SLOTS];
+    __shared__ uint32_t hc[CF_CNT_SLOTS];
+    const int64_t c0 = offsets[0], c1 = offsets[n_users];
+    for (int64_t a = c0 + (int64_t)blockIdx.x * CF_CNT_CHUNK; a < c1; a += (int64_t)gridDim.x * CF_CNT_CHUNK) {
+        for (int t = threadIdx.x; t < CF_CNT_SLOTS; t += CF_CNT_THREADS) {
+            hk[t] = -1;
+            hc[t] = 0;
+        }
+        __syncthreads();
+        const int64_t e1 = a + CF_CNT_CHUNK < c1 ? a + CF_CNT_CHUNK : c1;
+        for (int64_t e = a + threadIdx.x; e < e1; e += CF_CNT_THREADS) {
+            const int32_t it = items[e];  // >= 0
+            uint32_t t = ((uint32_t)it * 2654435761u) >> 19;  // 13-bit multiplicative hash
+            for (;;) {
+                const int32_t prev = atomicCAS(&hk[t], -1, it);
+                if (prev == -1 || prev == it) {
+                    atomicAdd(&hc[t], 1u);
+                    break;
+                }
+                t = (t + 1) & (CF_CNT_SLOTS - 1);
+            }
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < CF_CNT_SLOTS; t += CF_CNT_THREADS)
+            if (hc[t]) atomicAdd(&cnt[hk[t]], (unsigned long long)hc[t]);
+        __syncthreads();
+    }
+}
+
+// cf_pairs_flat_kernel: every ordered position pair's key, global slot and
+// weight, flat over the global pair index (round 6; round 5's one wave per
+// user left the kernel waiting on its heaviest users -- a user with L
+// clicks has L^2 pairs (a capped 250-click history: 62,500, one wave's
+// ~980 serial steps of fp64 pow / exp while the average user needs 1.3).
+// Here a wave takes chunks of CF_CHUNK consecutive pair slots (slot order =
+// the reference's (user, loc1, loc2) order, pair_off = the exclusive scan
+// of L^2) and every lane finds its pair's user in a window of 64 pair ends
+// that follows the chunk.  Same keys and slots as round 5; the weights differ only by
+// cf_apow's sub-ulp rounding.
+constexpr int CF_CHUNK = 64 * 8;
+
+__global__ __launch_bounds__(256) void cf_pairs_flat_kernel(
     const int64_t* __restrict__ offsets, int64_t n_users, const int32_t* __restrict__ items,
     const int64_t* __restrict__ ts, const double* __restrict__ created,
     const int64_t* __restrict__ pair_off, int64_t slot_base, CfParams prm, int bj, uint64_t sentinel,
-    uint64_t* __restrict__ keys, int32_t* __restrict__ vals, double* __restrict__ w,
-    unsigned long long* __restrict__ cnt) {
+    uint64_t* __restrict__ keys, int32_t* __restrict__ vals, double* __restrict__ w) {
     const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    // beta^dl for dl < 64 (the same device pow of the same arguments: same bits)
     __shared__ double lwt[64];
     if (threadIdx.x < 64) lwt[threadIdx.x] = pow(prm.loc_beta, (double)threadIdx.x);
     __syncthreads();
-    for (int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < n_users; u += nw) {
-        const int64_t b = offsets[u];
-        const int64_t L = offsets[u + 1] - b;
-        const int64_t base = pair_off[u];
-        // user_penalty = 1 / log_penalty(len) = 1 / log(L + 1) (item_cf.py:69-71)
-        const double pen = 1.0 / log((double)(L + 1));
-        for (int64_t l = lane; l < L; l += 64) atomicAdd(&cnt[items[b + l]], 1ull);
-        const bool small = L * L < (1ll << 31);  // 32-bit pair -> (l1, l2) division
-        for (int64_t s = lane; s < L * L; s += 64) {
-            const int64_t l1 = small ? (int64_t)((uint32_t)s / (uint32_t)L) : s / L, l2 = s - l1 * L;
+    const int64_t total = pair_off[n_users];
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t c0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * CF_CHUNK; c0 < total; c0 += nw * CF_CHUNK) {
+        // the chunk's first user, the largest u with pair_off[u] <= c0 (it has
+        // pairs: pair_off[u + 1] > c0): a 64-ary search by the whole wave
+        int64_t lo = 0, hi = n_users;  // pair_off[lo] <= c0 < pair_off[hi]
+        while (hi - lo > 1) {
+            const int64_t step = (hi - lo + 63) >> 6;
+            const int64_t q = lo + step * lane;
+            const uint64_t le = __ballot(q < hi && pair_off[q] <= c0);  // a prefix of the lanes
+            const int64_t nlo = lo + step * (63 - __builtin_clzll(le));
+            hi = nlo + step < hi ? nlo + step : hi;
+            lo = nlo;
+        }
+        // a window of 64 users' pair ends, one per lane; each lane finds its
+        // pair's user by a 6-step search over the window (shuffles), the
+        // window moving on to the last lane's user after every 64 pairs
+        int64_t ub = lo;
+        int64_t wend = ub + lane < n_users ? pair_off[ub + lane + 1] : INT64_MAX;
+        int64_t cu = -1, b = 0, L = 1, base = 0;
+        double pen = 0.0;
+        for (int it = 0; it < CF_CHUNK / 64; ++it) {
+            if (c0 + it * 64 >= total) break;  // wave-uniform
+            const int64_t p = c0 + it * 64 + lane;
+            const bool live = p < total;
+            int64_t u = -1;
+            for (;;) {  // converged: the shuffles below need every lane
+                int k = 0;
+#pragma unroll
+                for (int st = 32; st >= 1; st >>= 1)
+                    if (__shfl(wend, k + st - 1, WAVE) <= p) k += st;
+                if (u < 0 && k < 64) u = ub + k;
+                if (!__any(live && u < 0)) break;  // users with no pairs pushed a lane past the window
+                ub += 64;
+                wend = ub + lane < n_users ? pair_off[ub + lane + 1] : INT64_MAX;
+            }
+            const int64_t un = __shfl(u, 63, WAVE);
+            if (un >= 0 && un != ub) {
+                ub = un;
+                wend = ub + lane < n_users ? pair_off[ub + lane + 1] : INT64_MAX;
+            }
+            if (!live) break;
+            if (u != cu) {
+                cu = u;
+                b = offsets[u];
+                L = offsets[u + 1] - b;
+                base = pair_off[u];
+                // user_penalty = 1 / log_penalty(len) = 1 / log(L + 1) (item_cf.py:69-71)
+                pen = 1.0 / log((double)(L + 1));
+            }
+            const int64_t sl = p - base;
+            const bool small = L * L < (1ll << 31);  // 32-bit pair -> (l1, l2) division
+            const int64_t l1 = small ? (int64_t)((uint32_t)sl / (uint32_t)L) : sl / L, l2 = sl - l1 * L;
             const int32_t i = items[b + l1], j = items[b + l2];
             uint64_t key = sentinel;
             double wt = 0.0;
@@ -169,14 +283,14 @@ __global__ __launch_bounds__(256) void cf_pairs_kernel(
                 const double loc_w = la * (dl < 64 ? lwt[dl] : pow(prm.loc_beta, (double)dl));
                 const int64_t ti = ts[b + l1], tj = ts[b + l2];
                 const int64_t dt = ti > tj ? ti - tj : tj - ti;
-                const double click_w = dt >= prm.dt_zero ? 1.0 : exp(pow(prm.time_alpha, (double)dt));
-                const double created_w = exp(pow(prm.created_alpha, fabs(created[i] - created[j])));
+                const double click_w = dt >= prm.dt_zero ? 1.0 : exp(cf_apow(prm.time_alpha, prm.ln_time, (double)dt));
+                const double created_w = exp(cf_apow(prm.created_alpha, prm.ln_created, fabs(created[i] - created[j])));
                 wt = loc_w * click_w * created_w * pen;
                 key = ((uint64_t)(uint32_t)i << bj) | (uint32_t)j;
             }
-            keys[base + s] = key;
-            vals[base + s] = (int32_t)(slot_base + base + s);  // the pair's global slot
-            w[base + s] = wt;
+            keys[p] = key;
+            vals[p] = (int32_t)(slot_base + p);  // the pair's global slot
+            w[p] = wt;
         }
     }
 }
@@ -192,11 +306,15 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const uint64_t* __restr
     hist[tid] = 0;
     __syncthreads();
     const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
-#pragma unroll 4
+    uint32_t dr[RS_ITEMS];
+#pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         const int64_t e = t0 + r * RS_THREADS + tid;
-        if (e < n) atomicAdd(&hist[(keys[e] >> shift) & 255], 1u);
+        dr[r] = e < n ? (uint32_t)(keys[e] >> shift) & 255u : 256u;
     }
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r)
+        if (dr[r] < 256u) atomicAdd(&hist[dr[r]], 1u);
     __syncthreads();
     counts[(size_t)tid * nblk + blockIdx.x] = hist[tid];
 }
@@ -233,43 +351,63 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// Scatter pass.  Round 6: the tile is ranked into LDS first (digit-major,
+// stable: round-major input order within a digit) and then written out in
+// that order, so consecutive threads store consecutive addresses of a digit's
+// run (~16 keys per digit per tile) -- round 5 stored each 256-key round
+// straight from the ranking, one partial line per lane.  The tile's own digit
+// counts are the differences of the block-scanned counts row.  LDS: 52 KB
+// (three workgroups per CU).
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(
     const uint64_t* __restrict__ kin, const int32_t* __restrict__ vin, uint64_t* __restrict__ kout,
     int32_t* __restrict__ vout, int64_t n, int shift, int nblk, const uint32_t* __restrict__ counts,
     const uint32_t* __restrict__ totals) {
-    __shared__ uint32_t base[256];
-    __shared__ uint32_t run[256];
-    __shared__ uint32_t wc[4][256];
+    __shared__ uint64_t sk[RS_TILE];
+    __shared__ int32_t sv[RS_TILE];
+    __shared__ uint32_t base[256];    // global start of digit d minus its tile-local start
+    __shared__ uint16_t run[256];     // tile-local write position of digit d
+    __shared__ uint16_t wc[4][256];
     const int tid = threadIdx.x, wv = tid >> 6;
-    // digit base = exclusive scan of totals + this block's offset in the row
     {
+        // exclusive scans over the digits: the global starts (totals) and the
+        // tile-local starts (this tile's counts), both in one pass
         const uint32_t t = totals[tid];
-        base[tid] = t;
+        const uint32_t cb = counts[(size_t)tid * nblk + blockIdx.x];
+        const uint32_t cn = (blockIdx.x + 1 < (unsigned)nblk ? counts[(size_t)tid * nblk + blockIdx.x + 1] : t) - cb;
+        uint32_t* sg = reinterpret_cast<uint32_t*>(sv);  // scan scratch (sv is filled later)
+        uint32_t* sl = sg + 256;
+        sg[tid] = t;
+        sl[tid] = cn;
         __syncthreads();
         for (int d = 1; d < 256; d <<= 1) {
-            const uint32_t v = tid >= d ? base[tid - d] : 0;
+            const uint32_t vg = tid >= d ? sg[tid - d] : 0, vl = tid >= d ? sl[tid - d] : 0;
             __syncthreads();
-            base[tid] += v;
+            sg[tid] += vg;
+            sl[tid] += vl;
             __syncthreads();
         }
-        const uint32_t excl = base[tid] - t;
-        __syncthreads();
-        base[tid] = excl + counts[(size_t)tid * nblk + blockIdx.x];
-        run[tid] = 0;
+        const uint32_t lstart = sl[tid] - cn;
+        base[tid] = (sg[tid] - t) + cb - lstart;  // mod 2^32: base + local position = global position
+        run[tid] = (uint16_t)lstart;
     }
     const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    // the tile's 16 keys / values per thread, all in flight at once
+    uint64_t kr[RS_ITEMS];
+    int32_t vr[RS_ITEMS];
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const int64_t e = t0 + r * RS_THREADS + tid;
+        kr[r] = e < n ? kin[e] : 0;
+        vr[r] = e < n ? vin[e] : 0;
+    }
+#pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 4; ++k) wc[k][tid] = 0;
-        const int64_t e = t0 + r * RS_THREADS + tid;
-        const bool ok = e < n;
-        uint64_t key = 0;
-        int32_t val = 0;
-        if (ok) {
-            key = kin[e];
-            val = vin[e];
-        }
+        const bool ok = t0 + r * RS_THREADS + tid < n;
+        const uint64_t key = kr[r];
+        const int32_t val = vr[r];
         const uint32_t d = (uint32_t)(key >> shift) & 255u;
         uint64_t m = __ballot(ok);
 #pragma unroll
@@ -280,23 +418,31 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(
         }
         const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
         __syncthreads();
-        if (ok && rank == 0) wc[wv][d] = (uint32_t)__popcll(m);
+        if (ok && rank == 0) wc[wv][d] = (uint16_t)__popcll(m);
         __syncthreads();
         {
             const uint32_t c0 = wc[0][tid], c1 = wc[1][tid], c2 = wc[2][tid], c3 = wc[3][tid];
             const uint32_t r0 = run[tid];
-            wc[0][tid] = r0;
-            wc[1][tid] = r0 + c0;
-            wc[2][tid] = r0 + c0 + c1;
-            wc[3][tid] = r0 + c0 + c1 + c2;
-            run[tid] = r0 + c0 + c1 + c2 + c3;
+            wc[0][tid] = (uint16_t)r0;
+            wc[1][tid] = (uint16_t)(r0 + c0);
+            wc[2][tid] = (uint16_t)(r0 + c0 + c1);
+            wc[3][tid] = (uint16_t)(r0 + c0 + c1 + c2);
+            run[tid] = (uint16_t)(r0 + c0 + c1 + c2 + c3);
         }
         __syncthreads();
         if (ok) {
-            const uint32_t pos = base[d] + wc[wv][d] + rank;
-            kout[pos] = key;
-            vout[pos] = val;
+            const uint32_t lp = wc[wv][d] + rank;
+            sk[lp] = key;
+            sv[lp] = val;
         }
+    }
+    __syncthreads();
+    const int nloc = n - t0 < RS_TILE ? (int)(n - t0) : RS_TILE;
+    for (int i = tid; i < nloc; i += RS_THREADS) {
+        const uint64_t key = sk[i];
+        const uint32_t gp = base[(uint32_t)(key >> shift) & 255u] + (uint32_t)i;
+        kout[gp] = key;
+        vout[gp] = sv[i];
     }
 }
 
@@ -466,7 +612,12 @@ __global__ __launch_bounds__(1024) void cf_head_scan(const uint32_t* __restrict_
 
 // 3. one entry per distinct key: (i, j), the run's sum (normalised by
 //    sqrt(cnt_i cnt_j) when cnt is given, item_cf.py:81-84) and the first slot
-//    (the dict insertion order the reference's stable sorts break ties by)
+//    (the dict insertion order the reference's stable sorts break ties by).
+//    Round 6: the tile's heads are compacted in LDS (their tile positions and
+//    sums) and written by consecutive threads to consecutive entries -- round
+//    5 stored them from the per-thread chunk walk, every lane to its own line
+//    of each of the four outputs.  A run that ends in a later tile gets its sum
+//    from that tile (the only global scalar store left, one per tile at most).
 __global__ __launch_bounds__(RS_THREADS) void cf_emit(
     const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, const double* __restrict__ ws,
     int64_t n, uint64_t sentinel, const uint32_t* __restrict__ blkoff, const double* __restrict__ carry,
@@ -474,29 +625,31 @@ __global__ __launch_bounds__(RS_THREADS) void cf_emit(
     int32_t* __restrict__ out_i, int32_t* __restrict__ out_j, double* __restrict__ out_v,
     int64_t* __restrict__ out_first) {
     __shared__ __attribute__((aligned(16))) uint8_t fl[CF_FL];
-    __shared__ double sw[CF_SW];
+    __shared__ double sw[CF_SW];  // the sorted weights, then the heads' sums
+    __shared__ uint16_t hpos[RS_TILE];
     __shared__ double pv[RS_THREADS];
     __shared__ int pf[RS_THREADS];
     __shared__ uint32_t ph[RS_THREADS];
     const int tid = threadIdx.x;
     const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+    const int nloc = n - t0 < RS_TILE ? (int)(n - t0) : RS_TILE;
     cf_stage_flags(keys, n, t0, sentinel, fl);
 #pragma unroll 4
-    for (int i = tid; i < RS_TILE; i += RS_THREADS) {
-        const int64_t e = t0 + i;
-        if (e < n) sw[cf_pad(i)] = ws[e];
-    }
+    for (int i = tid; i < nloc; i += RS_THREADS) sw[cf_pad(i)] = ws[t0 + i];
     __syncthreads();
     const int l0 = tid * RS_ITEMS;
-    const int64_t a = t0 + l0;
     uint8_t f[RS_ITEMS + 1];
     cf_chunk_flags(fl, l0, f);
+    double x[RS_ITEMS];
     SegSum agg{0.0, 0};
     uint32_t my = 0;
+#pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        if (a + r >= n) break;
-        if (f[r] == 1) ++my;
-        agg = seg_combine(agg, SegSum{sw[cf_pad(l0 + r)], (f[r] & 1) ? 1 : 0});
+        x[r] = l0 + r < nloc ? sw[cf_pad(l0 + r)] : 0.0;
+        if (l0 + r < nloc) {
+            if (f[r] == 1) ++my;
+            agg = seg_combine(agg, SegSum{x[r], (f[r] & 1) ? 1 : 0});
+        }
     }
     pv[tid] = agg.v;
     pf[tid] = agg.f;
@@ -521,28 +674,41 @@ __global__ __launch_bounds__(RS_THREADS) void cf_emit(
     }
     SegSum run{carry[blockIdx.x], 0};
     if (tid > 0) run = seg_combine(run, SegSum{pv[tid - 1], pf[tid - 1]});
-    uint32_t idx = blkoff[blockIdx.x] + ph[tid] - my;  // heads before this thread's chunk
+    const uint32_t g0 = blkoff[blockIdx.x];
+    uint32_t lidx = ph[tid] - my;  // the tile's heads before this thread's chunk
     const uint64_t jmask = (1ull << bj) - 1;
+#pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const int64_t e = a + r;
-        if (e >= n) break;
+        if (l0 + r >= nloc) break;
         const bool b = f[r] & 1;
-        run = seg_combine(run, SegSum{sw[cf_pad(l0 + r)], b ? 1 : 0});
+        run = seg_combine(run, SegSum{x[r], b ? 1 : 0});
         if (f[r] & 2) continue;  // sentinel
-        const bool last = e + 1 == n || (f[r + 1] & 1);
-        if (!(b || last)) continue;
-        const uint64_t k = keys[e];  // run heads and ends only
-        const int32_t i = (int32_t)(k >> bj), j = (int32_t)(k & jmask);
-        if (b) {
-            out_i[idx] = i;
-            out_j[idx] = j;
-            out_first[idx] = slots ? slots[vals[e]] : vals[e];
-            ++idx;
+        if (b) hpos[lidx++] = (uint16_t)(l0 + r);
+        const int64_t e = t0 + l0 + r;
+        if (e + 1 == n || (f[r + 1] & 1)) {  // last of the run: its sum
+            double v = run.v;
+            if (cnt) {
+                const uint64_t k = keys[e];
+                const int32_t i = (int32_t)(k >> bj), j = (int32_t)(k & jmask);
+                v = v / sqrt((double)(cnt[i] * cnt[j]));
+            }
+            if (lidx > 0) sw[lidx - 1] = v;  // sw's weights are all in registers by now
+            else out_v[(int64_t)g0 - 1] = v;  // the run began in an earlier tile
         }
-        if (last) {  // last of the run: its sum
-            const unsigned long long ci = cnt ? cnt[i] : 1ull, cj = cnt ? cnt[j] : 1ull;
-            out_v[idx - 1] = cnt ? run.v / sqrt((double)(ci * cj)) : run.v;
-        }
+    }
+    __syncthreads();
+    const uint32_t nh = ph[RS_THREADS - 1];
+    // the last head's sum is set here unless its run (the run of the tile's
+    // last key, not the sentinel) continues into the next tile
+    const bool tail_open = t0 + nloc < n && !(fl[nloc] & 1) && !(fl[nloc - 1] & 2);
+    for (uint32_t h = tid; h < nh; h += RS_THREADS) {
+        const int64_t e = t0 + hpos[h];
+        const uint64_t k = keys[e];
+        const int64_t g = (int64_t)g0 + h;
+        out_i[g] = (int32_t)(k >> bj);
+        out_j[g] = (int32_t)(k & jmask);
+        out_first[g] = slots ? slots[vals[e]] : vals[e];
+        if (!(tail_open && h + 1 == nh)) out_v[g] = sw[h];
     }
 }
 
@@ -584,6 +750,17 @@ __device__ __forceinline__ void cf_sort64(CfEnt& x) {
     }
 }
 
+// True when no lane of the (unsorted) chunk x beats the current n-th best
+// entry (n <= 64): such a chunk cannot change the top n, and is skipped
+// without its sort (round 6; in a long row almost every chunk after the
+// first few).  (score, first) is a strict total order, so the kept top n is
+// the same.
+__device__ __forceinline__ bool cf_prunable(const CfEnt& cur, const CfEnt& x, int n) {
+    const double ts = __shfl(cur.s, n - 1, WAVE);
+    const int64_t tf = __shfl(cur.f, n - 1, WAVE);
+    return !__any(cf_better(x.s, x.f, ts, tf));
+}
+
 __global__ __launch_bounds__(256) void cf_topn_kernel(const int64_t* __restrict__ row_off, int64_t n_rows,
                                                     const int32_t* __restrict__ cols,
                                                     const double* __restrict__ vals,
@@ -607,6 +784,7 @@ __global__ __launch_bounds__(256) void cf_topn_kernel(const int64_t* __restrict_
                 x.f = first[a + c0 + lane];
                 x.c = cols[a + c0 + lane];
             }
+            if (c0 > 0 && cf_prunable(cur, x, topn)) continue;
             cf_sort64(x);
             if (c0 == 0) {
                 cur = x;
@@ -670,7 +848,7 @@ __global__ __launch_bounds__(256) void rc_count_kernel(const int64_t* __restrict
 
 
 struct RcParams {
-    double loc_beta, created_alpha;
+    double loc_beta, created_alpha, ln_created;
     int topn, ke, bj;
 };
 
@@ -699,16 +877,20 @@ __global__ __launch_bounds__(256) void rc_cand_kernel(
         if (sl < 0) continue;
         const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
         int64_t c = cand_off[q];
-        if (L <= 64) {
-            // history of <= 64 clicks held one per lane (the in-history test
-            // is L shuffles, not L dependent loads); the (loc, neighbour)
-            // candidates of all history positions are flattened over the
-            // wave -- lane f takes flat candidate f0 + f, its position loc
-            // found by a binary search of the lane-scanned neighbour counts
-            // (a row has <= topn neighbours, so one position per pass would
-            // leave most lanes idle).  Same values, same slots c + f.
-            const int32_t hl = lane < L ? items[b + lane] : -1;
-            const int nl = lane < L ? nbr_cnt[hl] : 0;
+        // History positions in chunks of 64, one per lane; the (loc,
+        // neighbour) candidates of a chunk's positions are flattened over the
+        // wave -- lane f takes flat candidate f0 + f, its position found by a
+        // binary search of the lane-scanned neighbour counts (a row has <=
+        // topn neighbours, so one position per pass would leave most lanes
+        // idle).  The in-history test is shuffles over the history held one
+        // per lane (chunk by chunk past 64 clicks) -- round 5 walked histories
+        // longer than 64 by dependent loads, one position per pass, and its
+        // few 200-click users set the kernel's length.  Candidate slots are
+        // c + (loc, x) order, as the reference's walk.
+        const int32_t h0 = lane < L ? items[b + lane] : -1;  // the first 64 clicks
+        for (int64_t p0 = 0; p0 < L; p0 += 64) {
+            const int32_t hl = p0 == 0 ? h0 : (p0 + lane < L ? items[b + p0 + lane] : -1);
+            const int nl = p0 + lane < L ? nbr_cnt[hl] : 0;
             int inc = nl;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
@@ -717,7 +899,7 @@ __global__ __launch_bounds__(256) void rc_cand_kernel(
             }
             const int total = __shfl(inc, 63, 64);
             // position_weight(len(hist) - loc) (:92-95), lane loc
-            const double lwl = lane < L ? pow(prm.loc_beta, (double)(L - lane)) : 0.0;
+            const double lwl = p0 + lane < L ? pow(prm.loc_beta, (double)(L - p0 - lane)) : 0.0;
             for (int f0 = 0; f0 < total; f0 += 64) {  // uniform: the shuffles run converged
                 const int f = f0 + lane;
                 int loc = 0;
@@ -730,14 +912,19 @@ __global__ __launch_bounds__(256) void rc_cand_kernel(
                 const bool ok = f < total;
                 const int32_t j = ok ? nbr_cols[(int64_t)i * prm.topn + x] : -2;
                 bool inh = false;
-                for (int l = 0; l < (int)L; ++l) inh |= __shfl(hl, l, 64) == j;
+                for (int l = 0; l < (int)(L < 64 ? L : 64); ++l) inh |= __shfl(h0, l, 64) == j;
+                for (int64_t hc = 64; hc < L; hc += 64) {
+                    const int32_t hv = hc + lane < L ? items[b + hc + lane] : -1;
+                    const int nh = (int)(L - hc < 64 ? L - hc : 64);
+                    for (int l = 0; l < nh; ++l) inh |= __shfl(hv, l, 64) == j;
+                }
                 if (!ok) continue;
                 const double wij = nbr_vals[(int64_t)i * prm.topn + x];
                 uint64_t key = sentinel;
                 double v = 0.0;
                 if (!inh) {
                     // time_decay_weight(created_i, created_j) (:86-90)
-                    const double cw = exp(pow(prm.created_alpha, fabs(created[i] - created[j])));
+                    const double cw = exp(cf_apow(prm.created_alpha, prm.ln_created, fabs(created[i] - created[j])));
                     double content = 1.0;  // (:98-103)
                     if (prm.ke > 0) {
                         double e;
@@ -753,49 +940,26 @@ __global__ __launch_bounds__(256) void rc_cand_kernel(
                 vals[c + f] = (int32_t)(c + f);
                 contrib[c + f] = v;
             }
-            continue;
-        }
-        // long histories: one position per pass, the in-history test by loads
-        for (int64_t loc = 0; loc < L; ++loc) {
-            const int32_t i = items[b + loc];
-            const int n = nbr_cnt[i];
-            const double lw = pow(prm.loc_beta, (double)(L - loc));
-            for (int x = lane; x < n; x += 64) {
-                const int32_t j = nbr_cols[(int64_t)i * prm.topn + x];
-                bool inh = false;
-                for (int64_t l = 0; l < L && !inh; ++l) inh = items[b + l] == j;
-                const double wij = nbr_vals[(int64_t)i * prm.topn + x];
-                uint64_t key = sentinel;
-                double v = 0.0;
-                if (!inh) {
-                    const double cw = exp(pow(prm.created_alpha, fabs(created[i] - created[j])));
-                    double content = 1.0;
-                    if (prm.ke > 0) {
-                        double e;
-                        if (rc_find(emb_cols + (int64_t)i * prm.ke, emb_vals + (int64_t)i * prm.ke, emb_cnt[i], j, e))
-                            content += e;
-                        if (rc_find(emb_cols + (int64_t)j * prm.ke, emb_vals + (int64_t)j * prm.ke, emb_cnt[j], i, e))
-                            content += e;
-                    }
-                    v = cw * lw * content * wij;
-                    key = ((uint64_t)q << prm.bj) | (uint32_t)j;
-                }
-                keys[c + x] = key;
-                vals[c + x] = (int32_t)(c + x);
-                contrib[c + x] = v;
-            }
-            c += n;
+            c += total;
         }
     }
 }
 
-// lower bound of q in the emitted (q, j) run (sorted by q)
+// lower bound of q in the emitted (q, j) run (sorted by q), searched by the
+// whole wave 64 probes at a time: ~4 dependent rounds over millions of
+// entries where round 5's per-lane bisection made ~23 (the query's two
+// bounds were most of rc_topk's time).  Probes below q form a lane prefix.
 __device__ __forceinline__ int64_t rc_lower(const int32_t* __restrict__ oq, int64_t n, int64_t q) {
-    int64_t lo = 0, hi = n;
+    const int lane = threadIdx.x & 63;
+    int64_t lo = 0, hi = n;  // oq[< lo] < q <= oq[>= hi]
     while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)oq[mid] < q) lo = mid + 1;
-        else hi = mid;
+        const int64_t step = (hi - lo + 63) >> 6;
+        const int64_t p = lo + step * lane;
+        const int c = __popcll(__ballot(p < hi && (int64_t)oq[p] < q));
+        if (c == 0) break;  // oq[lo] >= q
+        const int64_t nhi = lo + step * c;
+        lo += step * (c - 1) + 1;
+        hi = nhi < hi ? nhi : hi;
     }
     return lo;
 }
@@ -852,6 +1016,7 @@ __global__ __launch_bounds__(256) void rc_topk_kernel(
                 x.f = ef[a + c0 + lane];
                 x.c = ej[a + c0 + lane];
             }
+            if (c0 > 0 && cf_prunable(cur, x, topk)) continue;
             merge(x, c0 == 0);
         }
         int64_t total = n;
@@ -951,6 +1116,7 @@ __global__ __launch_bounds__(1024) void cf_topn_heavy_kernel(const int64_t* __re
                 x.f = first[a + c0 + lane];
                 x.c = cols[a + c0 + lane];
             }
+            if (started && cf_prunable(cur, x, topn)) continue;
             cf_sort64(x);
             if (!started) cur = x;
             else merge_in(x);
@@ -1256,12 +1422,15 @@ int nrk_itemcf_sim(const int64_t* offsets, int64_t n_users, const int32_t* items
     const int nbits = 2 * bj;
     const uint64_t sentinel = (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
     (void)hipMemsetAsync(out_cnt, 0, sizeof(int64_t) * (size_t)n_items, s);
-    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha, cf_dt_zero(time_alpha)};
-    const int64_t ugrid = (n_users + 3) / 4;
+    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha, cf_dt_zero(time_alpha),
+                       cf_ln(time_alpha), cf_ln(created_alpha)};
+    const int64_t pgrid = (n_pairs + 4 * CF_CHUNK - 1) / (4 * CF_CHUNK);
+    if (n_users > 0 && n_pairs > 0)
+        cf_pairs_flat_kernel<<<(int)(pgrid < 8192 ? pgrid : 8192), 256, 0, s>>>(
+            offsets, n_users, items, ts, created, pair_off, 0, prm, bj, sentinel, w.ka, w.va, w.w);
     if (n_users > 0)
-        cf_pairs_kernel<<<(int)(ugrid < 65536 ? ugrid : 65536), 256, 0, s>>>(
-            offsets, n_users, items, ts, created, pair_off, 0, prm, bj, sentinel, w.ka, w.va, w.w,
-            reinterpret_cast<unsigned long long*>(out_cnt));
+        cf_item_count_kernel<<<1024, CF_CNT_THREADS, 0, s>>>(offsets, n_users, items,
+                                                             reinterpret_cast<unsigned long long*>(out_cnt));
     const int64_t n = n_pairs;
     const int nblk = (int)((n + RS_TILE - 1) / RS_TILE);
     uint64_t* kin = w.ka;
@@ -1375,7 +1544,7 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
     const int64_t n = n_cand;
     const int nblk = (int)((n + RS_TILE - 1) / RS_TILE);
     if (n > 0) {
-        const RcParams prm{loc_beta, created_alpha, topn, ke, bj};
+        const RcParams prm{loc_beta, created_alpha, cf_ln(created_alpha), topn, ke, bj};
         rc_cand_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created,
                                           emb_cols, emb_vals, emb_cnt, prm, cand_off, sentinel, w.sort.ka,
                                           w.sort.va, w.sort.w);
@@ -1439,11 +1608,14 @@ int nrk_itemcf_pairs(const int64_t* offsets, int64_t n_users, const int32_t* ite
     const int bj = bits_for(n_items);
     const int nbits = 2 * bj;
     const uint64_t sentinel = (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
-    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha, cf_dt_zero(time_alpha)};
-    const int64_t ugrid = (n_users + 3) / 4;
-    cf_pairs_kernel<<<(int)(ugrid < 65536 ? ugrid : 65536), 256, 0, as_stream(stream)>>>(
-        offsets, n_users, items, ts, created, pair_off, slot_base, prm, bj, sentinel, keys, slots, w,
-        reinterpret_cast<unsigned long long*>(item_cnt));
+    const CfParams prm{loc_alpha, loc_alpha_rev, loc_beta, time_alpha, created_alpha, cf_dt_zero(time_alpha),
+                       cf_ln(time_alpha), cf_ln(created_alpha)};
+    // (the pair count lives on the device, pair_off[n_users]: a fixed
+    // persistent grid walks it)
+    cf_pairs_flat_kernel<<<2048, 256, 0, as_stream(stream)>>>(
+        offsets, n_users, items, ts, created, pair_off, slot_base, prm, bj, sentinel, keys, slots, w);
+    cf_item_count_kernel<<<1024, CF_CNT_THREADS, 0, as_stream(stream)>>>(
+        offsets, n_users, items, reinterpret_cast<unsigned long long*>(item_cnt));
     NRK_CHECK_LAUNCH();
     return NRK_OK;
 }
