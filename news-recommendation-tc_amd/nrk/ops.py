@@ -53,11 +53,12 @@ def _finite(t, name):
 
 
 # ------------------------------------------------------------------ tower --
-def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1, validate: bool = True):
+def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1, validate: bool = True, out=None):
     """YoutubeDNN user tower + re-normalisation (youtubednn_recaller.py:129-178, :467-470).
     ``validate`` checks hist_len against [0, T] (two device syncs); a caller
     that re-runs the tower on inputs it already validated (the bench's timed
-    steps) may pass False."""
+    steps) may pass False.  ``out``: a preallocated fp32 [n, w1 rows] output
+    (a pipelining caller's double buffer)."""
     _dev(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1)
     n, T = hist.shape
     D = user_table.shape[1]
@@ -73,7 +74,13 @@ def tt_user_fwd(user_table, item_table, uid, hist, hist_len, w0, b0, w1, b1, val
     _need(b1, torch.float32, (h1,), "b1")
     if validate and n and (int(hist_len.min()) < 0 or int(hist_len.max()) > T):
         raise ValueError("hist_len out of [0, T]")
-    out = torch.empty((n, h1), dtype=torch.float32, device=uid.device)
+    if out is None:
+        out = torch.empty((n, h1), dtype=torch.float32, device=uid.device)
+    else:
+        _dev(out)
+        _need(out, torch.float32, (n, h1), "out")
+        if not out.is_contiguous():
+            raise ValueError("out must be contiguous")
     _lib.call("nrk_tt_user_fwd", _ptr(user_table), user_table.shape[0], _ptr(item_table),
               item_table.shape[0], D, _ptr(uid), _ptr(hist), _ptr(hist_len), n, T,
               _ptr(w0), _ptr(b0), h0, _ptr(w1), _ptr(b1), h1, _ptr(out), _stream())
