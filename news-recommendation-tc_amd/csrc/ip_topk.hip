@@ -1650,7 +1650,27 @@ __global__ void ip_all_exact_kernel(int64_t n_users, int32_t* __restrict__ cand_
 __device__ __forceinline__ double exact_dot(const float* __restrict__ a, const float* __restrict__ b,
                                             int dim) {
     double s = 0.0;
-    if ((dim & 3) == 0) {
+    if ((dim & 31) == 0) {
+        // 8 float4 of both rows in flight per step (a runtime-dim loop
+        // otherwise waits on each row piece in turn); same sequential order
+        const float4* a4 = reinterpret_cast<const float4*>(a);
+        const float4* b4 = reinterpret_cast<const float4*>(b);
+        for (int t0 = 0; t0 < dim / 4; t0 += 8) {
+            float4 x[8], y[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                x[t] = a4[t0 + t];
+                y[t] = b4[t0 + t];
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                s += (double)x[t].x * (double)y[t].x;
+                s += (double)x[t].y * (double)y[t].y;
+                s += (double)x[t].z * (double)y[t].z;
+                s += (double)x[t].w * (double)y[t].w;
+            }
+        }
+    } else if ((dim & 3) == 0) {
         const float4* a4 = reinterpret_cast<const float4*>(a);
         const float4* b4 = reinterpret_cast<const float4*>(b);
         for (int t = 0; t < dim / 4; ++t) {
@@ -1695,7 +1715,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ?
     int64_t src_users = 0, int x_cap = 0, const int32_t* __restrict__ src_cnt = nullptr) {
     constexpr int SE = SV / WAVE;
     __shared__ Cand surv[4][SV];
-    __shared__ int32_t krow[DS4 > 0 ? 4 : 1][DS4 > 0 ? IP_KRING : 1];
+    __shared__ int32_t krow[4][IP_KRING];
     constexpr int RS = DS4 + 1;  // staged row stride in float4 (one float4 of padding)
     __shared__ float4 stage[DS4 > 0 ? 4 : 1][DS4 > 0 ? 32 * RS : 1];  // half a round (32 rows) at a time
     __shared__ uint32_t bandq[4][SV + 32 > IP_BQ ? SV + 32 : IP_BQ];
@@ -1989,10 +2009,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ?
             for (int d = lane; d < dpc; d += WAVE) ushl[wave][d] = d < dim ? (float)(_Float16)(uv[d] * s2) : 0.0f;
             wave_sync_lds();
         }
+        // items reaching the cut wait in the krow ring; whole 64-row exact
+        // rounds drain it (round 6: the exact dot ran inside each 64-item
+        // prefilter round, so a round with one kept lane paid a whole
+        // sequential fp64 row chain -- dim 128's refine: ~8 chains per user)
+        int kc = 0, ko = 0;
+        auto exact_generic = [&](int m) {
+            const int32_t rl = lane < m ? krow[wave][(ko + lane) & (IP_KRING - 1)] : -1;
+            double sd = 0.0;
+            bool keep = false;
+            if (rl >= 0) {
+                sd = exact_dot(uv, items + (int64_t)rl * dim, dim);
+                keep = sd >= thr;
+            }
+            push(keep, sd, rl);
+            ko += m;
+        };
         for (int base = 0; base < nitem; base += WAVE) {
             const int idx = base + lane;
             bool keep = false;
-            double sd = 0.0;
             int32_t row = 0;
             if (idx < nitem) {
                 const int bb = idx >> 4, r = idx & 15;
@@ -2016,13 +2051,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ?
                     }
                     keep = acc >= pcut;
                 }
-                if (keep) {
-                    sd = exact_dot(uv, items + (int64_t)row * dim, dim);
-                    keep = sd >= thr;
-                }
             }
-            push(keep, sd, row);
+            const unsigned long long bal = __ballot(keep);
+            if (keep) krow[wave][(kc + __popcll(bal & ((1ull << lane) - 1ull))) & (IP_KRING - 1)] = row;
+            kc += __popcll(bal);
+            wave_sync_lds();
+            while (kc - ko >= WAVE) exact_generic(WAVE);
         }
+        while (kc > ko) exact_generic(kc - ko < WAVE ? kc - ko : WAVE);
     }
     if (cnt > SV) {  // dense exact ties: hand the user to the exact fallback
         if (lane == 0) ovf_list[atomicAdd(ovf_count, 1)] = (int32_t)u;
