@@ -300,21 +300,23 @@ __global__ __launch_bounds__(256) void cf_pairs_flat_kernel(
 // counts is digit-major [256][nblk] so each digit's row scans contiguously.
 __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const uint64_t* __restrict__ keys, int64_t n,
                                                         int shift, int nblk,
-                                                        uint32_t* __restrict__ counts) {
+                                                        uint32_t* __restrict__ counts,
+                                                        const int64_t* __restrict__ n_dev = nullptr) {
+    if (n_dev) n = *n_dev;  // the count on the device (rc_query_kernel's overflow), nblk its bound
+    if ((int64_t)blockIdx.x * RS_TILE >= n && n_dev) {  // past the end: an empty tile
+        counts[(size_t)threadIdx.x * nblk + blockIdx.x] = 0;
+        return;
+    }
     __shared__ uint32_t hist[256];
     const int tid = threadIdx.x;
     hist[tid] = 0;
     __syncthreads();
     const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
-    uint32_t dr[RS_ITEMS];
-#pragma unroll
+#pragma unroll 4
     for (int r = 0; r < RS_ITEMS; ++r) {
         const int64_t e = t0 + r * RS_THREADS + tid;
-        dr[r] = e < n ? (uint32_t)(keys[e] >> shift) & 255u : 256u;
+        if (e < n) atomicAdd(&hist[(keys[e] >> shift) & 255], 1u);
     }
-#pragma unroll
-    for (int r = 0; r < RS_ITEMS; ++r)
-        if (dr[r] < 256u) atomicAdd(&hist[dr[r]], 1u);
     __syncthreads();
     counts[(size_t)tid * nblk + blockIdx.x] = hist[tid];
 }
@@ -361,7 +363,9 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(
     const uint64_t* __restrict__ kin, const int32_t* __restrict__ vin, uint64_t* __restrict__ kout,
     int32_t* __restrict__ vout, int64_t n, int shift, int nblk, const uint32_t* __restrict__ counts,
-    const uint32_t* __restrict__ totals) {
+    const uint32_t* __restrict__ totals, const int64_t* __restrict__ n_dev = nullptr) {
+    if (n_dev) n = *n_dev;
+    if ((int64_t)blockIdx.x * RS_TILE >= n) return;  // an empty tile writes nothing
     __shared__ uint64_t sk[RS_TILE];
     __shared__ int32_t sv[RS_TILE];
     __shared__ uint32_t base[256];    // global start of digit d minus its tile-local start
@@ -507,7 +511,16 @@ __device__ __forceinline__ void cf_chunk_flags(const uint8_t* fl, int l0, uint8_
 __global__ __launch_bounds__(RS_THREADS) void cf_tile_reduce(
     const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, const double* __restrict__ w,
     int64_t n, uint64_t sentinel, uint32_t* __restrict__ blkcnt, double* __restrict__ tail,
-    int32_t* __restrict__ brk, double* __restrict__ ws) {
+    int32_t* __restrict__ brk, double* __restrict__ ws, const int64_t* __restrict__ n_dev = nullptr) {
+    if (n_dev) n = *n_dev;
+    if ((int64_t)blockIdx.x * RS_TILE >= n) {  // an empty tile: no heads, no sum, no break
+        if (threadIdx.x == 0) {
+            tail[blockIdx.x] = 0.0;
+            brk[blockIdx.x] = 0;
+            blkcnt[blockIdx.x] = 0;
+        }
+        return;
+    }
     __shared__ __attribute__((aligned(16))) uint8_t fl[CF_FL];
     __shared__ double sw[CF_SW];
     __shared__ double tv[RS_THREADS];
@@ -623,7 +636,9 @@ __global__ __launch_bounds__(RS_THREADS) void cf_emit(
     int64_t n, uint64_t sentinel, const uint32_t* __restrict__ blkoff, const double* __restrict__ carry,
     const unsigned long long* __restrict__ cnt, const int32_t* __restrict__ slots, int bj,
     int32_t* __restrict__ out_i, int32_t* __restrict__ out_j, double* __restrict__ out_v,
-    int64_t* __restrict__ out_first) {
+    int64_t* __restrict__ out_first, const int64_t* __restrict__ n_dev = nullptr) {
+    if (n_dev) n = *n_dev;
+    if ((int64_t)blockIdx.x * RS_TILE >= n) return;
     __shared__ __attribute__((aligned(16))) uint8_t fl[CF_FL];
     __shared__ double sw[CF_SW];  // the sorted weights, then the heads' sums
     __shared__ uint16_t hpos[RS_TILE];
@@ -725,10 +740,16 @@ __device__ __forceinline__ bool cf_better(double as, int64_t af, double bs, int6
     return as > bs || (as == bs && af < bf);
 }
 
-__device__ __forceinline__ void cf_cmpx(CfEnt& x, int j, bool keep_better) {
-    const double ys = __shfl_xor(x.s, j, WAVE);
-    const int64_t yf = __shfl_xor(x.f, j, WAVE);
-    const int32_t yc = __shfl_xor(x.c, j, WAVE);
+// compare-exchange with lane ^ J through lane_xor (DPP / ds_swizzle /
+// permlane swaps; round 6: __shfl_xor's ds_bpermute made these sorts most of
+// the top-n and recall kernels' LDS instructions)
+template <int J>
+__device__ __forceinline__ void cf_cmpx(CfEnt& x, bool keep_better) {
+    const double ys = lane_xor_f64<J>(x.s);
+    const uint64_t fb = (uint64_t)x.f;
+    const int64_t yf =
+        (int64_t)(((uint64_t)lane_xor<J>((uint32_t)(fb >> 32)) << 32) | (uint64_t)lane_xor<J>((uint32_t)fb));
+    const int32_t yc = (int32_t)lane_xor<J>((uint32_t)x.c);
     const bool xb = cf_better(x.s, x.f, ys, yf);
     if (keep_better != xb) {
         x.s = ys;
@@ -739,15 +760,24 @@ __device__ __forceinline__ void cf_cmpx(CfEnt& x, int j, bool keep_better) {
 
 __device__ __forceinline__ void cf_sort64(CfEnt& x) {
     const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
+    static_for<6>([&](auto klc) {
+        constexpr int k = 2 << decltype(klc)::value;
+        static_for<decltype(klc)::value + 1>([&](auto jc) {
+            constexpr int j = (k >> 1) >> decltype(jc)::value;
             const bool lower = (lane & j) == 0;
             const bool up = (lane & k) == 0;
-            cf_cmpx(x, j, lower == up);
-        }
-    }
+            cf_cmpx<j>(x, lower == up);
+        });
+    });
+}
+
+// the bitonic clean of a 64-entry bitonic sequence, best first
+__device__ __forceinline__ void cf_clean64(CfEnt& x) {
+    const int lane = threadIdx.x & 63;
+    static_for<6>([&](auto jc) {
+        constexpr int j = 32 >> decltype(jc)::value;
+        cf_cmpx<j>(x, (lane & j) == 0);
+    });
 }
 
 // True when no lane of the (unsorted) chunk x beats the current n-th best
@@ -798,8 +828,7 @@ __global__ __launch_bounds__(256) void cf_topn_kernel(const int64_t* __restrict_
                     cur.f = yf;
                     cur.c = yc;
                 }
-#pragma unroll
-                for (int j = 32; j > 0; j >>= 1) cf_cmpx(cur, j, (lane & j) == 0);
+                cf_clean64(cur);
             }
         }
         const int64_t m = n < topn ? n : topn;
@@ -816,18 +845,24 @@ __global__ __launch_bounds__(256) void cf_topn_kernel(const int64_t* __restrict_
 // ItemCFRecaller.recall (itemcf_recaller.py:56-129) for a batch of query
 // users.  The reference accumulates item_rank[j] += w over (loc, x) -- the
 // history position and the rank in item i's top-n list -- and breaks score
-// ties by dict insertion order.  Every candidate (q, loc, x) gets a global
-// sequence number c = cand_off[q] + (position in that walk), so the same
-// stable (key, c) radix sort + ordered segment sums as the similarity pass
-// reproduce the reference's sums and first-encounter order exactly:
+// ties by dict insertion order.  Every candidate (q, loc, x) gets a sequence
+// number c = cand_off[q] + (position in that walk):
 //   rc_count / rc_scan   C_q = sum_loc nbr_cnt[items[loc]], exclusive offsets;
 //   rc_cand              one wave per query: key (q << bj | j) (sentinel for
-//                        j in the history), c, and the contribution
+//                        j in the history), c and the contribution
 //                        exp(alpha^|ct_i - ct_j|) * beta^(L - loc) * content * w_ij;
-//   radix sort + cf_emit (q, j, score, first c) per distinct key;
-//   rc_topk              one wave per query: hot-item fill while fewer than
-//                        topk entries (:116-122), then the top-k by
-//                        (score desc, insertion order asc), as sorted(...)[:topk].
+//   rc_query             (topk <= 64, C_q <= RC_CAP; round 6) one wave per
+//                        query: a register sort by (j, walk position), per-j
+//                        sums in walk order, top-k and the hot fill
+//                        (rc_finish_query);
+//   the radix path       (the larger queries, listed by rc_query and
+//                        compacted; every query when topk > 64) the stable
+//                        (key, c) radix sort + ordered segment sums
+//                        of the similarity pass, cf_emit (q, j, score, first
+//                        c) per distinct key; rc_topk: one wave per query, the
+//                        hot-item fill while fewer than topk entries
+//                        (:116-122), then the top-k by (score desc, insertion
+//                        order asc), as sorted(...)[:topk].
 __global__ __launch_bounds__(256) void rc_count_kernel(const int64_t* __restrict__ q_slot, int64_t nq,
                                                        const int64_t* __restrict__ offsets,
                                                        const int32_t* __restrict__ items,
@@ -862,6 +897,82 @@ __device__ __forceinline__ bool rc_find(const int32_t* __restrict__ cols, const 
     return false;
 }
 
+// One query's candidates in the reference's walk order (loc, x), handed to
+// sink(f, inh, j, v) for every flat candidate f < C_q (inh: j is in the
+// history -> no item_rank entry).  History positions in chunks of 64, one
+// per lane; the (loc, neighbour) candidates of a chunk's positions are
+// flattened over the wave -- lane f takes flat candidate f0 + f, its position
+// found by a binary search of the lane-scanned neighbour counts (a row has <=
+// topn neighbours, so one position per pass would leave most lanes idle).
+// The in-history test is shuffles over the history held one per lane (chunk
+// by chunk past 64 clicks) -- round 5 walked histories longer than 64 by
+// dependent loads, one position per pass, and its few 200-click users set
+// the kernel's length.
+template <class Sink>
+__device__ __forceinline__ void rc_gen_query(int64_t b, int64_t L, const int32_t* __restrict__ items,
+                                             const int32_t* __restrict__ nbr_cols,
+                                             const double* __restrict__ nbr_vals,
+                                             const int32_t* __restrict__ nbr_cnt, const double* __restrict__ created,
+                                             const int32_t* __restrict__ emb_cols,
+                                             const double* __restrict__ emb_vals,
+                                             const int32_t* __restrict__ emb_cnt, const RcParams& prm, Sink&& sink) {
+    const int lane = threadIdx.x & 63;
+    int64_t c = 0;
+    const int32_t h0 = lane < L ? items[b + lane] : -1;  // the first 64 clicks
+    for (int64_t p0 = 0; p0 < L; p0 += 64) {
+        const int32_t hl = p0 == 0 ? h0 : (p0 + lane < L ? items[b + p0 + lane] : -1);
+        const int nl = p0 + lane < L ? nbr_cnt[hl] : 0;
+        int inc = nl;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += t;
+        }
+        const int total = __shfl(inc, 63, 64);
+        // position_weight(len(hist) - loc) (:92-95), lane loc
+        const double lwl = p0 + lane < L ? pow(prm.loc_beta, (double)(L - p0 - lane)) : 0.0;
+        for (int f0 = 0; f0 < total; f0 += 64) {  // uniform: the shuffles run converged
+            const int f = f0 + lane;
+            int loc = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (__shfl(inc, loc + step - 1, 64) <= f) loc += step;
+            const int32_t i = __shfl(hl, loc, 64);
+            const int x = f - (__shfl(inc, loc, 64) - __shfl(nl, loc, 64));
+            const double lw = __shfl(lwl, loc, 64);
+            const bool ok = f < total;
+            const int32_t j = ok ? nbr_cols[(int64_t)i * prm.topn + x] : -2;
+            bool inh = false;
+            for (int l = 0; l < (int)(L < 64 ? L : 64); ++l) inh |= __shfl(h0, l, 64) == j;
+            for (int64_t hc = 64; hc < L; hc += 64) {
+                const int32_t hv = hc + lane < L ? items[b + hc + lane] : -1;
+                const int nh = (int)(L - hc < 64 ? L - hc : 64);
+                for (int l = 0; l < nh; ++l) inh |= __shfl(hv, l, 64) == j;
+            }
+            if (!ok) continue;
+            const double wij = nbr_vals[(int64_t)i * prm.topn + x];
+            double v = 0.0;
+            if (!inh) {
+                // time_decay_weight(created_i, created_j) (:86-90)
+                const double cw = exp(cf_apow(prm.created_alpha, prm.ln_created, fabs(created[i] - created[j])));
+                double content = 1.0;  // (:98-103)
+                if (prm.ke > 0) {
+                    double e;
+                    if (rc_find(emb_cols + (int64_t)i * prm.ke, emb_vals + (int64_t)i * prm.ke, emb_cnt[i], j, e))
+                        content += e;
+                    if (rc_find(emb_cols + (int64_t)j * prm.ke, emb_vals + (int64_t)j * prm.ke, emb_cnt[j], i, e))
+                        content += e;
+                }
+                v = cw * lw * content * wij;
+            }
+            sink(c + f, inh, j, v);
+        }
+        c += total;
+    }
+}
+
+// Every query's candidates to global memory at cand_off[q]: key (q << bj |
+// j) or the sentinel, the global slot, the contribution.
 __global__ __launch_bounds__(256) void rc_cand_kernel(
     const int64_t* __restrict__ q_slot, int64_t nq, const int64_t* __restrict__ offsets,
     const int32_t* __restrict__ items, const int32_t* __restrict__ nbr_cols,
@@ -870,78 +981,18 @@ __global__ __launch_bounds__(256) void rc_cand_kernel(
     const double* __restrict__ emb_vals, const int32_t* __restrict__ emb_cnt, RcParams prm,
     const int64_t* __restrict__ cand_off, uint64_t sentinel, uint64_t* __restrict__ keys,
     int32_t* __restrict__ vals, double* __restrict__ contrib) {
-    const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4;
     for (int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); q < nq; q += nw) {
         const int64_t sl = q_slot[q];
         if (sl < 0) continue;
         const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
-        int64_t c = cand_off[q];
-        // History positions in chunks of 64, one per lane; the (loc,
-        // neighbour) candidates of a chunk's positions are flattened over the
-        // wave -- lane f takes flat candidate f0 + f, its position found by a
-        // binary search of the lane-scanned neighbour counts (a row has <=
-        // topn neighbours, so one position per pass would leave most lanes
-        // idle).  The in-history test is shuffles over the history held one
-        // per lane (chunk by chunk past 64 clicks) -- round 5 walked histories
-        // longer than 64 by dependent loads, one position per pass, and its
-        // few 200-click users set the kernel's length.  Candidate slots are
-        // c + (loc, x) order, as the reference's walk.
-        const int32_t h0 = lane < L ? items[b + lane] : -1;  // the first 64 clicks
-        for (int64_t p0 = 0; p0 < L; p0 += 64) {
-            const int32_t hl = p0 == 0 ? h0 : (p0 + lane < L ? items[b + p0 + lane] : -1);
-            const int nl = p0 + lane < L ? nbr_cnt[hl] : 0;
-            int inc = nl;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int t = __shfl_up(inc, d, 64);
-                if (lane >= d) inc += t;
-            }
-            const int total = __shfl(inc, 63, 64);
-            // position_weight(len(hist) - loc) (:92-95), lane loc
-            const double lwl = p0 + lane < L ? pow(prm.loc_beta, (double)(L - p0 - lane)) : 0.0;
-            for (int f0 = 0; f0 < total; f0 += 64) {  // uniform: the shuffles run converged
-                const int f = f0 + lane;
-                int loc = 0;
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (__shfl(inc, loc + step - 1, 64) <= f) loc += step;
-                const int32_t i = __shfl(hl, loc, 64);
-                const int x = f - (__shfl(inc, loc, 64) - __shfl(nl, loc, 64));
-                const double lw = __shfl(lwl, loc, 64);
-                const bool ok = f < total;
-                const int32_t j = ok ? nbr_cols[(int64_t)i * prm.topn + x] : -2;
-                bool inh = false;
-                for (int l = 0; l < (int)(L < 64 ? L : 64); ++l) inh |= __shfl(h0, l, 64) == j;
-                for (int64_t hc = 64; hc < L; hc += 64) {
-                    const int32_t hv = hc + lane < L ? items[b + hc + lane] : -1;
-                    const int nh = (int)(L - hc < 64 ? L - hc : 64);
-                    for (int l = 0; l < nh; ++l) inh |= __shfl(hv, l, 64) == j;
-                }
-                if (!ok) continue;
-                const double wij = nbr_vals[(int64_t)i * prm.topn + x];
-                uint64_t key = sentinel;
-                double v = 0.0;
-                if (!inh) {
-                    // time_decay_weight(created_i, created_j) (:86-90)
-                    const double cw = exp(cf_apow(prm.created_alpha, prm.ln_created, fabs(created[i] - created[j])));
-                    double content = 1.0;  // (:98-103)
-                    if (prm.ke > 0) {
-                        double e;
-                        if (rc_find(emb_cols + (int64_t)i * prm.ke, emb_vals + (int64_t)i * prm.ke, emb_cnt[i], j, e))
-                            content += e;
-                        if (rc_find(emb_cols + (int64_t)j * prm.ke, emb_vals + (int64_t)j * prm.ke, emb_cnt[j], i, e))
-                            content += e;
-                    }
-                    v = cw * lw * content * wij;
-                    key = ((uint64_t)q << prm.bj) | (uint32_t)j;
-                }
-                keys[c + f] = key;
-                vals[c + f] = (int32_t)(c + f);
-                contrib[c + f] = v;
-            }
-            c += total;
-        }
+        const int64_t c = cand_off[q];
+        rc_gen_query(b, L, items, nbr_cols, nbr_vals, nbr_cnt, created, emb_cols, emb_vals, emb_cnt, prm,
+                     [&](int64_t f, bool inh, int32_t j, double v) {
+                         keys[c + f] = inh ? sentinel : (((uint64_t)q << prm.bj) | (uint32_t)j);
+                         vals[c + f] = (int32_t)(c + f);
+                         contrib[c + f] = v;
+                     });
     }
 }
 
@@ -964,116 +1015,332 @@ __device__ __forceinline__ int64_t rc_lower(const int32_t* __restrict__ oq, int6
     return lo;
 }
 
+// The end of one query's recall (itemcf_recaller.py:116-129): the top-k
+// (k <= 64) of its distinct candidates by (score desc, first slot asc) --
+// chunk(c0) gives each lane its entry of positions [c0, c0 + 64) of a source
+// of nsrc positions (or c = -1: none there) -- then the hot-item fill while
+// fewer than topk (:116-122; in_cands(h): h is one of the candidates, only
+// asked when there are some), then the output row.
+template <class Chunk, class InCands>
+__device__ __forceinline__ void rc_finish_query(int64_t q, int64_t nsrc, Chunk&& chunk, InCands&& in_cands,
+                                                int64_t b, int64_t L, const int32_t* __restrict__ items,
+                                                const int32_t* __restrict__ hot, int n_hot, int topk,
+                                                int32_t* __restrict__ out_items, double* __restrict__ out_scores,
+                                                int32_t* __restrict__ out_src, int32_t* __restrict__ out_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t HOT_FIRST = (int64_t)1 << 62;  // after every candidate (insertion order)
+    CfEnt cur{-INFINITY, INT64_MAX, -1};
+    bool started = false;
+    auto merge = [&](CfEnt x) {
+        cf_sort64(x);
+        if (!started) {
+            cur = x;
+            started = true;
+            return;
+        }
+        const double ys = __shfl(x.s, 63 - lane, WAVE);
+        const int64_t yf = __shfl(x.f, 63 - lane, WAVE);
+        const int32_t yc = __shfl(x.c, 63 - lane, WAVE);
+        if (cf_better(ys, yf, cur.s, cur.f)) {
+            cur.s = ys;
+            cur.f = yf;
+            cur.c = yc;
+        }
+        cf_clean64(cur);
+    };
+    int64_t n = 0;  // distinct candidates
+    for (int64_t c0 = 0; c0 < nsrc; c0 += 64) {
+        const CfEnt x = chunk(c0);
+        n += __popcll(__ballot(x.c >= 0));
+        if (started && cf_prunable(cur, x, topk)) continue;
+        merge(x);
+    }
+    int64_t total = n;
+    if (n < topk) {
+        // fill with popular items not yet ranked and not in the history,
+        // scored -x - 100, until topk entries (:116-122)
+        int need = (int)(topk - n);
+        CfEnt hx{-INFINITY, INT64_MAX, -1};
+        int got = 0;
+        for (int x0 = 0; x0 < n_hot && need > 0; x0 += 64) {
+            const int x = x0 + lane;
+            bool ok = false;
+            int32_t h = -1;
+            if (x < n_hot) {
+                h = hot[x];
+                ok = true;
+                for (int64_t l = 0; l < L && ok; ++l) ok = items[b + l] != h;
+                if (ok && n > 0) ok = !in_cands(h);
+            }
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(ok);
+            const int take = __builtin_popcountll(bal) < need ? __builtin_popcountll(bal) : need;
+            // the first `take' accepted entries, in hot order, into hx lanes
+            // got ..: lane got + t takes the t-th set bit of bal (the smallest
+            // p with t + 1 set bits in [0, p], by bisection)
+            const int t = lane - got;
+            int src = 0;
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1)
+                if (__builtin_popcountll(bal & ((2ull << (src + st - 1)) - 1ull)) < t + 1) src += st;
+            const int32_t hv = __shfl(h, src, WAVE);
+            if (t >= 0 && t < take) {
+                hx.s = (double)(-(x0 + src) - 100);
+                hx.f = HOT_FIRST + x0 + src;
+                hx.c = hv;
+            }
+            got += take;
+            need -= take;
+        }
+        total += got;
+        if (got > 0) merge(hx);
+    }
+    const int64_t m = total < topk ? total : topk;
+    if (lane < topk) {
+        const bool ok = lane < m;
+        out_items[q * topk + lane] = ok ? cur.c : -1;
+        out_scores[q * topk + lane] = ok ? cur.s : 0.0;
+        out_src[q * topk + lane] = ok ? (cur.f >= HOT_FIRST ? 1 : 0) : -1;
+    }
+    if (lane == 0) out_cnt[q] = (int32_t)m;
+}
+
+// cold start: [(hot[i], -i) for i < topk] (:68-70)
+__device__ __forceinline__ void rc_cold(int64_t q, const int32_t* __restrict__ hot, int n_hot, int topk,
+                                        int32_t* __restrict__ out_items, double* __restrict__ out_scores,
+                                        int32_t* __restrict__ out_src, int32_t* __restrict__ out_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int m = n_hot < topk ? n_hot : topk;
+    if (lane < topk) {
+        out_items[q * topk + lane] = lane < m ? hot[lane] : -1;
+        out_scores[q * topk + lane] = lane < m ? -(double)lane : 0.0;
+        out_src[q * topk + lane] = lane < m ? 2 : -1;
+    }
+    if (lane == 0) out_cnt[q] = m;
+}
+
+// The radix path's top-k: one wave per query over its emitted (q, j) run
+// (every query, or the *qcount listed ones).
 __global__ __launch_bounds__(256) void rc_topk_kernel(
     const int64_t* __restrict__ q_slot, int64_t nq, const int64_t* __restrict__ offsets,
     const int32_t* __restrict__ items, const int32_t* __restrict__ hot, int n_hot,
     const int32_t* __restrict__ eq, const int32_t* __restrict__ ej, const double* __restrict__ ev,
     const int64_t* __restrict__ ef, const int64_t* __restrict__ n_emit, int topk,
     int32_t* __restrict__ out_items, double* __restrict__ out_scores, int32_t* __restrict__ out_src,
-    int32_t* __restrict__ out_cnt) {
-    const int lane = threadIdx.x & 63;
+    int32_t* __restrict__ out_cnt, const int2* __restrict__ qlist = nullptr,
+    const int32_t* __restrict__ qcount = nullptr) {
     const int64_t nw = (int64_t)gridDim.x * 4;
     const int64_t ne = *n_emit;
-    const int64_t HOT_FIRST = (int64_t)1 << 62;  // after every candidate (insertion order)
-    for (int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); q < nq; q += nw) {
+    const int64_t nl = qlist ? (int64_t)*qcount : nq;
+    for (int64_t iq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); iq < nl; iq += nw) {
+        const int64_t q = qlist ? (int64_t)qlist[iq].x : iq;
         const int64_t sl = q_slot[q];
-        int32_t* oi = out_items + q * topk;
-        double* os = out_scores + q * topk;
-        int32_t* osrc = out_src + q * topk;
-        if (sl < 0) {  // cold start: [(hot[i], -i) for i < topk] (:68-70)
-            const int m = n_hot < topk ? n_hot : topk;
-            if (lane < topk) {
-                oi[lane] = lane < m ? hot[lane] : -1;
-                os[lane] = lane < m ? -(double)lane : 0.0;
-                osrc[lane] = lane < m ? 2 : -1;
-            }
-            if (lane == 0) out_cnt[q] = m;
+        if (sl < 0) {
+            rc_cold(q, hot, n_hot, topk, out_items, out_scores, out_src, out_cnt);
             continue;
         }
-        const int64_t a = rc_lower(eq, ne, q), e = rc_lower(eq, ne, q + 1), n = e - a;
-        CfEnt cur{-INFINITY, INT64_MAX, -1};
-        auto merge = [&](CfEnt x, bool first_chunk) {
-            cf_sort64(x);
-            if (first_chunk) {
-                cur = x;
-                return;
-            }
-            const double ys = __shfl(x.s, 63 - lane, WAVE);
-            const int64_t yf = __shfl(x.f, 63 - lane, WAVE);
-            const int32_t yc = __shfl(x.c, 63 - lane, WAVE);
-            if (cf_better(ys, yf, cur.s, cur.f)) {
-                cur.s = ys;
-                cur.f = yf;
-                cur.c = yc;
-            }
+        const int64_t a = rc_lower(eq, ne, q), e = rc_lower(eq, ne, q + 1);
+        const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
+        rc_finish_query(
+            q, e - a,
+            [&](int64_t c0) {
+                const int64_t i = a + c0 + (threadIdx.x & 63);
+                return i < e ? CfEnt{ev[i], ef[i], ej[i]} : CfEnt{-INFINITY, INT64_MAX, -1};
+            },
+            [&](int32_t h) {  // binary search in the query's candidate js (sorted)
+                int64_t lo = a, hi = e;
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (ej[mid] < h) lo = mid + 1;
+                    else hi = mid;
+                }
+                return lo < e && ej[lo] == h;
+            },
+            b, L, items, hot, n_hot, topk, out_items, out_scores, out_src, out_cnt);
+    }
+}
+
+// lane ^ stride's key (stride < 64, a constant once the sort below is
+// unrolled: lane_xor's DPP / swizzle / permlane forms)
+__device__ __forceinline__ uint64_t lane_xor_u64(uint64_t v, int stride) {
+    auto x = [&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        return ((uint64_t)lane_xor<J>((uint32_t)(v >> 32)) << 32) | (uint64_t)lane_xor<J>((uint32_t)v);
+    };
+    switch (stride) {
+        case 1: return x(std::integral_constant<int, 1>{});
+        case 2: return x(std::integral_constant<int, 2>{});
+        case 4: return x(std::integral_constant<int, 4>{});
+        case 8: return x(std::integral_constant<int, 8>{});
+        case 16: return x(std::integral_constant<int, 16>{});
+        default: return x(std::integral_constant<int, 32>{});
+    }
+}
+
+// ascending bitonic sort of 64 E keys, key e * 64 + lane in k[e]
+template <int E>
+__device__ __forceinline__ void wave_sort_u64(uint64_t (&k)[E]) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-            for (int j = 32; j > 0; j >>= 1) cf_cmpx(cur, j, (lane & j) == 0);
+    for (int size = 2; size <= 64 * E; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {
+                const int es = stride >> 6;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    if (e & es) continue;
+                    const bool up = ((e * 64 + lane) & size) == 0;
+                    const uint64_t x = k[e], y = k[e | es];
+                    if ((x > y) == up) {
+                        k[e] = y;
+                        k[e | es] = x;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const uint64_t y = lane_xor_u64(k[e], stride);
+                    const bool up = ((e * 64 + lane) & size) == 0;
+                    const bool lower = (lane & stride) == 0;
+                    k[e] = (lower == up) ? (k[e] < y ? k[e] : y) : (k[e] > y ? k[e] : y);
+                }
+            }
+        }
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void rc_sort_lds(uint64_t* kw, int c) {
+    const int lane = threadIdx.x & 63;
+    uint64_t k[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) k[e] = e * 64 + lane < c ? kw[e * 64 + lane] : ~0ull;
+    wave_sort_u64<E>(k);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (e * 64 + lane < c) kw[e * 64 + lane] = k[e];
+}
+
+// The recall of a query with at most RC_CAP candidates in one wave (round 6;
+// topk <= 64), from rc_cand's keys and contributions: the keys as (j << 32 |
+// f), f the walk position (in-history: j = 0xFFFFFFFF, sorted last), a
+// register bitonic sort of them (j, then walk order), the contributions in
+// LDS by f, then per distinct j the sum of its contributions in walk order --
+// exactly the reference's item_rank[j] += w sequence -- and the first walk
+// position, fed to rc_finish_query.  Queries with more candidates are listed
+// (q, compacted offset) for the radix path.  Round 5 sent every query through
+// the global radix sort (five 8-bit passes over all candidates, tile sums,
+// emit, rc_topk).  rc_cand stays a kernel of its own: with the gathers and
+// fp64 exp of the candidate walk inlined here the wave needed 150 VGPRs (3 per
+// SIMD), and the single-kernel form measured 1.92 ms against 0.24 + ...
+constexpr int RC_CAP = 512;
+
+__global__ __launch_bounds__(256) void rc_query_kernel(
+    const int64_t* __restrict__ q_slot, int64_t nq, const int64_t* __restrict__ offsets,
+    const int32_t* __restrict__ items, const int64_t* __restrict__ cand_off, const uint64_t* __restrict__ keys,
+    const double* __restrict__ contrib, uint64_t sentinel, int bj, const int32_t* __restrict__ hot, int n_hot,
+    int topk, int32_t* __restrict__ out_items, double* __restrict__ out_scores, int32_t* __restrict__ out_src,
+    int32_t* __restrict__ out_cnt, int2* __restrict__ hlist, int32_t* __restrict__ hcnt,
+    unsigned long long* __restrict__ htot) {
+    __shared__ uint64_t sk[4][RC_CAP];
+    __shared__ double rv[4][RC_CAP];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t* kw = sk[wave];
+    double* vw = rv[wave];
+    const uint64_t jmask = (1ull << bj) - 1;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t q = (int64_t)blockIdx.x * 4 + wave; q < nq; q += nw) {
+        const int64_t sl = q_slot[q];
+        if (sl < 0) {
+            rc_cold(q, hot, n_hot, topk, out_items, out_scores, out_src, out_cnt);
+            continue;
+        }
+        const int64_t c0 = cand_off[q], cq = cand_off[q + 1] - c0;
+        if (cq > RC_CAP) {
+            if (lane == 0) {
+                const int i = atomicAdd(hcnt, 1);
+                hlist[i] = make_int2((int)q, (int)atomicAdd(htot, (unsigned long long)cq));
+            }
+            continue;
+        }
+        const int c = (int)cq;
+        const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
+        wave_sync_lds();  // the previous query's reads of kw / vw are done
+        auto sort_in = [&](auto e_c) {
+            constexpr int E = decltype(e_c)::value;
+            uint64_t k[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int i = e * 64 + lane;
+                k[e] = ~0ull;
+                if (i < c) {
+                    const uint64_t kk = keys[c0 + i];
+                    k[e] = ((kk == sentinel ? 0xFFFFFFFFull : (kk & jmask)) << 32) | (uint32_t)i;
+                    vw[i] = contrib[c0 + i];
+                }
+            }
+            wave_sort_u64<E>(k);
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if (e * 64 + lane < c) kw[e * 64 + lane] = k[e];
         };
-        for (int64_t c0 = 0; c0 < n; c0 += 64) {
-            CfEnt x{-INFINITY, INT64_MAX, -1};
-            if (c0 + lane < n) {
-                x.s = ev[a + c0 + lane];
-                x.f = ef[a + c0 + lane];
-                x.c = ej[a + c0 + lane];
-            }
-            if (c0 > 0 && cf_prunable(cur, x, topk)) continue;
-            merge(x, c0 == 0);
-        }
-        int64_t total = n;
-        if (n < topk) {
-            // fill with popular items not yet ranked and not in the history,
-            // scored -x - 100, until topk entries (:116-122)
-            const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
-            int need = (int)(topk - n);
-            CfEnt hx{-INFINITY, INT64_MAX, -1};
-            int got = 0;
-            for (int x0 = 0; x0 < n_hot && need > 0; x0 += 64) {
-                const int x = x0 + lane;
-                bool ok = false;
-                int32_t h = -1;
-                if (x < n_hot) {
-                    h = hot[x];
-                    ok = true;
-                    for (int64_t l = 0; l < L && ok; ++l) ok = items[b + l] != h;
-                    if (ok && n > 0) {  // binary search in the query's candidate js (sorted)
-                        int64_t lo = a, hi = e;
-                        while (lo < hi) {
-                            const int64_t mid = (lo + hi) >> 1;
-                            if (ej[mid] < h) lo = mid + 1;
-                            else hi = mid;
+        if (c <= 64) sort_in(std::integral_constant<int, 1>{});
+        else if (c <= 128) sort_in(std::integral_constant<int, 2>{});
+        else if (c <= 256) sort_in(std::integral_constant<int, 4>{});
+        else sort_in(std::integral_constant<int, 8>{});
+        wave_sync_lds();
+        rc_finish_query(
+            q, c,
+            [&](int64_t p0) {
+                const int i = (int)p0 + lane;
+                CfEnt x{-INFINITY, INT64_MAX, -1};
+                if (i < c) {
+                    const uint64_t k = kw[i];
+                    const uint32_t j = (uint32_t)(k >> 32);
+                    if (j != 0xFFFFFFFFu && (i == 0 || (uint32_t)(kw[i - 1] >> 32) != j)) {
+                        double sum = 0.0;  // item_rank[j] += w, walk order (:118-119)
+                        for (int t = i; t < c; ++t) {
+                            const uint64_t kt = kw[t];
+                            if ((uint32_t)(kt >> 32) != j) break;
+                            sum += vw[(uint32_t)kt];
                         }
-                        ok = !(lo < e && ej[lo] == h);
+                        x = CfEnt{sum, c0 + (int64_t)(uint32_t)k, (int32_t)j};
                     }
                 }
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(ok);
-                const int take = __builtin_popcountll(bal) < need ? __builtin_popcountll(bal) : need;
-                // the first `take` accepted entries, in hot order, into hx lanes got ..
-                for (int t = 0; t < take; ++t) {
-                    // lane holding the t-th set bit of bal
-                    uint64_t bb = bal;
-                    for (int z = 0; z < t; ++z) bb &= bb - 1ull;
-                    const int src = __builtin_ctzll(bb);
-                    const int32_t hv = __shfl(h, src, WAVE);
-                    if (lane == got + t) {
-                        hx.s = (double)(-(x0 + src) - 100);
-                        hx.f = HOT_FIRST + x0 + src;
-                        hx.c = hv;
-                    }
+                return x;
+            },
+            [&](int32_t h) {  // h among the candidates: bisection of the sorted keys
+                const uint64_t kh = (uint64_t)(uint32_t)h << 32;
+                int lo = 0, hi = c;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (kw[mid] < kh) lo = mid + 1;
+                    else hi = mid;
                 }
-                got += take;
-                need -= take;
-            }
-            total += got;
-            if (got > 0) merge(hx, n == 0);
+                return lo < c && (uint32_t)(kw[lo] >> 32) == (uint32_t)h;
+            },
+            b, L, items, hot, n_hot, topk, out_items, out_scores, out_src, out_cnt);
+    }
+}
+
+// The listed queries' keys and slots to the front of (kout, vout), query by
+// query (the contributions stay where rc_cand wrote them: the slots index
+// them).  One wave per listed query.
+__global__ __launch_bounds__(256) void rc_compact_kernel(const int64_t* __restrict__ cand_off,
+                                                         const uint64_t* __restrict__ kin,
+                                                         const int32_t* __restrict__ vin,
+                                                         const int2* __restrict__ hlist,
+                                                         const int32_t* __restrict__ hcnt,
+                                                         uint64_t* __restrict__ kout, int32_t* __restrict__ vout) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4, nl = *hcnt;
+    for (int64_t iq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); iq < nl; iq += nw) {
+        const int2 h = hlist[iq];
+        const int64_t c0 = cand_off[h.x], cq = cand_off[h.x + 1] - c0;
+        for (int64_t i = lane; i < cq; i += 64) {
+            kout[h.y + i] = kin[c0 + i];
+            vout[h.y + i] = vin[c0 + i];
         }
-        const int64_t m = total < topk ? total : topk;
-        if (lane < topk) {
-            const bool ok = lane < m;
-            oi[lane] = ok ? cur.c : -1;
-            os[lane] = ok ? cur.s : 0.0;
-            osrc[lane] = ok ? (cur.f >= HOT_FIRST ? 1 : 0) : -1;
-        }
-        if (lane == 0) out_cnt[q] = (int32_t)m;
     }
 }
 
@@ -1091,9 +1358,23 @@ __global__ __launch_bounds__(1024) void cf_topn_heavy_kernel(const int64_t* __re
     __shared__ double ls[16][64];
     __shared__ int64_t lf[16][64];
     __shared__ int32_t lc[16][64];
+    __shared__ int64_t hrow[1024];
+    __shared__ int nh;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int64_t row = blockIdx.x; row < n_rows; row += gridDim.x) {
-        if (out_cnt[row] != -1) continue;  // uniform across the workgroup
+    // the flagged rows of a 1,024-row window, found by one coalesced read
+    // (round 6: each workgroup tested its rows one dependent load at a time,
+    // ~560 round trips per workgroup before any heavy row)
+    for (int64_t base = (int64_t)blockIdx.x * 1024; base < n_rows; base += (int64_t)gridDim.x * 1024) {
+    if (threadIdx.x == 0) nh = 0;
+    __syncthreads();
+    {
+        const int64_t r = base + threadIdx.x;
+        if (r < n_rows && out_cnt[r] == -1) hrow[atomicAdd(&nh, 1)] = r;
+    }
+    __syncthreads();
+    const int nhv = nh;
+    for (int ih = 0; ih < nhv; ++ih) {
+        const int64_t row = hrow[ih];
         const int64_t a = row_off[row], n = row_off[row + 1] - a;
         CfEnt cur{-INFINITY, INT64_MAX, -1};
         auto merge_in = [&](CfEnt x) {  // x sorted desc; keep the top 64 of cur + x
@@ -1105,22 +1386,35 @@ __global__ __launch_bounds__(1024) void cf_topn_heavy_kernel(const int64_t* __re
                 cur.f = yf;
                 cur.c = yc;
             }
-#pragma unroll
-            for (int j = 32; j > 0; j >>= 1) cf_cmpx(cur, j, (lane & j) == 0);
+            cf_clean64(cur);
         };
         bool started = false;
-        for (int64_t c0 = (int64_t)wv * 64; c0 < n; c0 += 16 * 64) {
-            CfEnt x{-INFINITY, INT64_MAX, -1};
-            if (c0 + lane < n) {
-                x.s = vals[a + c0 + lane];
-                x.f = first[a + c0 + lane];
-                x.c = cols[a + c0 + lane];
+        // the wave's chunks wv, wv + 16, ... in that order, CF_HB of them
+        // loaded at once (round 6: one chunk's loads per round trip, and most
+        // chunks are pruned without a sort, so the loads were the time)
+        constexpr int CF_HB = 4;
+        for (int64_t c0 = (int64_t)wv * 64; c0 < n; c0 += CF_HB * 16 * 64) {
+            CfEnt xs[CF_HB];
+#pragma unroll
+            for (int t = 0; t < CF_HB; ++t) {
+                const int64_t e = c0 + (int64_t)t * 16 * 64 + lane;
+                xs[t] = CfEnt{-INFINITY, INT64_MAX, -1};
+                if (e < n) {
+                    xs[t].s = vals[a + e];
+                    xs[t].f = first[a + e];
+                    xs[t].c = cols[a + e];
+                }
             }
-            if (started && cf_prunable(cur, x, topn)) continue;
-            cf_sort64(x);
-            if (!started) cur = x;
-            else merge_in(x);
-            started = true;
+#pragma unroll
+            for (int t = 0; t < CF_HB; ++t) {
+                if (c0 + (int64_t)t * 16 * 64 >= n) break;  // wave-uniform
+                CfEnt x = xs[t];
+                if (started && cf_prunable(cur, x, topn)) continue;
+                cf_sort64(x);
+                if (!started) cur = x;
+                else merge_in(x);
+                started = true;
+            }
         }
         ls[wv][lane] = cur.s;
         lf[wv][lane] = cur.f;
@@ -1137,6 +1431,8 @@ __global__ __launch_bounds__(1024) void cf_topn_heavy_kernel(const int64_t* __re
             if (lane == 0) out_cnt[row] = (int32_t)m;
         }
         __syncthreads();
+    }
+    __syncthreads();  // nh is reset for the next window
     }
 }
 
@@ -1349,6 +1645,9 @@ struct RcWs {
     int32_t *eq, *ej;
     double* ev;
     int64_t *ef, *n_emit;
+    int2* hlist;
+    int32_t* hcnt;
+    unsigned long long* htot;
     size_t bytes;
 };
 
@@ -1364,6 +1663,9 @@ static RcWs rc_ws_layout(void* base, int64_t n_cand) {
     w.ev = (double*)take(n * 8);
     w.ef = (int64_t*)take(n * 8);
     w.n_emit = (int64_t*)take(8);
+    w.hlist = (int2*)take((n / RC_CAP + 1) * sizeof(int2));  // at most n / (RC_CAP + 1) overflow queries
+    w.hcnt = (int32_t*)take(16);                              // + the overflow candidate total at +8
+    w.htot = reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(w.hcnt) + 8);
     w.bytes = o;
     return w;
 }
@@ -1483,7 +1785,8 @@ int nrk_itemcf_topn(const int64_t* row_off, int64_t n_rows, const int32_t* cols,
     const int64_t g = (n_rows + 3) / 4;
     cf_topn_kernel<<<(int)(g < 65536 ? g : 65536), 256, 0, as_stream(stream)>>>(
         row_off, n_rows, cols, vals, first, topn, out_cols, out_vals, out_cnt);
-    cf_topn_heavy_kernel<<<(int)(n_rows < 512 ? n_rows : 512), 1024, 0, as_stream(stream)>>>(
+    const int64_t gw = (n_rows + 1023) / 1024;
+    cf_topn_heavy_kernel<<<(int)(gw < 512 ? gw : 512), 1024, 0, as_stream(stream)>>>(
         row_off, n_rows, cols, vals, first, topn, out_cols, out_vals, out_cnt);
     NRK_CHECK_LAUNCH();
     return NRK_OK;
@@ -1543,8 +1846,16 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
     const int gq = (int)(g < 65536 ? g : 65536);
     const int64_t n = n_cand;
     const int nblk = (int)((n + RS_TILE - 1) / RS_TILE);
+    const RcParams prm{loc_beta, created_alpha, cf_ln(created_alpha), topn, ke, bj};
+    // topk <= 64: every query with <= RC_CAP candidates is finished by
+    // rc_query_kernel from rc_cand's output; the radix path then runs over
+    // the listed larger queries only, compacted to the front of the sort
+    // buffers (device-side count: its launches exit at once when there are
+    // none).  topk > 64: every query takes the radix path.
+    const bool fused = topk <= 64;
+    const int64_t* n_dev = nullptr;
+    int gl = gq;
     if (n > 0) {
-        const RcParams prm{loc_beta, created_alpha, cf_ln(created_alpha), topn, ke, bj};
         rc_cand_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, nbr_cols, nbr_vals, nbr_cnt, created,
                                           emb_cols, emb_vals, emb_cnt, prm, cand_off, sentinel, w.sort.ka,
                                           w.sort.va, w.sort.w);
@@ -1552,27 +1863,57 @@ int nrk_itemcf_recall(const int64_t* q_slot, int64_t n_query, const int64_t* off
         uint64_t* kout = w.sort.kb;
         int32_t* vin = w.sort.va;
         int32_t* vout = w.sort.vb;
+        if (fused) {
+            (void)hipMemsetAsync(w.hcnt, 0, 16, s);
+            static const int qgrid = [] {
+                int dev = 0, cu = 256, per = 0;
+                if (hipGetDevice(&dev) == hipSuccess)
+                    (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)rc_query_kernel, 256, 0) !=
+                        hipSuccess ||
+                    per <= 0)
+                    per = 4;
+                return per * (cu > 0 ? cu : 256);
+            }();
+            rc_query_kernel<<<(int)(g < qgrid ? g : qgrid), 256, 0, s>>>(
+                q_slot, n_query, offsets, items, cand_off, w.sort.ka, w.sort.w, sentinel, bj, hot, n_hot, topk,
+                out_items, out_scores, out_src, out_cnt, w.hlist, w.hcnt, w.htot);
+            const int64_t gh = (n / (RC_CAP + 1) + 4) / 4;
+            gl = (int)(gh < 65536 ? gh : 65536);
+            rc_compact_kernel<<<gl, 256, 0, s>>>(cand_off, kin, vin, w.hlist, w.hcnt, kout, vout);
+            uint64_t* tk = kin; kin = kout; kout = tk;
+            int32_t* tv = vin; vin = vout; vout = tv;
+            n_dev = reinterpret_cast<const int64_t*>(w.htot);
+        }
         for (int shift = 0; shift < nbits; shift += 8) {
-            rs_upsweep<<<nblk, RS_THREADS, 0, s>>>(kin, n, shift, nblk, w.sort.counts);
+            rs_upsweep<<<nblk, RS_THREADS, 0, s>>>(kin, n, shift, nblk, w.sort.counts, n_dev);
             rs_scan_rows<<<256, 256, 0, s>>>(w.sort.counts, nblk, w.sort.totals);
             rs_downsweep<<<nblk, RS_THREADS, 0, s>>>(kin, vin, kout, vout, n, shift, nblk, w.sort.counts,
-                                                     w.sort.totals);
+                                                     w.sort.totals, n_dev);
             uint64_t* tk = kin; kin = kout; kout = tk;
             int32_t* tv = vin; vin = vout; vout = tv;
         }
         double* wsorted = reinterpret_cast<double*>(kout);
         cf_tile_reduce<<<nblk, RS_THREADS, 0, s>>>(kin, vin, w.sort.w, n, sentinel, w.sort.blkcnt, w.sort.tail,
-                                                   w.sort.brk, wsorted);
+                                                   w.sort.brk, wsorted, n_dev);
         cf_head_scan<<<1, 1024, 0, s>>>(w.sort.blkcnt, nblk, w.sort.blkoff, w.n_emit);
         cf_carry_scan<<<1, 1024, 0, s>>>(w.sort.tail, w.sort.brk, nblk, w.sort.carry);
         cf_emit<<<nblk, RS_THREADS, 0, s>>>(kin, vin, wsorted, n, sentinel, w.sort.blkoff, w.sort.carry, nullptr,
-                                             nullptr, bj, w.eq, w.ej, w.ev, w.ef);
+                                             nullptr, bj, w.eq, w.ej, w.ev, w.ef, n_dev);
     } else {
         (void)hipMemsetAsync(w.n_emit, 0, sizeof(int64_t), s);
+        if (fused) (void)hipMemsetAsync(w.hcnt, 0, 16, s);
     }
-    if (topk <= 64) {
-        rc_topk_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, hot, n_hot, w.eq, w.ej, w.ev, w.ef,
-                                          w.n_emit, topk, out_items, out_scores, out_src, out_cnt);
+    if (fused) {
+        // n == 0: no listed queries, every query is a cold start or has no
+        // candidates -> all of them through the list-free form
+        if (n > 0)
+            rc_topk_kernel<<<gl, 256, 0, s>>>(q_slot, n_query, offsets, items, hot, n_hot, w.eq, w.ej, w.ev, w.ef,
+                                              w.n_emit, topk, out_items, out_scores, out_src, out_cnt, w.hlist,
+                                              w.hcnt);
+        else
+            rc_topk_kernel<<<gq, 256, 0, s>>>(q_slot, n_query, offsets, items, hot, n_hot, w.eq, w.ej, w.ev, w.ef,
+                                              w.n_emit, topk, out_items, out_scores, out_src, out_cnt);
     } else {
         const int K = cf_wide_k(topk);
         const size_t lds = (size_t)2 * K * sizeof(CfEnt);
