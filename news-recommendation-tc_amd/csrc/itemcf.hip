@@ -71,16 +71,24 @@ __global__ __launch_bounds__(1024) void scan_exclusive_kernel(F f, int64_t n, in
     __shared__ int64_t wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int64_t carry = 0;
-    for (int64_t t0 = 0; t0 < n; t0 += SCAN_TILE) {
-        int64_t v[SCAN_PT];
+    // the next tile's values load while this one is scanned (round 6: one
+    // load round trip per tile was most of the time; tiles never overlap, so
+    // an aliased out is still read before it is written)
+    int64_t v[SCAN_PT];
 #pragma unroll
-        for (int j = 0; j < SCAN_PT; ++j) {
-            const int64_t e = t0 + j * 1024 + tid;
-            v[j] = e < n ? f(e) : 0;
-        }
+    for (int j = 0; j < SCAN_PT; ++j) {
+        const int64_t e = j * 1024 + tid;
+        v[j] = e < n ? f(e) : 0;
+    }
+    for (int64_t t0 = 0; t0 < n; t0 += SCAN_TILE) {
 #pragma unroll
         for (int j = 0; j < SCAN_PT; ++j) sv[cf_pad(j * 1024 + tid)] = v[j];
         __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SCAN_PT; ++j) {
+            const int64_t e = t0 + SCAN_TILE + j * 1024 + tid;
+            v[j] = e < n ? f(e) : 0;
+        }
         int64_t c[SCAN_PT], sum = 0;
 #pragma unroll
         for (int r = 0; r < SCAN_PT; ++r) {
@@ -1064,14 +1072,20 @@ __device__ __forceinline__ void rc_finish_query(int64_t q, int64_t nsrc, Chunk&&
         int got = 0;
         for (int x0 = 0; x0 < n_hot && need > 0; x0 += 64) {
             const int x = x0 + lane;
-            bool ok = false;
-            int32_t h = -1;
-            if (x < n_hot) {
-                h = hot[x];
-                ok = true;
-                for (int64_t l = 0; l < L && ok; ++l) ok = items[b + l] != h;
-                if (ok && n > 0) ok = !in_cands(h);
+            const int32_t h = x < n_hot ? hot[x] : -1;
+            bool ok = x < n_hot;
+            // not in the history: its clicks 64 at a time, one per lane, each
+            // compared by a uniform-index read (round 5: every lane walked the
+            // history by dependent loads)
+            for (int64_t hc = 0; hc < L; hc += 64) {
+                const int32_t hv = hc + lane < L ? items[b + hc + lane] : -1;
+                const int nh = (int)(L - hc < 64 ? L - hc : 64);
+                for (int l = 0; l < nh; ++l) {
+                    const int32_t hl = __shfl(hv, l, WAVE);  // every lane active: a shuffle under
+                    ok = ok && hl != h;                      // a short-circuit reads stale lanes
+                }
             }
+            if (ok && n > 0) ok = !in_cands(h);
             const uint64_t bal = __builtin_amdgcn_ballot_w64(ok);
             const int take = __builtin_popcountll(bal) < need ? __builtin_popcountll(bal) : need;
             // the first `take' accepted entries, in hot order, into hx lanes
@@ -1114,6 +1128,58 @@ __device__ __forceinline__ void rc_cold(int64_t q, const int32_t* __restrict__ h
         out_items[q * topk + lane] = lane < m ? hot[lane] : -1;
         out_scores[q * topk + lane] = lane < m ? -(double)lane : 0.0;
         out_src[q * topk + lane] = lane < m ? 2 : -1;
+    }
+    if (lane == 0) out_cnt[q] = m;
+}
+
+// rc_finish_query for at most 64 distinct candidates, lane i < nd holding
+// entry x: the hot fill goes to lanes [nd, nd + got) (it only runs when nd <
+// topk <= 64), then one 64-wide sort gives the output row.
+template <class InCands>
+__device__ __forceinline__ void rc_finish_small(int64_t q, CfEnt x, int nd, InCands&& in_cands, int64_t b,
+                                                int64_t L, const int32_t* __restrict__ items,
+                                                const int32_t* __restrict__ hot, int n_hot, int topk,
+                                                int32_t* __restrict__ out_items, double* __restrict__ out_scores,
+                                                int32_t* __restrict__ out_src, int32_t* __restrict__ out_cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t HOT_FIRST = (int64_t)1 << 62;
+    int total = nd;
+    if (nd < topk) {
+        int need = topk - nd, got = 0;
+        for (int x0 = 0; x0 < n_hot && need > 0; x0 += 64) {
+            const int xi = x0 + lane;
+            const int32_t h = xi < n_hot ? hot[xi] : -1;
+            bool ok = xi < n_hot;
+            for (int64_t hc = 0; hc < L; hc += 64) {
+                const int32_t hv = hc + lane < L ? items[b + hc + lane] : -1;
+                const int nh = (int)(L - hc < 64 ? L - hc : 64);
+                for (int l = 0; l < nh; ++l) {
+                    const int32_t hl = __shfl(hv, l, WAVE);  // every lane active: a shuffle under
+                    ok = ok && hl != h;                      // a short-circuit reads stale lanes
+                }
+            }
+            if (ok && nd > 0) ok = !in_cands(h);
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(ok);
+            const int take = __builtin_popcountll(bal) < need ? __builtin_popcountll(bal) : need;
+            const int t = lane - nd - got;
+            int src = 0;
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1)
+                if (__builtin_popcountll(bal & ((2ull << (src + st - 1)) - 1ull)) < t + 1) src += st;
+            const int32_t hv = __shfl(h, src, WAVE);
+            if (t >= 0 && t < take) x = CfEnt{(double)(-(x0 + src) - 100), HOT_FIRST + x0 + src, hv};
+            got += take;
+            need -= take;
+        }
+        total += got;
+    }
+    cf_sort64(x);
+    const int m = total < topk ? total : topk;
+    if (lane < topk) {
+        const bool ok = lane < m;
+        out_items[q * topk + lane] = ok ? x.c : -1;
+        out_scores[q * topk + lane] = ok ? x.s : 0.0;
+        out_src[q * topk + lane] = ok ? (x.f >= HOT_FIRST ? 1 : 0) : -1;
     }
     if (lane == 0) out_cnt[q] = m;
 }
@@ -1266,7 +1332,11 @@ __global__ __launch_bounds__(256) void rc_query_kernel(
         const int c = (int)cq;
         const int64_t b = offsets[sl], L = offsets[sl + 1] - b;
         wave_sync_lds();  // the previous query's reads of kw / vw are done
-        auto sort_in = [&](auto e_c) {
+        // (1) keys (j << 32 | f) sorted in registers; (2) per distinct j, its
+        // sum in walk order by the run's first lane (registers); (3) the
+        // distinct entries compacted in j order into the front of kw / vw
+        // (key, sum) -- every read of (1) / (2) is done first.  Returns nd.
+        auto distinct = [&](auto e_c) -> int {
             constexpr int E = decltype(e_c)::value;
             uint64_t k[E];
 #pragma unroll
@@ -1283,43 +1353,69 @@ __global__ __launch_bounds__(256) void rc_query_kernel(
 #pragma unroll
             for (int e = 0; e < E; ++e)
                 if (e * 64 + lane < c) kw[e * 64 + lane] = k[e];
-        };
-        if (c <= 64) sort_in(std::integral_constant<int, 1>{});
-        else if (c <= 128) sort_in(std::integral_constant<int, 2>{});
-        else if (c <= 256) sort_in(std::integral_constant<int, 4>{});
-        else sort_in(std::integral_constant<int, 8>{});
-        wave_sync_lds();
-        rc_finish_query(
-            q, c,
-            [&](int64_t p0) {
-                const int i = (int)p0 + lane;
-                CfEnt x{-INFINITY, INT64_MAX, -1};
-                if (i < c) {
-                    const uint64_t k = kw[i];
-                    const uint32_t j = (uint32_t)(k >> 32);
-                    if (j != 0xFFFFFFFFu && (i == 0 || (uint32_t)(kw[i - 1] >> 32) != j)) {
-                        double sum = 0.0;  // item_rank[j] += w, walk order (:118-119)
-                        for (int t = i; t < c; ++t) {
-                            const uint64_t kt = kw[t];
-                            if ((uint32_t)(kt >> 32) != j) break;
-                            sum += vw[(uint32_t)kt];
-                        }
-                        x = CfEnt{sum, c0 + (int64_t)(uint32_t)k, (int32_t)j};
+            wave_sync_lds();
+            bool hd[E];
+            double hs[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int i = e * 64 + lane;
+                const uint32_t j = (uint32_t)(k[e] >> 32);
+                hd[e] = i < c && j != 0xFFFFFFFFu && (i == 0 || (uint32_t)(kw[i - 1] >> 32) != j);
+                hs[e] = 0.0;
+                if (hd[e]) {
+                    double sum = 0.0;  // item_rank[j] += w, walk order (:118-119)
+                    for (int t = i; t < c; ++t) {
+                        const uint64_t kt = kw[t];
+                        if ((uint32_t)(kt >> 32) != j) break;
+                        sum += vw[(uint32_t)kt];
                     }
+                    hs[e] = sum;
                 }
-                return x;
-            },
-            [&](int32_t h) {  // h among the candidates: bisection of the sorted keys
-                const uint64_t kh = (uint64_t)(uint32_t)h << 32;
-                int lo = 0, hi = c;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (kw[mid] < kh) lo = mid + 1;
-                    else hi = mid;
+            }
+            wave_sync_lds();
+            int nd = 0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint64_t bal = __ballot(hd[e]);
+                if (hd[e]) {
+                    const int pos = nd + __popcll(bal & ((1ull << lane) - 1ull));
+                    kw[pos] = k[e];
+                    vw[pos] = hs[e];
                 }
-                return lo < c && (uint32_t)(kw[lo] >> 32) == (uint32_t)h;
-            },
-            b, L, items, hot, n_hot, topk, out_items, out_scores, out_src, out_cnt);
+                nd += __popcll(bal);
+            }
+            return nd;
+        };
+        int nd;
+        if (c <= 64) nd = distinct(std::integral_constant<int, 1>{});
+        else if (c <= 128) nd = distinct(std::integral_constant<int, 2>{});
+        else if (c <= 256) nd = distinct(std::integral_constant<int, 4>{});
+        else nd = distinct(std::integral_constant<int, 8>{});
+        wave_sync_lds();
+        auto in_cands = [&](int32_t h) {  // h among the distinct js: bisection
+            const uint64_t kh = (uint64_t)(uint32_t)h << 32;
+            int lo = 0, hi = nd;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (kw[mid] < kh) lo = mid + 1;
+                else hi = mid;
+            }
+            return lo < nd && (uint32_t)(kw[lo] >> 32) == (uint32_t)h;
+        };
+        auto ent = [&](int i) {
+            return i < nd ? CfEnt{vw[i], c0 + (int64_t)(uint32_t)kw[i], (int32_t)(kw[i] >> 32)}
+                          : CfEnt{-INFINITY, INT64_MAX, -1};
+        };
+        if (nd <= 64) {
+            // one sort: the distinct entries in lanes [0, nd), the hot fill
+            // (only when nd < topk <= 64) behind them
+            rc_finish_small(q, ent(lane), nd, in_cands, b, L, items, hot, n_hot, topk, out_items, out_scores,
+                            out_src, out_cnt);
+        } else {
+            rc_finish_query(
+                q, nd, [&](int64_t p0) { return ent((int)p0 + lane); }, in_cands, b, L, items, hot, n_hot, topk,
+                out_items, out_scores, out_src, out_cnt);
+        }
     }
 }
 
