@@ -2814,6 +2814,11 @@ static void launch_scan_v(const float* users, int n_users, const uint8_t* cat, i
         w.bnd_m);
 }
 
+// ring slots of dim 128's 8-wave scan: 4 x 32 KB (tools/scan128.py, 250k x
+// 5M, one box, two pairs: 240.2-240.7 vs 241.6-242.8 ms at 3; rows identical)
+#ifndef NRK_SCAN128_NSL
+#define NRK_SCAN128_NSL 4
+#endif
 template <int DP, int MT>
 static void launch_scan(const float* users, int n_users, const uint8_t* cat, int n_items, int dim, int k,
                         const IpWs& w, hipStream_t s) {
@@ -2837,7 +2842,8 @@ static void launch_scan(const float* users, int n_users, const uint8_t* cat, int
     // inserts 8.1 (the lagging cut doubles the appends)
     // ring slots capped by the CU's 160 KB of LDS (dim 128's 32-KB tiles: 4 -> 3 at UG = 1)
     constexpr int TILE_B = scan_tb(DP) * 64 * DP, NSL_CAP = 163840 / TILE_B;
-    constexpr int NW = (UG == 2) ? 8 : 4, NSL0 = (UG == 2) ? 3 : 4, NSL = NSL0 < NSL_CAP ? NSL0 : NSL_CAP;
+    constexpr int NW = (UG == 2) ? 8 : 4, NSL0 = (UG == 2) ? (DP == 128 ? NRK_SCAN128_NSL : 3) : 4,
+                  NSL = NSL0 < NSL_CAP ? NSL0 : NSL_CAP;
     static_assert(NSL >= 2, "ring");
     launch_scan_v<DP, NW, NSL, UG, MT, WPE>(users, n_users, cat, n_items, dim, k, w, s);
 }
