@@ -1698,14 +1698,18 @@ __device__ __forceinline__ double exact_dot(const float* __restrict__ a, const f
 #endif
 constexpr bool REFINE_DIRECT = NRK_REFINE_DIRECT;
 // waves per SIMD the refine's registers are sized for (dim 64's staged
-// rounds take 2).  Round 6: two prefilter rounds in flight (three register
-// slots rotated by unrolling) at 3 waves per SIMD measured slower than one
-// round ahead at 4: finish 0.961-0.966 vs 0.873-0.884 ms (config 2, one box)
+// rounds take 2, the generic dims 4).  Round 6: two prefilter rounds in
+// flight (three register slots rotated by unrolling) at 3 waves per SIMD
+// measured slower than one round ahead at 4: finish 0.961-0.966 vs
+// 0.873-0.884 ms (config 2, one box).  Then the user's fp16 row moved to LDS
+// and the direct exact dot to two half-rows: dim 32 needs 80 VGPRs instead of
+// 128, and finish went 0.871 -> 0.776 ms at 4 / 0.772 at 6 waves per SIMD
+// (one box, two runs each)
 #ifndef NRK_REFINE_WPE
-#define NRK_REFINE_WPE 4
+#define NRK_REFINE_WPE 6
 #endif
 template <int DS4, int SV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ? 2 : NRK_REFINE_WPE))) void ip_refine_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ? 2 : DS4 == 0 ? 4 : NRK_REFINE_WPE))) void ip_refine_kernel(
     const float* __restrict__ users, int64_t n_users, const float* __restrict__ items,
     const uint8_t* __restrict__ catalog, int64_t n_items, int dim, int k, int64_t row_offset,
     const uint2* __restrict__ cand, int bandcap, const int32_t* __restrict__ cand_cnt,
@@ -1789,7 +1793,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ?
     // for the exact score.
     constexpr int DSK = DS4 / 4;  // 16-dim k-steps of the packed layout
     const bool pre = catalog != nullptr && ce.x != -INFINITY;
-    _Float16 ush[DS4 > 0 ? 4 * DS4 : 1];  // the user's fp16 values (packed: half the VGPRs)
+    // the user's fp16 values, read 8 at a time by the prefilter (wave-uniform:
+    // in registers they held 4 DS4 / 2 VGPRs for the whole kernel)
+    __shared__ __attribute__((aligned(16))) _Float16 ushs[4][DS4 > 0 ? 4 * DS4 : 8];
+    _Float16* ush = ushs[wave];
     float pcut = 0.0f;
     if (pre) {
         const int dpc = pad_dim(dim);
@@ -1801,7 +1808,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ?
         const float su = pow2_scale(ua);
         if constexpr (DS4 > 0) {
 #pragma unroll
-            for (int d = 0; d < 4 * DS4; ++d) ush[d] = (_Float16)(uv[d] * su);
+            for (int d = lane; d < 4 * DS4; d += WAVE) ush[d] = (_Float16)(uv[d] * su);
+            wave_sync_lds();
         }
         pcut = ce.x * (su * hdr->scale);
     }
@@ -1900,17 +1908,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ?
                 if (rl >= 0) {
                     const float4* a4 = reinterpret_cast<const float4*>(uv);
                     const float4* b4 = reinterpret_cast<const float4*>(items + (int64_t)rl * dim);
-                    float4 y[DS4];
-#pragma unroll
-                    for (int t = 0; t < DS4; ++t) y[t] = b4[t];
+                    constexpr int YH = DS4 > 4 ? DS4 / 2 : DS4;  // half-rows: fewer live VGPRs
                     double acc = 0.0;
 #pragma unroll
-                    for (int t = 0; t < DS4; ++t) {
-                        const float4 x = a4[t];
-                        acc += (double)x.x * (double)y[t].x;
-                        acc += (double)x.y * (double)y[t].y;
-                        acc += (double)x.z * (double)y[t].z;
-                        acc += (double)x.w * (double)y[t].w;
+                    for (int t0 = 0; t0 < DS4; t0 += YH) {
+                        float4 y[YH];
+#pragma unroll
+                        for (int t = 0; t < YH; ++t) y[t] = b4[t0 + t];
+#pragma unroll
+                        for (int t = 0; t < YH; ++t) {
+                            const float4 x = a4[t0 + t];
+                            acc += (double)x.x * (double)y[t].x;
+                            acc += (double)x.y * (double)y[t].y;
+                            acc += (double)x.z * (double)y[t].z;
+                            acc += (double)x.w * (double)y[t].w;
+                        }
                     }
                     sd = acc + 0.0;
                     keep = sd >= thr;
@@ -1973,9 +1985,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DS4 == 16 ?
 #pragma unroll
                     for (int hh = 0; hh < 2; ++hh) {
                         const f16x8 hv = __builtin_bit_cast(f16x8, pc[2 * st + hh]);
+                        const f16x8 uh = *reinterpret_cast<const f16x8*>(&ush[16 * st + 8 * hh]);
 #pragma unroll
                         for (int e = 0; e < 8; ++e)
-                            acc = fmaf((float)hv[e], (float)ush[16 * st + 8 * hh + e], acc);  // exact product: fma_mix
+                            acc = fmaf((float)hv[e], (float)uh[e], acc);  // exact product: fma_mix
                     }
                 keep = acc >= pcut;
             }
