@@ -115,20 +115,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void t
             const float* wr0 = sw0 + (lane < h0 ? lane : 0) * S0;
             const float* wr1 = sw0 + (lane + WAVE < h0 ? lane + WAVE : 0) * S0;
             // 4 inputs (broadcast) and 4 weights per LDS read; the fma
-            // chain still runs q = 0, 1, 2, ... in order
+            // chain still runs q = 0, 1, 2, ... in order.  Outputs 64 ..
+            // only when h0 > 64 (round 6: the second chain ran, on row 0,
+            // for every h0)
+            if (h0 > WAVE) {
 #pragma unroll 2
-            for (int q = 0; q < 2 * D; q += 4) {
-                const float4 xq = *reinterpret_cast<const float4*>(sx + q);
-                const float4 a = *reinterpret_cast<const float4*>(wr0 + q);
-                const float4 b = *reinterpret_cast<const float4*>(wr1 + q);
-                z0 += a.x * xq.x;
-                z0 += a.y * xq.y;
-                z0 += a.z * xq.z;
-                z0 += a.w * xq.w;
-                z1 += b.x * xq.x;
-                z1 += b.y * xq.y;
-                z1 += b.z * xq.z;
-                z1 += b.w * xq.w;
+                for (int q = 0; q < 2 * D; q += 4) {
+                    const float4 xq = *reinterpret_cast<const float4*>(sx + q);
+                    const float4 a = *reinterpret_cast<const float4*>(wr0 + q);
+                    const float4 b = *reinterpret_cast<const float4*>(wr1 + q);
+                    z0 += a.x * xq.x;
+                    z0 += a.y * xq.y;
+                    z0 += a.z * xq.z;
+                    z0 += a.w * xq.w;
+                    z1 += b.x * xq.x;
+                    z1 += b.y * xq.y;
+                    z1 += b.z * xq.z;
+                    z1 += b.w * xq.w;
+                }
+            } else {
+#pragma unroll 2
+                for (int q = 0; q < 2 * D; q += 4) {
+                    const float4 xq = *reinterpret_cast<const float4*>(sx + q);
+                    const float4 a = *reinterpret_cast<const float4*>(wr0 + q);
+                    z0 += a.x * xq.x;
+                    z0 += a.y * xq.y;
+                    z0 += a.z * xq.z;
+                    z0 += a.w * xq.w;
+                }
             }
             y0 = fmaxf(z0, 0.0f);
             y1 = fmaxf(z1, 0.0f);
