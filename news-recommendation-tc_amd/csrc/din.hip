@@ -533,7 +533,15 @@ __global__ void din_absmax_kernel(const void* __restrict__ table, int dtype, int
     m = fmaxf(m, __shfl_xor(m, 4, WAVE));
     m = fmaxf(m, __shfl_xor(m, 2, WAVE));
     m = fmaxf(m, __shfl_xor(m, 1, WAVE));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // m >= 0: bit order == value order
+    // one atomic per workgroup (round 6: one per wave, thousands on one
+    // address, made each call ~26 us)
+    __shared__ float wm[16];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = fmaxf(m, wm[w]);
+        atomicMax(out, __float_as_uint(m));  // m >= 0: bit order == value order
+    }
 }
 
 
@@ -2284,7 +2292,7 @@ int nrk_din_prepare(const float* att_w0, int n_item, const void* table, int tabl
     (void)hipMemsetAsync(mx, 0, 8, s);
     const int64_t n = n_table_rows * DIN_E;
     const int64_t g = (n + 255) / 256;
-    din_absmax_kernel<<<(int)(g < 2048 ? g : 2048), 256, 0, s>>>(table, table_dtype, n, mx);
+    din_absmax_kernel<<<(int)(g < 512 ? g : 512), 256, 0, s>>>(table, table_dtype, n, mx);
     din_scales_kernel<<<1, 256, 0, s>>>(pf, ID, mx, sc);
     // the position-major kernel's scales and packed weight fragments
     uint8_t* tm = reinterpret_cast<uint8_t*>(prep) + din_tm_base(n_item);
@@ -2420,7 +2428,7 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
             return NRK_EHIP;
         }
         const int64_t nw = (int64_t)h1 * IN;
-        din_absmax_kernel<<<(int)std::min<int64_t>((nw + 255) / 256, 1024), 256, 0, s>>>(mlp_w0, 0, nw, w1max);
+        din_absmax_kernel<<<(int)std::min<int64_t>((nw + 255) / 256, 128), 256, 0, s>>>(mlp_w0, 0, nw, w1max);
         const int NT = din_mlp1_nt(h1);
         const int64_t npk = (int64_t)(IN / DIN_E) * NT * 64;
         const int gp = (int)std::min<int64_t>((npk + 255) / 256, 2048);
@@ -2482,7 +2490,7 @@ int nrk_din_forward_segments(const void* table, int table_dtype, const int64_t* 
         unsigned int* z1max = w.whmax + n_seg + 1;
         unsigned int* w2max = z1max + n_seg;
         const int64_t nw = (int64_t)h2 * h1;
-        din_absmax_kernel<<<(int)std::min<int64_t>((nw + 255) / 256, 256), 256, 0, s>>>(mlp_w1, 0, nw, w2max);
+        din_absmax_kernel<<<(int)std::min<int64_t>((nw + 255) / 256, 64), 256, 0, s>>>(mlp_w1, 0, nw, w2max);
         const int NT2 = din_mlp2_nt(h2);
         const int KS2 = (h1 + DIN_E - 1) / DIN_E;
         const int gp = (int)std::min<int64_t>(((int64_t)KS2 * NT2 * 64 + 255) / 256, 512);
