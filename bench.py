@@ -352,14 +352,14 @@ def run_itemcf(args, device):
     # median of 5 end-to-end runs: once, a single slow run moved the 3-run
     # mean of the similarity from 2.3 to 7.6 ms
     reps = 5
-    ts, tr = [], []
+    sim_s, rec_s = [], []
     for _ in range(reps):
         t0 = time.perf_counter()
         t1, oi, ocnt = one()
         t2 = time.perf_counter()
-        ts.append(t1 - t0)
-        tr.append(t2 - t1)
-    t_sim, t_rec = float(np.median(ts)), float(np.median(tr))
+        sim_s.append(t1 - t0)
+        rec_s.append(t2 - t1)
+    t_sim, t_rec = float(np.median(sim_s)), float(np.median(rec_s))
     recalled = int(ocnt.sum())
     out = {"unit": "ordered pairs/s (similarity), recalled pairs/s (recall)",
            "users": len(users), "items": len(ids), "ordered_pairs": n_pairs,
